@@ -1,0 +1,372 @@
+/*
+ * vcfc_oracle.c -- TEST INFRASTRUCTURE ONLY (the parity oracle).
+ *
+ * A plain-C, single-threaded CPU restatement of theferrit32/vcf-compression's
+ * `.vcfc` codec, written from the reference's behaviour (not copied):
+ *
+ *   vcfo_encode_line   <- compress_data_line      src/compress.cpp:5-203
+ *   vcfo_compress      <- compress                src/compress.cpp:205-257
+ *   vcfo_decompress    <- decompress2_fd          src/compress.cpp:1214-1257
+ *                         + decompress2_metadata_headers_fd :1108-1211
+ *                         + decompress2_data_line            :741-986
+ *   vcfo_sparse_offset <- SparsificationConfiguration::compute_sparse_offset
+ *                                                 src/sparse.cpp:18-51
+ *   vcfo_sparsify      <- sparsify_file           src/sparse.cpp:290-580
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+ * load this file's library, and only as the checker -- never as the thing that
+ * is measured or shipped.  The product path (vcf-compression_amd/) never links
+ * it.
+ *
+ * Parity pinning: tests/test_oracle.py checks this restatement against the
+ * golden vectors in tests/golden/ (produced by the compiled reference,
+ * oracle/_ref/main, and by other/random_vcf.py run in the build container --
+ * see tests/golden/make_golden.py).
+ */
+#define _GNU_SOURCE
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <stdio.h>
+#include <fcntl.h>
+#include <unistd.h>
+#include <sys/stat.h>
+
+#include "vcfc_oracle.h"
+
+/* Flag bytes: src/utils.hpp:44-56 */
+#define M_00  0x00u
+#define M_01  0xA0u
+#define M_10  0xC0u
+#define M_11  0x80u
+#define M_ESC 0xE0u
+#define CAP_00 127u /* src/compress.cpp:126 */
+#define CAP_XX 31u  /* src/compress.cpp:127 */
+
+typedef struct { const uint8_t *p; size_t n; } span_t;
+
+/* Field tokenisation = split_string(line, "\t") (src/utils.cpp:82-112):
+ * maximal runs of non-TAB bytes; empty terms are dropped (:95). */
+static size_t next_field(const uint8_t *s, size_t len, size_t pos, span_t *f) {
+    while (pos < len && s[pos] == '\t') pos++;
+    size_t b = pos;
+    while (pos < len && s[pos] != '\t') pos++;
+    f->p = s + b;
+    f->n = pos - b;
+    return pos;
+}
+
+static int gt_class(span_t t) {
+    if (t.n != 3 || t.p[1] != '|') return 4;
+    if (t.p[0] == '0' && t.p[2] == '0') return 0;
+    if (t.p[0] == '0' && t.p[2] == '1') return 1;
+    if (t.p[0] == '1' && t.p[2] == '0') return 2;
+    if (t.p[0] == '1' && t.p[2] == '1') return 3;
+    return 4;
+}
+
+static const uint8_t class_mask[4] = {M_00, M_01, M_10, M_11};
+
+static void put_be30(uint8_t *o, uint32_t v) {
+    /* compress.cpp:97-100 / :196-199: 32-bit big endian, top two bits forced 1 */
+    o[0] = (uint8_t)(((v >> 24) & 0xFF) | 0xC0);
+    o[1] = (uint8_t)((v >> 16) & 0xFF);
+    o[2] = (uint8_t)((v >> 8) & 0xFF);
+    o[3] = (uint8_t)(v & 0xFF);
+}
+
+#define EMIT(b) do { if (o >= cap) return VCFO_E_NOSPACE; out[o++] = (uint8_t)(b); } while (0)
+
+int vcfo_encode_line(const uint8_t *line, size_t len, int add_newline,
+                     uint8_t *out, size_t cap, size_t *out_len) {
+    span_t f[9];
+    size_t pos = 0, nf = 0;
+    size_t o = 0;
+    /* first nine non-empty fields (8 required + FORMAT) */
+    while (nf < 9) {
+        span_t t;
+        pos = next_field(line, len, pos, &t);
+        if (t.n == 0) break;
+        f[nf++] = t;
+    }
+    if (nf < 8) return VCFO_E_LT8COLS;           /* compress.cpp:9-11 */
+    /* is there at least one sample token? */
+    span_t first;
+    size_t gpos = next_field(line, len, pos, &first);
+    int has_samples = (nf == 9) && first.n > 0;
+    if (nf == 8) return VCFO_E_8COLS;           /* size_t underflow -> abort, compress.cpp:89,107 */
+
+    if (cap < 8) return VCFO_E_NOSPACE;
+    o = 8;
+    uint32_t req = 0;
+    for (size_t k = 0; k < 9; k++) {
+        if (k) { EMIT('\t'); req++; }
+        for (size_t j = 0; j < f[k].n; j++) EMIT(f[k].p[j]);
+        req += (uint32_t)f[k].n;
+    }
+    if (has_samples) { EMIT('\t'); req++; }      /* compress.cpp:90-93 */
+
+    if (has_samples) {
+        /* genotype run-length coder, compress.cpp:124-186 */
+        span_t cur = first;
+        size_t cpos = gpos;
+        while (cur.n > 0) {
+            int c = gt_class(cur);
+            span_t nxt;
+            size_t npos = next_field(line, len, cpos, &nxt);
+            if (c == 4) {
+                EMIT(M_ESC | 1);
+                for (size_t j = 0; j < cur.n; j++) EMIT(cur.p[j]);
+                if (nxt.n > 0) EMIT('\t');      /* not the last sample, :182-184 */
+                cur = nxt; cpos = npos;
+                continue;
+            }
+            uint32_t capc = c == 0 ? CAP_00 : CAP_XX;
+            uint32_t count = 1;
+            while (count < capc && nxt.n > 0 && gt_class(nxt) == c) {
+                count++;
+                cpos = npos;
+                npos = next_field(line, len, cpos, &nxt);
+            }
+            EMIT(class_mask[c] | count);
+            cur = nxt; cpos = npos;
+        }
+    }
+    if (add_newline) EMIT('\n');
+    put_be30(out + 4, req);
+    put_be30(out, (uint32_t)(o - 4));            /* compress.cpp:194 */
+    *out_len = o;
+    return VCFO_OK;
+}
+
+size_t vcfo_encode_bound(size_t line_len) {
+    /* header 8 + prefix <= len + 1 + GT escapes: each token of n bytes costs at
+     * most n + 2 output bytes and tokens are >=1 tab apart. */
+    return 8 + line_len + (line_len + 1) / 2 + 8;
+}
+
+/* compress(), src/compress.cpp:205-257, over an in-memory file.
+ * getline() semantics: '\n'-terminated lines, a final unterminated line is
+ * still a line; empty lines are skipped; "##" lines and "#" lines pass through
+ * with a '\n' appended. */
+int vcfo_compress(const uint8_t *in, size_t n, uint8_t *out, size_t cap,
+                  size_t *out_len, int64_t *err_line) {
+    size_t ip = 0, o = 0;
+    int64_t lineno = 0;
+    while (ip < n) {
+        const uint8_t *nl = memchr(in + ip, '\n', n - ip);
+        size_t e = nl ? (size_t)(nl - in) : n;
+        const uint8_t *line = in + ip;
+        size_t len = e - ip;
+        ip = nl ? e + 1 : n;
+        lineno++;
+        if (len == 0) continue;
+        if (line[0] == '#') {
+            if (!(len >= 2 && line[1] == '#')) {
+                /* header line: split and require >= 8 terms (:230-234) */
+                size_t p = 0, cnt = 0;
+                span_t t;
+                for (;;) { p = next_field(line, len, p, &t); if (!t.n) break; cnt++; }
+                if (cnt < 8) { if (err_line) *err_line = lineno; *out_len = o; return VCFO_E_HEADER; }
+            }
+            if (o + len + 1 > cap) return VCFO_E_NOSPACE;
+            memcpy(out + o, line, len); o += len; out[o++] = '\n';
+            continue;
+        }
+        size_t rl = 0;
+        int st = vcfo_encode_line(line, len, 1, out + o, cap - o, &rl);
+        if (st != VCFO_OK) { if (err_line) *err_line = lineno; *out_len = o; return st; }
+        o += rl;
+    }
+    *out_len = o;
+    return VCFO_OK;
+}
+
+/* ------------------------------------------------------------------ */
+/* Decoder: decompress2_fd (src/compress.cpp:1214-1257).               */
+
+static const char GTS[4][3] = {{'0','|','0'},{'0','|','1'},{'1','|','0'},{'1','|','1'}};
+
+#define DEMIT(b) do { if (o >= cap) return VCFO_E_NOSPACE; out[o++] = (uint8_t)(b); } while (0)
+
+int vcfo_decompress(const uint8_t *in, size_t n, uint8_t *out, size_t cap, size_t *out_len) {
+    size_t ip = 0, o = 0;
+    int got_meta = 0, got_header = 0;
+    uint64_t sample_count = 0;
+    uint8_t c1 = 0;
+    *out_len = 0;
+    /* decompress2_metadata_headers_fd :1108-1211 */
+    for (;;) {
+        if (ip < n) c1 = in[ip++];
+        else if (!got_header || !got_meta) return VCFO_E_FORMAT; /* "File ended before a header or metadata line" */
+        /* at EOF with both seen, c1 keeps its previous value ('#'): the
+         * reference then throws "Read a metadata or header row after already
+         * reading a header" (:1138-1150) */
+        if (c1 != '#') {
+            if (!got_meta || !got_header) return VCFO_E_FORMAT;
+            ip--;
+            break;
+        } else if (got_header) {
+            return VCFO_E_FORMAT;
+        }
+        if (ip >= n) return VCFO_E_FORMAT;
+        uint8_t c2 = in[ip++];
+        if (c2 == '#') got_meta = 1;
+        else { if (!got_meta) return VCFO_E_FORMAT; got_header = 1; }
+        DEMIT(c1); DEMIT(c2);
+        size_t tabs = 0;
+        for (;;) {
+            if (ip >= n) return VCFO_E_FORMAT;
+            uint8_t c3 = in[ip++];
+            if (c3 == '\n') { DEMIT(c3); break; }
+            if (got_header && c3 == '\t') { tabs++; if (tabs > 8) sample_count++; }
+            DEMIT(c3);
+        }
+    }
+    /* data lines: decompress2_data_line :741-986 */
+    for (;;) {
+        if (n - ip < 8) break;                     /* 0 or partial header: stop (:768-774) */
+        const uint8_t *h = in + ip;
+        if ((h[0] >> 6) != 3 || (h[4] >> 6) != 3) return VCFO_E_FORMAT; /* utils.hpp:200-206 */
+        uint32_t req = ((uint32_t)(h[4] & 0x3F) << 24) | ((uint32_t)h[5] << 16) | ((uint32_t)h[6] << 8) | h[7];
+        ip += 8;
+        if (req == 0 || n - ip < req) return VCFO_E_FORMAT;
+        size_t tabs = 0;
+        /* linebuf.append(buf): C string, stops at the first NUL (:798) */
+        int nul = 0;
+        for (uint32_t i = 0; i < req; i++) {
+            uint8_t b = in[ip + i];
+            if (b == '\t') tabs++;
+            if (b == 0) nul = 1;
+            if (!nul) DEMIT(b);
+        }
+        ip += req;
+        if (tabs != 9 && !(tabs == 8 && sample_count == 0)) return VCFO_E_FORMAT;
+        uint64_t got = 0;
+        while (got < sample_count) {
+            if (ip >= n) return VCFO_E_FORMAT;
+            uint8_t b = in[ip++];
+            if ((b & 0x80) == 0) {
+                uint32_t cnt = b & 0x7F;
+                for (uint32_t k = 0; k < cnt; k++) { DEMIT('0'); DEMIT('|'); DEMIT('0'); DEMIT('\t'); }
+                got += cnt;
+                if (got >= sample_count) o--;     /* pop_back the trailing tab (:864-867) */
+            } else if ((b & 0xE0) == 0xE0) {
+                uint32_t ucount = b & 0x1F, u = 0;
+                while (u < ucount) {
+                    if (ip >= n) return VCFO_E_FORMAT;
+                    uint8_t x = in[ip++];
+                    if (x == '\n') {
+                        u++; got++;
+                        if (u != ucount) return VCFO_E_FORMAT;
+                        ip--;                     /* fseek(-1): re-read as the line end */
+                    } else if (x == '\t') {
+                        u++; got++;
+                        if (got < sample_count) DEMIT('\t');
+                    } else {
+                        DEMIT(x);
+                    }
+                }
+            } else {
+                uint32_t m = b & 0xE0, cnt = b & 0x1F;
+                int c = m == M_01 ? 1 : m == M_10 ? 2 : 3;
+                while (cnt--) {
+                    DEMIT(GTS[c][0]); DEMIT(GTS[c][1]); DEMIT(GTS[c][2]);
+                    got++;
+                    if (got < sample_count) DEMIT('\t');
+                }
+            }
+        }
+        if (ip >= n) return VCFO_E_FORMAT;
+        if (in[ip++] != '\n') return VCFO_E_FORMAT;
+        DEMIT('\n');
+    }
+    *out_len = o;
+    return VCFO_OK;
+}
+
+/* ------------------------------------------------------------------ */
+/* Sparse layout (src/sparse.cpp).                                      */
+
+uint64_t vcfo_sparse_offset(uint64_t pos) {
+    /* VCFC_SPARSE_MULTIPLE_REF_PER_FILE == false (src/sparse.hpp:15): the
+     * reference name is ignored; L = 3e8, F = 4, B = 4096 (sparse.hpp:29-32) */
+    return (300000000ull + pos) * (4ull * 4096ull);
+}
+
+static void be64(uint8_t *o, uint64_t v) {
+    for (int i = 0; i < 8; i++) o[i] = (uint8_t)(v >> (56 - 8 * i));
+}
+
+/* sparsify_file (src/sparse.cpp:290-580): writes the sparse file with one
+ * pwrite per record (same final bytes as the reference's per-byte writes). */
+int vcfo_sparsify(const uint8_t *in, size_t n, const char *out_path) {
+    int fd = open(out_path, O_CREAT | O_TRUNC | O_RDWR, 0600);
+    if (fd < 0) return VCFO_E_IO;
+    size_t ip = 0;
+    int got_meta = 0, got_header = 0;
+    /* header lines (decompress2_metadata_headers, compress.cpp:995-1100) */
+    for (;;) {
+        if (ip >= n) { if (!got_header || !got_meta) { close(fd); return VCFO_E_FORMAT; } close(fd); return VCFO_E_FORMAT; }
+        uint8_t c1 = in[ip];
+        if (c1 != '#') { if (!got_meta || !got_header) { close(fd); return VCFO_E_FORMAT; } break; }
+        if (got_header) { close(fd); return VCFO_E_FORMAT; }
+        if (ip + 1 >= n) { close(fd); return VCFO_E_FORMAT; }
+        uint8_t c2 = in[ip + 1];
+        if (c2 == '#') got_meta = 1; else { if (!got_meta) { close(fd); return VCFO_E_FORMAT; } got_header = 1; }
+        const uint8_t *nl = memchr(in + ip + 2, '\n', n - ip - 2);
+        if (!nl) { close(fd); return VCFO_E_FORMAT; }
+        size_t e = (size_t)(nl - in) + 1;
+        if (write(fd, in + ip, e - ip) != (ssize_t)(e - ip)) { close(fd); return VCFO_E_IO; }
+        ip = e;
+    }
+    uint8_t zero8[8] = {0};
+    if (write(fd, zero8, 8) != 8) { close(fd); return VCFO_E_IO; }
+    uint64_t data_start = (uint64_t)lseek(fd, 0, SEEK_CUR);
+    uint64_t prev = data_start;
+    int first = 1;
+    uint8_t *rec = NULL; size_t reccap = 0;
+    while (n - ip >= 8) {
+        const uint8_t *h = in + ip;
+        if ((h[0] >> 6) != 3 || (h[4] >> 6) != 3) { free(rec); close(fd); return VCFO_E_FORMAT; }
+        uint32_t L = ((uint32_t)(h[0] & 0x3F) << 24) | ((uint32_t)h[1] << 16) | ((uint32_t)h[2] << 8) | h[3];
+        if (L < 4 || n - ip - 8 < (size_t)L - 4) { free(rec); close(fd); return VCFO_E_FORMAT; }
+        size_t body = L - 4;
+        size_t rl = 16 + 8 + body;
+        if (rl > reccap) { reccap = rl * 2; rec = realloc(rec, reccap); }
+        memset(rec, 0, 16);
+        memcpy(rec + 16, h, 8);
+        memcpy(rec + 24, h + 8, body);
+        /* CHROM, POS: first two tab-terminated fields of the body (:431-471) */
+        size_t p = 0;
+        while (p < body && h[8 + p] != '\t') p++;
+        if (p == 0 || p >= body) { free(rec); close(fd); return VCFO_E_FORMAT; }
+        size_t ps = ++p;
+        uint64_t pos = 0;
+        while (p < body && h[8 + p] != '\t') {
+            uint8_t d = h[8 + p];
+            if (d < '0' || d > '9') { free(rec); close(fd); return VCFO_E_FORMAT; }
+            pos = pos * 10 + (d - '0');
+            p++;
+        }
+        if (p == ps || p >= body) { free(rec); close(fd); return VCFO_E_FORMAT; }
+        uint64_t voff = vcfo_sparse_offset(pos);
+        uint64_t foff = voff + data_start;
+        be64(rec, foff - prev);                       /* dist_to_prev (:479-488) */
+        if (first) {
+            /* host byte order (little endian) at data_start-8 (:495-511) */
+            if (pwrite(fd, &voff, 8, (off_t)(data_start - 8)) != 8) { free(rec); close(fd); return VCFO_E_IO; }
+            first = 0;
+        } else {
+            uint8_t d[8]; be64(d, foff - prev);       /* previous record's dist_to_next (:529-553) */
+            if (pwrite(fd, d, 8, (off_t)(prev + 8)) != 8) { free(rec); close(fd); return VCFO_E_IO; }
+        }
+        if (pwrite(fd, rec, rl, (off_t)foff) != (ssize_t)rl) { free(rec); close(fd); return VCFO_E_IO; }
+        prev = foff;
+        ip += 8 + body;
+    }
+    free(rec);
+    close(fd);
+    /* a trailing partial header is "Failed to read line length headers" (:365-368) */
+    return ip == n ? VCFO_OK : VCFO_E_FORMAT;
+}

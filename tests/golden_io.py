@@ -1,0 +1,79 @@
+"""Helpers to load the committed golden vectors and the oracle library
+(test infrastructure only)."""
+import ctypes
+import gzip
+import json
+import os
+import subprocess
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(REPO, "tests", "golden")
+ORACLE_SO = os.path.join(REPO, "oracle", "_build", "liboracle.so")
+
+
+def manifest():
+    with open(os.path.join(GOLDEN, "manifest.json")) as f:
+        return json.load(f)
+
+
+def edge_cases():
+    with open(os.path.join(GOLDEN, "edge_cases.json")) as f:
+        return json.load(f)
+
+
+def gz(name):
+    with gzip.open(os.path.join(GOLDEN, name), "rb") as f:
+        return f.read()
+
+
+_oracle = None
+
+
+def oracle():
+    """ctypes handle to the C restatement (built by `make -C oracle`)."""
+    global _oracle
+    if _oracle is None:
+        if not os.path.exists(ORACLE_SO):
+            subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle"),
+                            os.path.join(REPO, "oracle", "_build", "liboracle.so")], check=True)
+        lib = ctypes.CDLL(ORACLE_SO)
+        u8p, szp = ctypes.c_char_p, ctypes.POINTER(ctypes.c_size_t)
+        lib.vcfo_encode_line.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, szp]
+        lib.vcfo_compress.argtypes = [u8p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, szp,
+                                      ctypes.POINTER(ctypes.c_int64)]
+        lib.vcfo_decompress.argtypes = [u8p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, szp]
+        lib.vcfo_sparsify.argtypes = [u8p, ctypes.c_size_t, ctypes.c_char_p]
+        lib.vcfo_sparse_offset.restype = ctypes.c_uint64
+        lib.vcfo_sparse_offset.argtypes = [ctypes.c_uint64]
+        lib.vcfo_encode_bound.restype = ctypes.c_size_t
+        lib.vcfo_encode_bound.argtypes = [ctypes.c_size_t]
+        _oracle = lib
+    return _oracle
+
+
+def oracle_encode_line(line, add_newline=True):
+    lib = oracle()
+    cap = lib.vcfo_encode_bound(len(line))
+    buf = ctypes.create_string_buffer(cap)
+    n = ctypes.c_size_t(0)
+    st = lib.vcfo_encode_line(line, len(line), int(add_newline), buf, cap, ctypes.byref(n))
+    return st, buf.raw[:n.value]
+
+
+def oracle_compress(data):
+    lib = oracle()
+    cap = len(data) * 2 + 1024
+    buf = ctypes.create_string_buffer(cap)
+    n = ctypes.c_size_t(0)
+    err = ctypes.c_int64(0)
+    st = lib.vcfo_compress(data, len(data), buf, cap, ctypes.byref(n), ctypes.byref(err))
+    return st, buf.raw[:n.value], err.value
+
+
+def oracle_decompress(data, cap=None):
+    lib = oracle()
+    cap = cap or len(data) * 8 + 1024
+    buf = ctypes.create_string_buffer(cap)
+    n = ctypes.c_size_t(0)
+    st = lib.vcfo_decompress(data, len(data), buf, cap, ctypes.byref(n))
+    return st, buf.raw[:n.value]
