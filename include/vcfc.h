@@ -1,0 +1,138 @@
+/*
+ * vcfc.h -- C ABI of the MI355X-native `.vcfc` genotype-line codec
+ * (libvcfc.so).  Plain pointers and sizes only; no C++ or torch types.
+ *
+ * Drop-in boundary.  The reference has no FFI: its only boundary for this
+ * path is the C++ function
+ *     int compress_data_line(const std::string& line,
+ *                            const VcfCompressionSchema& schema,
+ *                            std::vector<byte_t>& byte_vec, bool add_newline);
+ * (reference src/compress.hpp:20-23, defined src/compress.cpp:5-203) whose
+ * single caller is compress() (src/compress.cpp:205-257, call at :244).
+ * vcfc_compress_data_line() is its one-line replacement; the batch entry
+ * points below replace the compress() loop around it.  INTEGRATION.md shows
+ * the shim a maintainer adds on the reference side.
+ *
+ * Output is byte-identical to the reference for every input line: records
+ * [LEN][REQ][cols][GT][\n] concatenated in row order (format: reference
+ * src/utils.hpp:44-56,140-247, src/compress.cpp:32-199).
+ */
+#ifndef VCFC_H
+#define VCFC_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes -------------------------------------------------------- */
+#define VCFC_OK 0
+/* VcfValidationError("VCF data line did not contain at least 8 terms"),
+ * reference src/compress.cpp:9-11 */
+#define VCFC_E_LT8COLS 1
+/* exactly 8 terms: the reference's size_t underflow -> std::length_error ->
+ * abort (src/compress.cpp:89,107); reported instead of aborting */
+#define VCFC_E_8COLS 2
+/* VcfValidationError("VCF Header did not have enough columns"),
+ * src/compress.cpp:231-234 */
+#define VCFC_E_HEADER 3
+#define VCFC_E_NOSPACE 4   /* caller buffer too small */
+#define VCFC_E_ARG 5       /* bad argument */
+#define VCFC_E_HIP 6       /* HIP runtime error / no GPU */
+#define VCFC_E_IO 7        /* file open/read/write failed */
+#define VCFC_E_FORMAT 8    /* malformed .vcfc input (decoder) */
+
+const char *vcfc_version(void);
+const char *vcfc_strerror(int status);
+
+/* ---- context ----------------------------------------------------------------
+ * One context per GPU (device ordinal); not shared across host threads.
+ * Fails with VCFC_E_HIP when no GPU is visible: there is no CPU fallback. */
+typedef struct vcfc_ctx vcfc_ctx;
+int vcfc_ctx_create(int device, vcfc_ctx **out);
+void vcfc_ctx_destroy(vcfc_ctx *ctx);
+
+/* ---- one line: replaces compress_data_line (src/compress.hpp:20-23) --------
+ * Appends the record for `line` (no trailing '\n'; `len` bytes) to `out`
+ * (capacity `out_cap`), writes its size to *out_len.  add_newline as in the
+ * reference (compress() always passes true).  Returns VCFC_OK or an error;
+ * nothing is written on error. */
+int vcfc_compress_data_line(vcfc_ctx *ctx, const char *line, uint64_t len, int add_newline,
+                            uint8_t *out, uint64_t out_cap, uint64_t *out_len);
+
+/* ---- batches of lines ------------------------------------------------------
+ * Upper bound of the encoded size of rows whose line bytes sum to
+ * total_line_bytes (records only). */
+uint64_t vcfc_encode_bound(uint64_t n_rows, uint64_t total_line_bytes);
+
+/* Device workspace bytes needed by vcfc_encode_rows_device. */
+uint64_t vcfc_encode_workspace_size(uint64_t n_rows, uint64_t total_line_bytes);
+
+/* Device-resident batch encode, asynchronous on `stream` (a hipStream_t; 0 =
+ * the default stream).  All pointers are device pointers.
+ *   d_buf            data-line bytes
+ *   d_line_off/len   line i = d_buf[d_line_off[i] .. + d_line_len[i]) (no '\n')
+ *   d_out            records in row order; d_rec_off[0..n] exclusive offsets
+ *                    (d_rec_off[n] = total bytes)
+ *   d_ws             workspace of vcfc_encode_workspace_size(n, total) bytes
+ *                    where total >= sum of d_line_len
+ *   d_err            one uint64: ~0 = success, else (row << 8 | status) of the
+ *                    first failing row (rows before it are valid output)
+ * Returns VCFC_OK if the work was enqueued. Capturable in a hipGraph. */
+int vcfc_encode_rows_device(const uint8_t *d_buf, const uint64_t *d_line_off,
+                            const uint32_t *d_line_len, uint64_t n, uint64_t total_line_bytes,
+                            uint8_t *d_out, uint64_t out_cap, uint64_t *d_rec_off,
+                            void *d_ws, uint64_t ws_bytes, uint64_t *d_err, void *stream);
+
+/* Per-stage timing of vcfc_encode_rows_device (HIP events on the same
+ * stream).  vcfc_timer_read synchronises and returns the per-stage totals in
+ * ms summed over the timed calls since the last read:
+ *   ms[0] slot-offset scan, ms[1] k_encode, ms[2] record-offset scan,
+ *   ms[3] k_compact;  *calls = number of timed calls. */
+typedef struct vcfc_timer vcfc_timer;
+int vcfc_timer_create(vcfc_timer **t);
+void vcfc_timer_destroy(vcfc_timer *t);
+int vcfc_encode_rows_device_timed(const uint8_t *d_buf, const uint64_t *d_line_off,
+                                  const uint32_t *d_line_len, uint64_t n, uint64_t total_line_bytes,
+                                  uint8_t *d_out, uint64_t out_cap, uint64_t *d_rec_off,
+                                  void *d_ws, uint64_t ws_bytes, uint64_t *d_err, void *stream,
+                                  vcfc_timer *t);
+int vcfc_timer_read(vcfc_timer *t, double ms[4], uint64_t *calls);
+
+/* Host batch encode (synchronous: H2D, encode on the context's GPU, D2H).
+ * rec_off has n + 1 entries.  On a failing row, returns its status and
+ * *err_row = its index; records of the rows before it are in `out`. */
+int vcfc_encode_rows(vcfc_ctx *ctx, const uint8_t *buf, uint64_t buf_bytes,
+                     const uint64_t *line_off, const uint32_t *line_len, uint64_t n,
+                     uint8_t *out, uint64_t out_cap, uint64_t *rec_off, int64_t *err_row);
+
+/* ---- whole files: compress() / decompress2_fd() ---------------------------
+ * compress: header ("##" and "#") lines pass through with '\n', empty lines
+ * are skipped, data lines are encoded on the GPU (reference
+ * src/compress.cpp:205-257).  On error returns the status and *err_line =
+ * 1-based input line number. */
+int vcfc_compress_file(vcfc_ctx *ctx, const char *in_path, const char *out_path, int64_t *err_line);
+/* In-memory variant of vcfc_compress_file (out_cap >= vcfc_compress_bound). */
+uint64_t vcfc_compress_bound(uint64_t in_bytes);
+int vcfc_compress_buffer(vcfc_ctx *ctx, const uint8_t *in, uint64_t n, uint8_t *out, uint64_t out_cap,
+                         uint64_t *out_len, int64_t *err_line);
+
+/* ---- device-side helpers used by the benchmark ---------------------------
+ * Synthetic genotype rows generated in HBM (no host round trip).  `law`:
+ *   0 = random_vcf law (alleles i.i.d. 0/1/2 with p .90/.08/.02,
+ *       reference other/random_vcf.py:66-70)
+ *   1 = chr22-shaped (per-row alt-allele frequency from d_row_af; ~1% of
+ *       rows multi-allelic)
+ * The prefix (9 columns + '\t') of row i is copied from
+ * d_prefix[d_prefix_off[i] .. d_prefix_off[i+1]); row i is written at
+ * d_buf + d_line_off[i] with S tokens and a trailing '\n'. */
+int vcfc_synth_rows_device(uint8_t *d_buf, const uint64_t *d_line_off, uint64_t n,
+                           const uint8_t *d_prefix, const uint64_t *d_prefix_off,
+                           const float *d_row_af, uint32_t samples, int law, uint64_t seed,
+                           void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,57 @@
+"""TEST INFRASTRUCTURE ONLY: ctypes binding of the fiber-emulated build of the
+product kernels (tests/simt_emu) + helpers to index VCF data lines."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EMU_SO = os.path.join(REPO, "tests", "simt_emu", "_build", "libvcfc_emu.so")
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        subprocess.run(["make", "-s", "-C", os.path.join(REPO, "tests", "simt_emu")], check=True)
+        L = ctypes.CDLL(EMU_SO)
+        vp = ctypes.c_void_p
+        L.emu_encode_rows.argtypes = [vp, vp, vp, ctypes.c_uint64, vp, ctypes.c_uint64, vp,
+                                      ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+        _lib = L
+    return _lib
+
+
+def data_lines(vcf):
+    """(buf, line_off, line_len) of the data lines of a VCF buffer, following
+    compress()'s getline loop (reference src/compress.cpp:218-253): empty
+    lines and '#' lines are not data lines."""
+    offs, lens = [], []
+    p, n = 0, len(vcf)
+    while p < n:
+        e = vcf.find(b"\n", p)
+        e = n if e < 0 else e
+        if e > p and vcf[p] != 0x23:
+            offs.append(p)
+            lens.append(e - p)
+        p = e + 1
+    return vcf, np.array(offs, dtype=np.uint64), np.array(lens, dtype=np.uint32)
+
+
+def emu_encode(buf, line_off, line_len):
+    """Run the product encode pipeline on the emulator.
+    Returns (status, records bytes, rec_off array, err_word)."""
+    n = len(line_off)
+    cap = int(sum(int(x) * 3 // 2 + 32 for x in line_len)) + 64
+    out = np.zeros(cap, dtype=np.uint8)
+    rec_off = np.zeros(n + 1, dtype=np.uint64)
+    src = np.frombuffer(buf, dtype=np.uint8).copy()
+    lo = np.ascontiguousarray(line_off, dtype=np.uint64)
+    ll = np.ascontiguousarray(line_len, dtype=np.uint32)
+    err = ctypes.c_uint64(0)
+    sw = ctypes.c_uint64(0)
+    st = lib().emu_encode_rows(src.ctypes.data, lo.ctypes.data, ll.ctypes.data, n, out.ctypes.data, cap,
+                               rec_off.ctypes.data, ctypes.byref(err), ctypes.byref(sw))
+    total = int(rec_off[n]) if n else 0
+    return st, out[:total].tobytes(), rec_off, err.value

@@ -1,0 +1,34 @@
+// TEST INFRASTRUCTURE ONLY: C entry point that runs the product encode
+// pipeline (vcfc_encode_device from csrc/vcfc_encode.hip) on the fiber
+// emulator, with host memory standing in for HBM.
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+#include "vcfc_device.h"
+#include "emu.h"
+
+extern "C" int emu_encode_rows(const uint8_t *buf, const uint64_t *line_off, const uint32_t *line_len,
+                               uint64_t n, uint8_t *out, uint64_t out_cap, uint64_t *rec_off,
+                               uint64_t *err_word, uint64_t *switches) {
+    uint64_t total = 0;
+    for (uint64_t i = 0; i < n; i++) total += line_len[i];
+    VcfcWorkspaceLayout L = vcfc_encode_workspace_layout(n, total);
+    uint8_t *ws = (uint8_t *)aligned_alloc(256, (L.total + 255) & ~255ull);
+    memset(ws, 0xCD, L.total);  // poison: stale workspace must not leak into results
+    VcfcEncodeArgs a;
+    a.buf = buf; a.line_off = line_off; a.line_len = line_len; a.n = n;
+    a.out = out; a.out_cap = out_cap; a.rec_off = rec_off;
+    a.slot_off = (uint64_t *)(ws + L.slot_off);
+    a.rec_size = (uint32_t *)(ws + L.rec_size);
+    a.partials = (uint64_t *)(ws + L.partials);
+    a.err = (uint64_t *)(ws + L.err);
+    a.slots = ws + L.slots;
+    a.slots_cap = L.total - L.slots;
+    emu::g.switches = 0;
+    int st = (int)vcfc_encode_device(a, nullptr);
+    *err_word = *a.err;
+    if (switches) *switches = emu::g.switches;
+    free(ws);
+    return st;
+}

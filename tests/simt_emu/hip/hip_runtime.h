@@ -1,0 +1,50 @@
+// TEST INFRASTRUCTURE ONLY: minimal <hip/hip_runtime.h> stand-in so the
+// product kernel sources compile with g++ against the fiber SIMT emulator.
+#pragma once
+#include <cstdint>
+#include <cstring>
+#include <cstddef>
+#include "../emu.h"
+
+#define __global__
+#define __device__
+#define __host__
+#define __forceinline__ inline
+#define __launch_bounds__(...)
+#define __shared__ static
+#define __restrict__
+
+struct dim3 {
+    unsigned x, y, z;
+    dim3(unsigned a = 1, unsigned b = 1, unsigned c = 1) : x(a), y(b), z(c) {}
+};
+struct uint4 { uint32_t x, y, z, w; };
+struct uint2 { uint32_t x, y; };
+inline uint4 make_uint4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) { return uint4{a, b, c, d}; }
+
+#define threadIdx (emu::g.cur->tid)
+#define blockIdx (emu::g.bid)
+#define blockDim (emu::g.block)
+#define gridDim (emu::g.grid)
+
+typedef void *hipStream_t;
+typedef void *hipEvent_t;
+inline int hipEventRecord(hipEvent_t, hipStream_t) { return 0; }
+typedef int hipError_t;
+#define hipSuccess 0
+inline hipError_t hipGetLastError() { return hipSuccess; }
+inline const char *hipGetErrorString(hipError_t) { return "emu"; }
+inline hipError_t hipMemsetAsync(void *p, int v, size_t n, hipStream_t) { memset(p, v, n); return hipSuccess; }
+inline hipError_t hipMemcpyAsync(void *d, const void *s, size_t n, int, hipStream_t) { memmove(d, s, n); return hipSuccess; }
+#define hipMemcpyDeviceToDevice 3
+
+inline void __syncthreads() { emu::collective(emu::OP_SYNCTHREADS, 0, 0, 0); }
+
+template <class T> inline T atomicAdd(T *p, T v) { T o = *p; *p = o + v; return o; }
+template <class T> inline T atomicMin(T *p, T v) { T o = *p; if (v < o) *p = v; return o; }
+template <class T> inline T atomicMax(T *p, T v) { T o = *p; if (v > o) *p = v; return o; }
+template <class T> inline T atomicOr(T *p, T v) { T o = *p; *p = o | v; return o; }
+
+inline emu::dim3v emu_dim(dim3 d) { emu::dim3v r; r.x = d.x; r.y = d.y; r.z = d.z; return r; }
+#define hipLaunchKernelGGL(K, G, B, SHM, STREAM, ...) \
+    emu::launch(emu_dim(dim3(G)), emu_dim(dim3(B)), [=]() { K(__VA_ARGS__); })

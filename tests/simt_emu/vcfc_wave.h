@@ -1,0 +1,45 @@
+// TEST INFRASTRUCTURE ONLY: emulated twin of
+// vcf-compression_amd/csrc/vcfc_wave.h (same API, fiber-emulated wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace vw {
+inline uint32_t lane_id() { return emu::lane(); }
+inline uint64_t ballot(bool p) { return emu::collective(emu::OP_BALLOT, p ? 1 : 0, 0, 0); }
+inline uint64_t lanemask_lt() { uint32_t l = lane_id(); return l == 0 ? 0ull : (~0ull >> (64 - l)); }
+inline uint32_t shfl(uint32_t v, uint32_t src) { return (uint32_t)emu::collective(emu::OP_SHFL, v, src & 63, 0); }
+inline uint32_t readlane(uint32_t v, uint32_t l) { return shfl(v, l); }
+inline uint32_t readfirst(uint32_t v) { return (uint32_t)emu::collective(emu::OP_READFIRST, v, 0, 0); }
+inline uint32_t dpp(uint32_t old, uint32_t src, int ctrl, int rm, int bm, bool bc) {
+    uint64_t c = (uint64_t)ctrl | ((uint64_t)rm << 16) | ((uint64_t)bm << 20) | ((uint64_t)(bc ? 1 : 0) << 24);
+    return (uint32_t)emu::collective(emu::OP_DPP, old, src, c);
+}
+inline uint32_t shr1(uint32_t v, uint32_t fill) { return dpp(fill, v, 0x138, 0xf, 0xf, false); }
+inline uint32_t shl1(uint32_t v, uint32_t fill) { return dpp(fill, v, 0x130, 0xf, 0xf, false); }
+inline uint32_t scan_add(uint32_t v) {
+    v += dpp(0u, v, 0x111, 0xf, 0xf, false);
+    v += dpp(0u, v, 0x112, 0xf, 0xf, false);
+    v += dpp(0u, v, 0x114, 0xf, 0xf, false);
+    v += dpp(0u, v, 0x118, 0xf, 0xf, false);
+    v += dpp(0u, v, 0x142, 0xa, 0xf, false);
+    v += dpp(0u, v, 0x143, 0xc, 0xf, false);
+    return v;
+}
+inline uint32_t umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
+inline uint32_t scan_max(uint32_t v) {
+    v = umax(v, dpp(0u, v, 0x111, 0xf, 0xf, false));
+    v = umax(v, dpp(0u, v, 0x112, 0xf, 0xf, false));
+    v = umax(v, dpp(0u, v, 0x114, 0xf, 0xf, false));
+    v = umax(v, dpp(0u, v, 0x118, 0xf, 0xf, false));
+    v = umax(v, dpp(0u, v, 0x142, 0xa, 0xf, false));
+    v = umax(v, dpp(0u, v, 0x143, 0xc, 0xf, false));
+    return v;
+}
+inline uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t s) {
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * (s & 3)));
+}
+inline void wave_sync() { emu::collective(emu::OP_WAVESYNC, 0, 0, 0); }
+inline int popc64(uint64_t m) { return __builtin_popcountll(m); }
+inline int hibit64(uint64_t m) { return 63 - __builtin_clzll(m); }
+}  // namespace vw

@@ -1,0 +1,154 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference's golden
+vectors and the oracle.  Needs a gfx950 GPU (-m gpu)."""
+import hashlib
+import io
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+import pytest
+
+import golden_io as G
+
+pytestmark = pytest.mark.gpu
+REPO = G.REPO
+sys.path.insert(0, os.path.join(REPO, "vcf-compression_amd"))
+
+
+def sha(b):
+    return hashlib.sha256(b).hexdigest()
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as T   # import before libvcfc: one HIP runtime in the process
+    assert T.cuda.is_available(), "GPU tests need a GPU"
+    return T
+
+
+@pytest.fixture(scope="module")
+def vcfc(torch):
+    import vcfc as V
+    return V
+
+
+@pytest.fixture(scope="module")
+def ctx(vcfc):
+    c = vcfc.Context(0)
+    yield c
+    c.close()
+
+
+def test_edge_cases_known_answers(ctx, vcfc):
+    for case in G.edge_cases()["cases"]:
+        line = bytes.fromhex(case["line"])
+        if "record" in case:
+            assert ctx.compress_data_line(line).hex() == case["record"], case["name"]
+        elif case["error"] == "length_error":
+            with pytest.raises(vcfc.LengthError):
+                ctx.compress_data_line(line)
+        else:
+            with pytest.raises(vcfc.VcfValidationError):
+                ctx.compress_data_line(line)
+
+
+def test_compress_data_line_without_newline(ctx):
+    line = bytes.fromhex(G.edge_cases()["cases"][0]["line"])
+    st, want = G.oracle_encode_line(line, add_newline=False)
+    assert st == 0 and ctx.compress_data_line(line, add_newline=False) == want
+
+
+def test_edge_file_and_bad_header(ctx, vcfc):
+    ec = G.edge_cases()
+    assert ctx.compress_buffer(bytes.fromhex(ec["file"]["input"])).hex() == ec["file"]["output"]
+    with pytest.raises(vcfc.VcfValidationError):
+        ctx.compress_buffer(bytes.fromhex(ec["bad_header_file"]["input"]))
+
+
+def test_config1_random_100x10000(ctx):
+    m = G.manifest()["random_100x10000"]
+    out = ctx.compress_buffer(G.gz("random_100x10000.vcf.gz"))
+    assert sha(out) == m["vcfc_sha256"]
+
+
+def test_fuzz_corpus(ctx):
+    assert ctx.compress_buffer(G.gz("fuzz_encode.vcf.gz")) == G.gz("fuzz_encode.vcfc.gz")
+
+
+def test_random_2504x4000_sha256(ctx):
+    import random_vcf
+    m = G.manifest()["random_2504x4000"]
+    buf = io.BytesIO()
+    random_vcf.generate(2504, 4000, buf)
+    vcf = buf.getvalue()
+    assert sha(vcf) == m["vcf_sha256"]
+    assert sha(ctx.compress_buffer(vcf)) == m["vcfc_sha256"]
+
+
+def test_cli_compress_matches_reference_bytes():
+    with tempfile.TemporaryDirectory() as d:
+        src = os.path.join(d, "t.vcf")
+        with open(src, "wb") as f:
+            f.write(G.gz("random_100x10000.vcf.gz"))
+        r = subprocess.run([os.path.join(REPO, "build", "main"), "compress", src, src + ".vcfc"],
+                           capture_output=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        assert sha(open(src + ".vcfc", "rb").read()) == G.manifest()["random_100x10000"]["vcfc_sha256"]
+
+
+def _device_encode(torch, vcfc, rows):
+    n = rows.n
+    ws_bytes = vcfc.workspace_size(n, rows.line_bytes)
+    cap = vcfc.encode_bound(n, rows.line_bytes)
+    dev = rows.buf.device
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    out = torch.empty(cap, dtype=torch.uint8, device=dev)
+    rec = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    err = torch.empty(1, dtype=torch.int64, device=dev)
+    vcfc.encode_rows_device(rows.buf.data_ptr(), rows.line_off.data_ptr(), rows.line_len.data_ptr(), n,
+                            rows.line_bytes, out.data_ptr(), cap, rec.data_ptr(), ws.data_ptr(), ws_bytes,
+                            err.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    return out, rec.cpu().numpy().astype(np.uint64), int(err.cpu().numpy().view(np.uint64)[0])
+
+
+@pytest.mark.parametrize("law,samples,n", [(0, 2504, 3000), (1, 2504, 3000), (0, 100, 20000), (1, 5003, 700)])
+def test_synthetic_rows_all_vs_oracle(torch, vcfc, law, samples, n):
+    import workload
+    rows = workload.DeviceRows(torch, vcfc, n, samples, law, seed=7 + law, device="cuda:0")
+    out, rec, err = _device_encode(torch, vcfc, rows)
+    assert err == vcfc.NO_ERROR
+    host = out[:int(rec[n])].cpu().numpy().tobytes()
+    lines = rows.host_lines(range(n))
+    for i, ln in enumerate(lines):
+        st, want = G.oracle_encode_line(ln)
+        assert st == 0
+        assert host[int(rec[i]):int(rec[i + 1])] == want, i
+
+
+def test_config2_full_size_sampled(torch, vcfc):
+    """2504 x 1M chr22-shaped rows: sampled rows byte-exact vs the oracle, and
+    the record offsets consistent with every record's own LEN header."""
+    import workload
+    n = 1_000_000
+    rows = workload.DeviceRows(torch, vcfc, n, 2504, 1, seed=11, device="cuda:0")
+    out, rec, err = _device_encode(torch, vcfc, rows)
+    assert err == vcfc.NO_ERROR
+    sizes = np.diff(rec)
+    # LEN header of every record == size - 4 (checked on device)
+    rt = torch.from_numpy(rec[:-1].astype(np.int64)).cuda()
+    hdr = torch.stack([out[rt + k].to(torch.int64) for k in range(4)], 1)
+    L = ((hdr[:, 0] & 0x3F) << 24) | (hdr[:, 1] << 16) | (hdr[:, 2] << 8) | hdr[:, 3]
+    assert bool(((hdr[:, 0] & 0xC0) == 0xC0).all())
+    assert bool((L.cpu().numpy() == sizes.astype(np.int64) - 4).all())
+    last = out[rt + torch.from_numpy(sizes.astype(np.int64)).cuda() - 1]
+    assert bool((last == 10).all())
+    rng = np.random.default_rng(5)
+    pick = np.unique(np.concatenate([rng.integers(0, n, 400), [0, n - 1]]))
+    lines = rows.host_lines(pick)
+    for i, ln in zip(pick, lines):
+        st, want = G.oracle_encode_line(ln)
+        got = out[int(rec[i]):int(rec[i + 1])].cpu().numpy().tobytes()
+        assert got == want, i

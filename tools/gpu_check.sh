@@ -1,0 +1,26 @@
+#!/bin/bash
+# GPU-box driver for one round trip: smoke -> GPU parity tests -> bench ->
+# rocprofv3 kernel trace.  Every GPU step has its own time limit; the chain
+# stops at the first failure.  Usage: tools/gpu_check.sh <tag> [steps...]
+set -o pipefail
+R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+TAG="${1:-r}"; shift
+STEPS="${*:-smoke tests bench prof}"
+O="$R/gpurun_out/$TAG"
+mkdir -p "$O"
+cd "$R" || exit 1
+echo "box: $(hostname) $(date)" > "$O/info.txt"
+rocm-smi --showproductname >> "$O/info.txt" 2>&1 || true
+for s in $STEPS; do
+  echo "== $s $(date +%T)" | tee -a "$O/progress.txt"
+  case $s in
+    smoke) timeout -k 10 420 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 || { echo "smoke failed rc=$?"; tail -30 "$O/smoke.log"; exit 1; } ;;
+    tests) timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > "$O/pytest_gpu.log" 2>&1 || { echo "tests failed rc=$?"; tail -40 "$O/pytest_gpu.log"; exit 1; } ;;
+    bench) timeout -k 10 600 python bench.py > "$O/bench.json" 2> "$O/bench.err" || { echo "bench failed rc=$?"; tail -30 "$O/bench.err"; exit 1; } ; cat "$O/bench.json" ;;
+    bench0) timeout -k 10 600 python bench.py --law 0 --no-cpu-baseline > "$O/bench_law0.json" 2> "$O/bench_law0.err" || { echo "bench0 failed"; tail -30 "$O/bench_law0.err"; exit 1; } ; cat "$O/bench_law0.json" ;;
+    prof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof" -o run -- python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu-baseline > "$O/prof.log" 2>&1) || { echo "prof failed rc=$?"; tail -30 "$O/prof.log"; exit 1; } ;;
+    pmc) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$O/pmc_fetch" -o run -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$O/pmc_fetch.log" 2>&1 && timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$O/pmc_write" -o run -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$O/pmc_write.log" 2>&1) || { echo "pmc failed rc=$?"; tail -30 "$O/pmc_fetch.log" "$O/pmc_write.log"; exit 1; } ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo "all ok $(date +%T)"

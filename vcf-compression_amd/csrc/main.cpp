@@ -1,0 +1,60 @@
+// main.cpp -- CLI with the reference's argv contract (src/main.cpp:4028-4185)
+// for the encode path: `main compress <in.vcf> <out.vcfc>`.  Data lines are
+// encoded on the GPU through libvcfc.so.  Error messages mirror the
+// reference's exceptions (which terminate the reference process).
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <sys/stat.h>
+
+#include "vcfc.h"
+
+static int usage() {
+    fprintf(stderr, "./main [compress|decompress|sparsify] <input_file> <output_file>\n");
+    return 1;
+}
+
+static bool file_exists(const char *p) {
+    struct stat s;
+    return stat(p, &s) == 0;
+}
+
+int main(int argc, char **argv) {
+    if (argc < 2) return usage();
+    std::string action(argv[1]);
+    if (action == "compress") {
+        if (argc < 4) return usage();
+        if (!file_exists(argv[2])) printf("Input file does not exist: %s\n", argv[2]);
+        if (std::string(argv[2]) == argv[3]) {
+            fprintf(stderr, "terminate called after throwing an instance of 'std::runtime_error'\n"
+                            "  what():  input and output file are the same\n");
+            return 134;
+        }
+        vcfc_ctx *ctx = nullptr;
+        int st = vcfc_ctx_create(0, &ctx);
+        if (st != VCFC_OK) {
+            fprintf(stderr, "vcfc: %s\n", vcfc_strerror(st));
+            return 1;
+        }
+        int64_t err_line = -1;
+        st = vcfc_compress_file(ctx, argv[2], argv[3], &err_line);
+        vcfc_ctx_destroy(ctx);
+        if (st == VCFC_E_LT8COLS || st == VCFC_E_HEADER) {
+            fprintf(stderr, "terminate called after throwing an instance of 'VcfValidationError'\n"
+                            "  what():  %s (input line %lld)\n", vcfc_strerror(st), (long long)err_line);
+            return 134;
+        }
+        if (st == VCFC_E_8COLS) {
+            fprintf(stderr, "terminate called after throwing an instance of 'std::length_error'\n"
+                            "  what():  vector::_M_default_append (input line %lld)\n", (long long)err_line);
+            return 134;
+        }
+        if (st != VCFC_OK) {
+            fprintf(stderr, "Error in compression of file: %s\n", vcfc_strerror(st));
+            return 1;
+        }
+        return 0;
+    }
+    std::printf("Unknown action name: %s\n", action.c_str());
+    return 0;
+}

@@ -1,0 +1,413 @@
+// vcfc_api.cpp -- the C ABI (include/vcfc.h): contexts, device buffers and
+// the host-side drivers that mirror the reference's compress() loop
+// (src/compress.cpp:205-257) around the GPU encoder.
+#include <hip/hip_runtime.h>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "vcfc.h"
+#include "vcfc_device.h"
+
+hipError_t vcfc_synth_device(uint8_t *buf, const uint64_t *line_off, uint64_t n, const uint8_t *prefix,
+                             const uint64_t *prefix_off, const float *row_af, uint32_t S, int law,
+                             uint64_t seed, hipStream_t s);
+
+namespace {
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap && p) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(bytes, 1 << 20);
+        want = want + want / 8;
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+// Rows per device batch is bounded by bytes so a multi-GB file streams
+// through a fixed device footprint.
+constexpr uint64_t BATCH_BYTES = 1ull << 30;
+
+}  // namespace
+
+struct vcfc_timer {
+    std::vector<hipEvent_t> ev;   // 5 per timed call
+    size_t used = 0;
+};
+
+struct vcfc_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    DevBuf in, off, len, out, rec, ws, err;
+};
+
+extern "C" {
+
+const char *vcfc_version(void) { return "vcfc-mi355x 0.1 (gfx950)"; }
+
+const char *vcfc_strerror(int s) {
+    switch (s) {
+    case VCFC_OK: return "ok";
+    case VCFC_E_LT8COLS: return "VCF data line did not contain at least 8 terms";
+    case VCFC_E_8COLS: return "VCF data line has exactly 8 terms (reference aborts: std::length_error)";
+    case VCFC_E_HEADER: return "VCF Header did not have enough columns";
+    case VCFC_E_NOSPACE: return "output buffer too small";
+    case VCFC_E_ARG: return "invalid argument";
+    case VCFC_E_HIP: return "HIP runtime error (is a gfx950 GPU visible?)";
+    case VCFC_E_IO: return "file I/O error";
+    case VCFC_E_FORMAT: return "malformed .vcfc input";
+    default: return "unknown status";
+    }
+}
+
+int vcfc_ctx_create(int device, vcfc_ctx **out) {
+    if (!out) return VCFC_E_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0 || device < 0 || device >= n) return VCFC_E_HIP;
+    if (hipSetDevice(device) != hipSuccess) return VCFC_E_HIP;
+    vcfc_ctx *c = new vcfc_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return VCFC_E_HIP;
+    }
+    *out = c;
+    return VCFC_OK;
+}
+
+void vcfc_ctx_destroy(vcfc_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    c->in.release(); c->off.release(); c->len.release(); c->out.release();
+    c->rec.release(); c->ws.release(); c->err.release();
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+uint64_t vcfc_encode_bound(uint64_t n_rows, uint64_t total_line_bytes) {
+    return total_line_bytes + total_line_bytes / 2 + 16 * n_rows + 16;
+}
+
+uint64_t vcfc_encode_workspace_size(uint64_t n_rows, uint64_t total_line_bytes) {
+    return vcfc_encode_workspace_layout(n_rows, total_line_bytes).total;
+}
+
+static int encode_rows_device_impl(const uint8_t *d_buf, const uint64_t *d_line_off, const uint32_t *d_line_len,
+                                   uint64_t n, uint64_t total_line_bytes, uint8_t *d_out, uint64_t out_cap,
+                                   uint64_t *d_rec_off, void *d_ws, uint64_t ws_bytes, uint64_t *d_err, void *stream,
+                                   hipEvent_t *ev) {
+    if ((n && (!d_buf || !d_line_off || !d_line_len || !d_out)) || !d_rec_off || !d_err || (n && !d_ws))
+        return VCFC_E_ARG;
+    const VcfcWorkspaceLayout L = vcfc_encode_workspace_layout(n, total_line_bytes);
+    if (ws_bytes < L.total) return VCFC_E_NOSPACE;
+    uint8_t *ws = static_cast<uint8_t *>(d_ws);
+    VcfcEncodeArgs a;
+    a.buf = d_buf;
+    a.line_off = d_line_off;
+    a.line_len = d_line_len;
+    a.n = n;
+    a.out = d_out;
+    a.out_cap = out_cap;
+    a.rec_off = d_rec_off;
+    a.slot_off = reinterpret_cast<uint64_t *>(ws + L.slot_off);
+    a.rec_size = reinterpret_cast<uint32_t *>(ws + L.rec_size);
+    a.partials = reinterpret_cast<uint64_t *>(ws + L.partials);
+    a.err = d_err;
+    a.slots = ws + L.slots;
+    a.slots_cap = L.total - L.slots;
+    return vcfc_encode_device(a, static_cast<hipStream_t>(stream), ev) == hipSuccess ? VCFC_OK : VCFC_E_HIP;
+}
+
+int vcfc_encode_rows_device(const uint8_t *d_buf, const uint64_t *d_line_off, const uint32_t *d_line_len,
+                            uint64_t n, uint64_t total_line_bytes, uint8_t *d_out, uint64_t out_cap,
+                            uint64_t *d_rec_off, void *d_ws, uint64_t ws_bytes, uint64_t *d_err, void *stream) {
+    return encode_rows_device_impl(d_buf, d_line_off, d_line_len, n, total_line_bytes, d_out, out_cap, d_rec_off,
+                                   d_ws, ws_bytes, d_err, stream, nullptr);
+}
+
+int vcfc_timer_create(vcfc_timer **t) {
+    if (!t) return VCFC_E_ARG;
+    *t = new vcfc_timer();
+    return VCFC_OK;
+}
+
+void vcfc_timer_destroy(vcfc_timer *t) {
+    if (!t) return;
+    for (auto &e : t->ev) (void)hipEventDestroy(e);
+    delete t;
+}
+
+int vcfc_encode_rows_device_timed(const uint8_t *d_buf, const uint64_t *d_line_off, const uint32_t *d_line_len,
+                                  uint64_t n, uint64_t total_line_bytes, uint8_t *d_out, uint64_t out_cap,
+                                  uint64_t *d_rec_off, void *d_ws, uint64_t ws_bytes, uint64_t *d_err, void *stream,
+                                  vcfc_timer *t) {
+    if (!t) return VCFC_E_ARG;
+    const size_t base = 5 * t->used;
+    while (t->ev.size() < base + 5) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return VCFC_E_HIP;
+        t->ev.push_back(e);
+    }
+    int st = encode_rows_device_impl(d_buf, d_line_off, d_line_len, n, total_line_bytes, d_out, out_cap, d_rec_off,
+                                     d_ws, ws_bytes, d_err, stream, t->ev.data() + base);
+    if (st == VCFC_OK) t->used++;
+    return st;
+}
+
+int vcfc_timer_read(vcfc_timer *t, double ms[4], uint64_t *calls) {
+    if (!t || !ms) return VCFC_E_ARG;
+    for (int k = 0; k < 4; k++) ms[k] = 0;
+    for (size_t i = 0; i < t->used; i++) {
+        hipEvent_t *e = t->ev.data() + 5 * i;
+        if (hipEventSynchronize(e[4]) != hipSuccess) return VCFC_E_HIP;
+        for (int k = 0; k < 4; k++) {
+            float f = 0;
+            if (hipEventElapsedTime(&f, e[k], e[k + 1]) != hipSuccess) return VCFC_E_HIP;
+            ms[k] += f;
+        }
+    }
+    if (calls) *calls = t->used;
+    t->used = 0;
+    return VCFC_OK;
+}
+
+int vcfc_synth_rows_device(uint8_t *d_buf, const uint64_t *d_line_off, uint64_t n, const uint8_t *d_prefix,
+                           const uint64_t *d_prefix_off, const float *d_row_af, uint32_t samples, int law,
+                           uint64_t seed, void *stream) {
+    if (n && (!d_buf || !d_line_off || !d_prefix || !d_prefix_off)) return VCFC_E_ARG;
+    return vcfc_synth_device(d_buf, d_line_off, n, d_prefix, d_prefix_off, d_row_af, samples, law, seed,
+                             static_cast<hipStream_t>(stream)) == hipSuccess
+               ? VCFC_OK
+               : VCFC_E_HIP;
+}
+
+// Host batch: copy in, encode, copy out.  Synchronous on the context stream.
+int vcfc_encode_rows(vcfc_ctx *c, const uint8_t *buf, uint64_t buf_bytes, const uint64_t *line_off,
+                     const uint32_t *line_len, uint64_t n, uint8_t *out, uint64_t out_cap, uint64_t *rec_off,
+                     int64_t *err_row) {
+    if (!c || !rec_off || (n && (!buf || !line_off || !line_len || !out))) return VCFC_E_ARG;
+    if (err_row) *err_row = -1;
+    if (hipSetDevice(c->device) != hipSuccess) return VCFC_E_HIP;
+    uint64_t total = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        if (line_off[i] + line_len[i] > buf_bytes) return VCFC_E_ARG;
+        total += line_len[i];
+    }
+    const uint64_t bound = vcfc_encode_bound(n, total);
+    const uint64_t wsz = vcfc_encode_workspace_size(n, total);
+    if (c->in.ensure(buf_bytes + 64) || c->off.ensure(8 * n + 8) || c->len.ensure(4 * n + 8) ||
+        c->out.ensure(bound) || c->rec.ensure(8 * (n + 1)) || c->ws.ensure(wsz) || c->err.ensure(8))
+        return VCFC_E_HIP;
+    hipStream_t s = c->stream;
+    if (hipMemcpyAsync(c->in.p, buf, buf_bytes, hipMemcpyHostToDevice, s) ||
+        hipMemcpyAsync(c->off.p, line_off, 8 * n, hipMemcpyHostToDevice, s) ||
+        hipMemcpyAsync(c->len.p, line_len, 4 * n, hipMemcpyHostToDevice, s))
+        return VCFC_E_HIP;
+    int st = vcfc_encode_rows_device(static_cast<uint8_t *>(c->in.p), static_cast<uint64_t *>(c->off.p),
+                                     static_cast<uint32_t *>(c->len.p), n, total, static_cast<uint8_t *>(c->out.p),
+                                     c->out.cap, static_cast<uint64_t *>(c->rec.p), c->ws.p, c->ws.cap,
+                                     static_cast<uint64_t *>(c->err.p), s);
+    if (st != VCFC_OK) return st;
+    uint64_t errw = 0;
+    if (hipMemcpyAsync(rec_off, c->rec.p, 8 * (n + 1), hipMemcpyDeviceToHost, s) ||
+        hipMemcpyAsync(&errw, c->err.p, 8, hipMemcpyDeviceToHost, s) || hipStreamSynchronize(s))
+        return VCFC_E_HIP;
+    uint64_t upto = n, status = VCFC_OK;
+    if (errw != VCFCD_NO_ERROR) {
+        upto = errw >> 8;
+        status = errw & 0xFF;
+        if (err_row) *err_row = (int64_t)upto;
+    }
+    const uint64_t bytes = rec_off[upto];
+    if (bytes > out_cap) return VCFC_E_NOSPACE;
+    if (bytes && (hipMemcpyAsync(out, c->out.p, bytes, hipMemcpyDeviceToHost, s) || hipStreamSynchronize(s)))
+        return VCFC_E_HIP;
+    return (int)status;
+}
+
+int vcfc_compress_data_line(vcfc_ctx *c, const char *line, uint64_t len, int add_newline, uint8_t *out,
+                            uint64_t out_cap, uint64_t *out_len) {
+    if (!c || !line || !out || !out_len || len > 0xFFFFFFFFull) return VCFC_E_ARG;
+    const uint64_t off = 0;
+    const uint32_t l32 = (uint32_t)len;
+    uint64_t ro[2] = {0, 0};
+    std::vector<uint8_t> tmp(vcfc_encode_bound(1, len) + 16);
+    int64_t er = -1;
+    int st = vcfc_encode_rows(c, reinterpret_cast<const uint8_t *>(line), len, &off, &l32, 1, tmp.data(),
+                              tmp.size(), ro, &er);
+    if (st != VCFC_OK) return st;
+    uint64_t n = ro[1];
+    if (!add_newline) n -= 1;  // records always end in '\n' (compress.cpp:188-190)
+    if (n > out_cap) return VCFC_E_NOSPACE;
+    if (!add_newline) {
+        // LEN counts the record without the newline
+        const uint32_t L = (uint32_t)(n - 4);
+        tmp[0] = (uint8_t)(((L >> 24) & 0xFF) | 0xC0);
+        tmp[1] = (uint8_t)((L >> 16) & 0xFF);
+        tmp[2] = (uint8_t)((L >> 8) & 0xFF);
+        tmp[3] = (uint8_t)(L & 0xFF);
+    }
+    memcpy(out, tmp.data(), n);
+    *out_len = n;
+    return VCFC_OK;
+}
+
+uint64_t vcfc_compress_bound(uint64_t in_bytes) { return in_bytes + in_bytes / 2 + 64; }
+
+// compress() over an in-memory file (reference src/compress.cpp:205-257).
+int vcfc_compress_buffer(vcfc_ctx *c, const uint8_t *in, uint64_t n, uint8_t *out, uint64_t out_cap,
+                         uint64_t *out_len, int64_t *err_line) {
+    if (!c || (!in && n) || !out || !out_len) return VCFC_E_ARG;
+    if (err_line) *err_line = -1;
+    *out_len = 0;
+    struct Pass { uint64_t before_data, off, len, lineno; };
+    std::vector<Pass> pass;           // non-data lines, with the data index they precede
+    std::vector<uint64_t> doff, dline;
+    std::vector<uint32_t> dlen;
+    int64_t hdr_err_line = -1;
+    uint64_t p = 0, lineno = 0;
+    while (p < n) {
+        const uint8_t *nl = static_cast<const uint8_t *>(memchr(in + p, '\n', n - p));
+        const uint64_t e = nl ? (uint64_t)(nl - in) : n;
+        const uint64_t len = e - p;
+        lineno++;
+        if (len > 0) {
+            if (in[p] == '#') {
+                if (!(len >= 2 && in[p + 1] == '#')) {
+                    // header line: >= 8 tab-separated non-empty terms (:230-234)
+                    uint64_t terms = 0, q = p;
+                    while (q < e) {
+                        while (q < e && in[q] == '\t') q++;
+                        if (q >= e) break;
+                        terms++;
+                        while (q < e && in[q] != '\t') q++;
+                    }
+                    if (terms < 8) { hdr_err_line = (int64_t)lineno; break; }
+                }
+                pass.push_back({doff.size(), p, len, lineno});
+            } else {
+                if (len > 0xFFFFFFFFull) return VCFC_E_ARG;
+                doff.push_back(p);
+                dlen.push_back((uint32_t)len);
+                dline.push_back(lineno);
+            }
+        }
+        p = nl ? e + 1 : n;
+    }
+    const uint64_t nd = doff.size();
+    uint64_t o = 0;
+    size_t pi = 0;
+    auto emit_pass_upto = [&](uint64_t d) -> int {
+        while (pi < pass.size() && pass[pi].before_data <= d) {
+            if (o + pass[pi].len + 1 > out_cap) return VCFC_E_NOSPACE;
+            memcpy(out + o, in + pass[pi].off, pass[pi].len);
+            o += pass[pi].len;
+            out[o++] = '\n';
+            pi++;
+        }
+        return VCFC_OK;
+    };
+    std::vector<uint64_t> rec;
+    std::vector<uint8_t> recbuf;
+    uint64_t d = 0;
+    while (d < nd) {
+        // batch [d, e): contiguous input span bounded by BATCH_BYTES
+        uint64_t e = d, bytes = 0;
+        while (e < nd && (e == d || bytes + dlen[e] + 1 <= BATCH_BYTES)) { bytes += dlen[e] + 1; e++; }
+        const uint64_t base = doff[d];
+        const uint64_t span = doff[e - 1] + dlen[e - 1] - base;
+        std::vector<uint64_t> lo(e - d);
+        for (uint64_t i = d; i < e; i++) lo[i - d] = doff[i] - base;
+        rec.assign(e - d + 1, 0);
+        recbuf.resize(vcfc_encode_bound(e - d, bytes) + 16);
+        int64_t er = -1;
+        int st = vcfc_encode_rows(c, in + base, span, lo.data(), dlen.data() + d, e - d, recbuf.data(), recbuf.size(),
+                                  rec.data(), &er);
+        const uint64_t good = st == VCFC_OK ? e - d : (er >= 0 ? (uint64_t)er : 0);
+        // interleave pass-through lines at their positions
+        uint64_t a = 0;
+        while (a < good) {
+            int s2 = emit_pass_upto(d + a);
+            if (s2) return s2;
+            uint64_t b = a + 1;
+            while (b < good && !(pi < pass.size() && pass[pi].before_data <= d + b)) b++;
+            const uint64_t nb = rec[b] - rec[a];
+            if (o + nb > out_cap) return VCFC_E_NOSPACE;
+            memcpy(out + o, recbuf.data() + rec[a], nb);
+            o += nb;
+            a = b;
+        }
+        if (st != VCFC_OK) {
+            const int64_t bad_line = er >= 0 ? (int64_t)dline[d + er] : -1;
+            if (hdr_err_line >= 0 && hdr_err_line < bad_line) break;  // header error comes first
+            int s2 = emit_pass_upto(d + good);
+            if (s2) return s2;
+            *out_len = o;
+            if (err_line) *err_line = bad_line;
+            return st;
+        }
+        d = e;
+    }
+    int s2 = emit_pass_upto(nd);
+    if (s2) return s2;
+    *out_len = o;
+    if (hdr_err_line >= 0) {
+        if (err_line) *err_line = hdr_err_line;
+        return VCFC_E_HEADER;
+    }
+    return VCFC_OK;
+}
+
+int vcfc_compress_file(vcfc_ctx *c, const char *in_path, const char *out_path, int64_t *err_line) {
+    if (!c || !in_path || !out_path) return VCFC_E_ARG;
+    int fd = open(in_path, O_RDONLY);
+    if (fd < 0) return VCFC_E_IO;
+    struct stat st;
+    if (fstat(fd, &st) != 0) { close(fd); return VCFC_E_IO; }
+    const uint64_t n = (uint64_t)st.st_size;
+    const uint8_t *in = nullptr;
+    if (n) {
+        void *m = mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fd, 0);
+        if (m == MAP_FAILED) { close(fd); return VCFC_E_IO; }
+        madvise(m, n, MADV_SEQUENTIAL);
+        in = static_cast<const uint8_t *>(m);
+    }
+    std::vector<uint8_t> out(vcfc_compress_bound(n));
+    uint64_t olen = 0;
+    int s = vcfc_compress_buffer(c, in, n, out.data(), out.size(), &olen, err_line);
+    if (n) munmap(const_cast<uint8_t *>(in), n);
+    close(fd);
+    int ofd = open(out_path, O_CREAT | O_TRUNC | O_WRONLY, 0644);
+    if (ofd < 0) return VCFC_E_IO;
+    uint64_t w = 0;
+    while (w < olen) {
+        ssize_t k = write(ofd, out.data() + w, std::min<uint64_t>(olen - w, 1ull << 30));
+        if (k <= 0) { close(ofd); return VCFC_E_IO; }
+        w += (uint64_t)k;
+    }
+    close(ofd);
+    return s;
+}
+
+}  // extern "C"

@@ -1,0 +1,62 @@
+// vcfc_synth.hip -- synthetic genotype rows generated directly in HBM for the
+// benchmark and the large parity cases (config 2/4 inputs do not fit on disk
+// comfortably; the reference's own generator other/random_vcf.py needs ~40 min
+// for 2504 x 1M in Python).  Not on the encode path.
+#include <hip/hip_runtime.h>
+#include <vcfc_wave.h>
+#include "vcfc_device.h"
+
+namespace {
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// allele from a 32-bit uniform
+__device__ __forceinline__ uint32_t allele(uint32_t u, int law, float af) {
+    if (law == 0) {
+        // p(0) = .90, p(1) = .08, p(2) = .02  (reference other/random_vcf.py:66-67)
+        return u < 3865470566u ? 0u : (u < 4209067950u ? 1u : 2u);
+    }
+    const float x = (float)(u >> 8) * (1.0f / 16777216.0f);
+    if (af <= 1.0f) return x < af ? 1u : 0u;
+    const float a1 = af - 1.0f;           // multi-allelic row: second ALT at 0.5 %
+    return x < a1 ? 1u : (x < a1 + 0.005f ? 2u : 0u);
+}
+
+// one wave per row: prefix copy + S tokens "a|b" separated by TABs + '\n'
+__global__ __launch_bounds__(256) void k_synth(uint8_t *buf, const uint64_t *line_off, uint64_t n,
+                                               const uint8_t *prefix, const uint64_t *prefix_off,
+                                               const float *row_af, uint32_t S, int law, uint64_t seed) {
+    const uint64_t row = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= n) return;
+    const uint32_t l = vw::lane_id();
+    uint8_t *dst = buf + line_off[row];
+    const uint64_t p0 = prefix_off[row], p1 = prefix_off[row + 1];
+    const uint32_t P = (uint32_t)(p1 - p0);
+    for (uint32_t i = l; i < P; i += 64) dst[i] = prefix[p0 + i];
+    uint8_t *g = dst + P;
+    const float af = row_af ? row_af[row] : 0.0f;
+    for (uint32_t j = l; j < S; j += 64) {
+        const uint64_t h = mix64(seed ^ mix64(row * 0x100000001B3ull + j));
+        const uint32_t a1 = allele((uint32_t)h, law, af), a2 = allele((uint32_t)(h >> 32), law, af);
+        g[4 * j + 0] = (uint8_t)('0' + a1);
+        g[4 * j + 1] = (uint8_t)'|';
+        g[4 * j + 2] = (uint8_t)('0' + a2);
+        g[4 * j + 3] = (uint8_t)(j + 1 == S ? '\n' : '\t');
+    }
+}
+
+}  // namespace
+
+hipError_t vcfc_synth_device(uint8_t *buf, const uint64_t *line_off, uint64_t n, const uint8_t *prefix,
+                             const uint64_t *prefix_off, const float *row_af, uint32_t S, int law,
+                             uint64_t seed, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_synth, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, buf, line_off, n, prefix,
+                       prefix_off, row_af, S, law, seed);
+    return hipGetLastError();
+}

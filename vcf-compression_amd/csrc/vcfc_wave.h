@@ -1,0 +1,78 @@
+// vcfc_wave.h -- wave64 primitives for the gfx950 kernels.
+//
+// Everything the kernels need from the CDNA4 wave: lane id, ballot, DPP
+// scans, cross-lane shifts, alignbyte.  Scans are built from DPP row_shr /
+// row_bcast so they cost VALU slots only (no LDS round trip).
+//
+// tests/simt_emu/ provides a drop-in header of the same name that emulates
+// these primitives on the CPU (64 fibers per wave) so the kernel source can be
+// exercised without a GPU; this file is the only implementation the product
+// library is built with.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace vw {
+
+__device__ __forceinline__ uint32_t lane_id() {
+    return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ uint64_t lanemask_lt() {
+    const uint32_t l = lane_id();
+    return l == 0 ? 0ull : (~0ull >> (64 - l));
+}
+__device__ __forceinline__ uint32_t readlane(uint32_t v, uint32_t l) {
+    return __builtin_amdgcn_readlane(v, l);
+}
+__device__ __forceinline__ uint32_t readfirst(uint32_t v) {
+    return __builtin_amdgcn_readfirstlane(v);
+}
+// lane i receives lane i-1's value; lane 0 receives `fill` (DPP wave_shr:1)
+__device__ __forceinline__ uint32_t shr1(uint32_t v, uint32_t fill) {
+    return __builtin_amdgcn_update_dpp(fill, v, 0x138, 0xf, 0xf, false);
+}
+// lane i receives lane i+1's value; lane 63 receives `fill` (DPP wave_shl:1)
+__device__ __forceinline__ uint32_t shl1(uint32_t v, uint32_t fill) {
+    return __builtin_amdgcn_update_dpp(fill, v, 0x130, 0xf, 0xf, false);
+}
+// generic lane gather (ds_bpermute)
+__device__ __forceinline__ uint32_t shfl(uint32_t v, uint32_t src) {
+    return __builtin_amdgcn_ds_bpermute(src << 2, v);
+}
+// inclusive add scan over the wave
+__device__ __forceinline__ uint32_t scan_add(uint32_t v) {
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false);
+    return v;
+}
+__device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
+// inclusive unsigned-max scan over the wave (identity 0)
+__device__ __forceinline__ uint32_t scan_max(uint32_t v) {
+    v = umax(v, __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false));
+    v = umax(v, __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false));
+    v = umax(v, __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false));
+    v = umax(v, __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false));
+    v = umax(v, __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false));
+    v = umax(v, __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false));
+    return v;
+}
+// ((hi:lo) >> 8*s)[31:0]
+__device__ __forceinline__ uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t s) {
+    return __builtin_amdgcn_alignbyte(hi, lo, s);
+}
+// order LDS traffic between the lanes of one wave (no s_barrier needed)
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ int popc64(uint64_t m) { return __popcll(m); }
+// index of the highest set bit (m != 0)
+__device__ __forceinline__ int hibit64(uint64_t m) { return 63 - __clzll(m); }
+
+}  // namespace vw

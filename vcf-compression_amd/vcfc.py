@@ -1,0 +1,209 @@
+"""Python binding (ctypes) of libvcfc.so -- the C ABI in include/vcfc.h.
+
+Mirrors the reference's operator interface for the encode path:
+  compress_data_line(line, add_newline=True)   (reference src/compress.hpp:20-23)
+  compress_file(in_path, out_path)             (reference src/compress.cpp:205-257)
+Errors raise VcfValidationError / RuntimeError like the reference's exceptions
+(src/utils.hpp:117-123, src/compress.cpp:9-11,231-234).
+
+There is no CPU fallback: without a visible gfx950 GPU, Context() raises.
+If PyTorch is used in the same process, import torch BEFORE loading this
+module so both share one HIP runtime (libvcfc.so binds to whatever
+libamdhip64.so is already loaded).
+"""
+import ctypes
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(ROOT, "build", "libvcfc.so")
+
+OK, E_LT8COLS, E_8COLS, E_HEADER, E_NOSPACE, E_ARG, E_HIP, E_IO, E_FORMAT = range(9)
+NO_ERROR = (1 << 64) - 1
+
+EXPORTS = [
+    "vcfc_version", "vcfc_strerror", "vcfc_ctx_create", "vcfc_ctx_destroy",
+    "vcfc_compress_data_line", "vcfc_encode_bound", "vcfc_encode_workspace_size",
+    "vcfc_encode_rows_device", "vcfc_encode_rows", "vcfc_compress_file",
+    "vcfc_compress_bound", "vcfc_compress_buffer", "vcfc_synth_rows_device",
+    "vcfc_timer_create", "vcfc_timer_destroy", "vcfc_encode_rows_device_timed", "vcfc_timer_read",
+]
+
+
+class VcfValidationError(RuntimeError):
+    """Same meaning as the reference's VcfValidationError (src/utils.hpp:117-123)."""
+
+
+class LengthError(RuntimeError):
+    """The reference aborts with std::length_error on 8-column data lines."""
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError("libvcfc.so not built: run `make -C vcf-compression_amd` (or __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u64, u32, i64 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int64
+    L.vcfc_version.restype = ctypes.c_char_p
+    L.vcfc_strerror.restype = ctypes.c_char_p
+    L.vcfc_strerror.argtypes = [ctypes.c_int]
+    L.vcfc_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
+    L.vcfc_ctx_destroy.argtypes = [vp]
+    L.vcfc_ctx_destroy.restype = None
+    L.vcfc_compress_data_line.argtypes = [vp, ctypes.c_char_p, u64, ctypes.c_int, vp, u64, ctypes.POINTER(u64)]
+    L.vcfc_encode_bound.restype = u64
+    L.vcfc_encode_bound.argtypes = [u64, u64]
+    L.vcfc_encode_workspace_size.restype = u64
+    L.vcfc_encode_workspace_size.argtypes = [u64, u64]
+    L.vcfc_encode_rows_device.argtypes = [vp, vp, vp, u64, u64, vp, u64, vp, vp, u64, vp, vp]
+    L.vcfc_encode_rows.argtypes = [vp, vp, u64, vp, vp, u64, vp, u64, vp, ctypes.POINTER(i64)]
+    L.vcfc_compress_file.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(i64)]
+    L.vcfc_compress_bound.restype = u64
+    L.vcfc_compress_bound.argtypes = [u64]
+    L.vcfc_compress_buffer.argtypes = [vp, vp, u64, vp, u64, ctypes.POINTER(u64), ctypes.POINTER(i64)]
+    L.vcfc_timer_create.argtypes = [ctypes.POINTER(vp)]
+    L.vcfc_timer_destroy.argtypes = [vp]
+    L.vcfc_timer_destroy.restype = None
+    L.vcfc_encode_rows_device_timed.argtypes = [vp, vp, vp, u64, u64, vp, u64, vp, vp, u64, vp, vp, vp]
+    L.vcfc_timer_read.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64)]
+    L.vcfc_synth_rows_device.argtypes = [vp, vp, u64, vp, vp, vp, u32, ctypes.c_int, u64, vp]
+    _lib = L
+    return L
+
+
+def strerror(st):
+    return lib().vcfc_strerror(st).decode()
+
+
+def raise_for(st, where=""):
+    if st == OK:
+        return
+    msg = strerror(st) + (" (%s)" % where if where else "")
+    if st in (E_LT8COLS, E_HEADER):
+        raise VcfValidationError(msg)
+    if st == E_8COLS:
+        raise LengthError(msg)
+    raise RuntimeError(msg)
+
+
+class Context:
+    """One GPU (device ordinal).  Raises if no GPU is visible."""
+
+    def __init__(self, device=0):
+        self._h = ctypes.c_void_p()
+        st = lib().vcfc_ctx_create(device, ctypes.byref(self._h))
+        if st != OK:
+            raise RuntimeError("vcfc: cannot create a GPU context: " + strerror(st))
+
+    def close(self):
+        if self._h:
+            lib().vcfc_ctx_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # -- reference interface ------------------------------------------------
+    def compress_data_line(self, line, add_newline=True):
+        """bytes line (no '\\n') -> record bytes, as compress_data_line."""
+        cap = lib().vcfc_encode_bound(1, len(line)) + 16
+        buf = ctypes.create_string_buffer(cap)
+        n = ctypes.c_uint64(0)
+        st = lib().vcfc_compress_data_line(self._h, line, len(line), int(add_newline), buf, cap, ctypes.byref(n))
+        raise_for(st)
+        return buf.raw[:n.value]
+
+    def compress_buffer(self, data):
+        """Whole VCF (bytes) -> .vcfc bytes, as compress()."""
+        cap = lib().vcfc_compress_bound(len(data))
+        out = np.empty(cap, dtype=np.uint8)
+        n = ctypes.c_uint64(0)
+        line = ctypes.c_int64(-1)
+        src = np.frombuffer(data, dtype=np.uint8)
+        st = lib().vcfc_compress_buffer(self._h, src.ctypes.data, len(data), out.ctypes.data, cap,
+                                        ctypes.byref(n), ctypes.byref(line))
+        raise_for(st, "line %d" % line.value)
+        return out[:n.value].tobytes()
+
+    def compress_file(self, in_path, out_path):
+        line = ctypes.c_int64(-1)
+        st = lib().vcfc_compress_file(self._h, in_path.encode(), out_path.encode(), ctypes.byref(line))
+        raise_for(st, "line %d" % line.value)
+
+    def encode_rows(self, buf, line_off, line_len):
+        """Host batch: returns (status, records bytes, rec_off, err_row)."""
+        n = len(line_off)
+        lo = np.ascontiguousarray(line_off, dtype=np.uint64)
+        ll = np.ascontiguousarray(line_len, dtype=np.uint32)
+        src = np.frombuffer(buf, dtype=np.uint8)
+        cap = lib().vcfc_encode_bound(n, int(ll.sum(dtype=np.uint64))) + 16
+        out = np.empty(cap, dtype=np.uint8)
+        rec = np.zeros(n + 1, dtype=np.uint64)
+        er = ctypes.c_int64(-1)
+        st = lib().vcfc_encode_rows(self._h, src.ctypes.data, len(buf), lo.ctypes.data, ll.ctypes.data, n,
+                                    out.ctypes.data, cap, rec.ctypes.data, ctypes.byref(er))
+        upto = n if st == OK else max(er.value, 0)
+        return st, out[:int(rec[upto])].tobytes(), rec, er.value
+
+
+# -- device-pointer API (used with torch tensors in bench.py / GPU tests) ----
+def workspace_size(n_rows, total_line_bytes):
+    return int(lib().vcfc_encode_workspace_size(n_rows, total_line_bytes))
+
+
+def encode_bound(n_rows, total_line_bytes):
+    return int(lib().vcfc_encode_bound(n_rows, total_line_bytes))
+
+
+def encode_rows_device(d_buf, d_line_off, d_line_len, n, total_line_bytes, d_out, out_cap, d_rec_off,
+                       d_ws, ws_bytes, d_err, stream=0):
+    st = lib().vcfc_encode_rows_device(d_buf, d_line_off, d_line_len, n, total_line_bytes, d_out, out_cap,
+                                       d_rec_off, d_ws, ws_bytes, d_err, stream)
+    raise_for(st)
+
+
+class StageTimer:
+    """Per-stage HIP-event timing of encode_rows_device (see vcfc_timer_read)."""
+    STAGES = ("slot_scan", "k_encode", "size_scan", "k_compact")
+
+    def __init__(self):
+        self._h = ctypes.c_void_p()
+        raise_for(lib().vcfc_timer_create(ctypes.byref(self._h)))
+
+    def encode(self, d_buf, d_line_off, d_line_len, n, total_line_bytes, d_out, out_cap, d_rec_off,
+               d_ws, ws_bytes, d_err, stream=0):
+        raise_for(lib().vcfc_encode_rows_device_timed(d_buf, d_line_off, d_line_len, n, total_line_bytes, d_out,
+                                                      out_cap, d_rec_off, d_ws, ws_bytes, d_err, stream, self._h))
+
+    def read(self):
+        ms = (ctypes.c_double * 4)()
+        calls = ctypes.c_uint64(0)
+        raise_for(lib().vcfc_timer_read(self._h, ms, ctypes.byref(calls)))
+        return dict(zip(self.STAGES, list(ms))), calls.value
+
+    def __del__(self):
+        try:
+            lib().vcfc_timer_destroy(self._h)
+        except Exception:
+            pass
+
+
+def synth_rows_device(d_buf, d_line_off, n, d_prefix, d_prefix_off, d_row_af, samples, law, seed, stream=0):
+    st = lib().vcfc_synth_rows_device(d_buf, d_line_off, n, d_prefix, d_prefix_off, d_row_af, samples,
+                                      law, seed, stream)
+    raise_for(st)

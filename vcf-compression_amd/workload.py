@@ -1,0 +1,103 @@
+"""Synthetic genotype workloads, generated in HBM (bench.py and the large GPU
+parity cases).
+
+law 0 "random_vcf": the reference generator's law (other/random_vcf.py:50-70):
+       CHROM 1, POS 10000+2i, ID var<i>, random REF, two other bases as ALT,
+       QUAL 100, FILTER PASS, INFO INFO, FORMAT GT; alleles i.i.d. 0/1/2 with
+       p = .90/.08/.02 (counter-based RNG instead of Python's Mersenne
+       Twister, so the bytes differ from the script's but the law is the same).
+law 1 "chr22": 1000 Genomes chr22-shaped rows (BASELINE configs[1]): CHROM 22,
+       POS from 16,050,075 with geometric gaps (mean 32), rsIDs, SNP REF/ALT,
+       INFO with AC/AF/AN/NS/DP and five population AFs (~170 B); per-variant
+       alt-allele count k ~ 1/k on [1, 5007] (neutral site-frequency
+       spectrum), so most rows are rare variants with long 0|0 runs; 1 % of
+       rows carry a second ALT (tokens with allele 2 -> escapes).
+
+The 9 leading columns are built on the host; the genotype columns (the
+dominant bytes) are generated on the GPU by vcfc_synth_rows_device.
+"""
+import numpy as np
+
+BASES = np.array(list("ATGC"))
+
+
+def prefixes(n, law, seed, row0=0):
+    """Return (prefix bytes blob, prefix_off[n+1] int64, row_af float32 or None)."""
+    rng = np.random.default_rng(seed)
+    ref = rng.integers(0, 4, n)
+    if law == 0:
+        alt1 = (ref + rng.integers(1, 4, n)) % 4
+        alt2 = (alt1 + 1) % 4
+        alt2 = np.where(alt2 == ref, (alt2 + 1) % 4, alt2)
+        rows = ["1\t%d\tvar%d\t%s\t%s,%s\t100\tPASS\tINFO\tGT\t" % (10000 + 2 * (row0 + i), row0 + i, BASES[r], BASES[a], BASES[b])
+                for i, (r, a, b) in enumerate(zip(ref.tolist(), alt1.tolist(), alt2.tolist()))]
+        af = None
+    else:
+        gaps = rng.geometric(1.0 / 32.0, n)
+        pos = 16050075 + row0 * 32 + np.cumsum(gaps) - gaps[0]
+        k = np.floor(np.exp(rng.random(n) * np.log(5008.0))).astype(np.int64)
+        k = np.clip(k, 1, 5007)
+        afv = k / 5008.0
+        alt = (ref + rng.integers(1, 4, n)) % 4
+        dp = rng.integers(10000, 30000, n)
+        pops = np.clip(afv[:, None] * rng.uniform(0.2, 1.8, (n, 5)), 0, 1)
+        multi = rng.random(n) < 0.01
+        rs = rng.integers(1, 800000000, n)
+        rows = []
+        for i in range(n):
+            p = pops[i]
+            rows.append("22\t%d\trs%d\t%s\t%s\t100\tPASS\tAC=%d;AF=%.4g;AN=5008;NS=2504;DP=%d;"
+                        "EAS_AF=%.4g;AMR_AF=%.4g;AFR_AF=%.4g;EUR_AF=%.4g;SAS_AF=%.4g;AA=.|||;VT=SNP\tGT\t"
+                        % (pos[i], rs[i], BASES[ref[i]], BASES[alt[i]], k[i], afv[i], dp[i],
+                           p[0], p[1], p[2], p[3], p[4]))
+        af = (afv + multi.astype(np.float64)).astype(np.float32)
+    blob = "".join(rows).encode()
+    plen = np.fromiter((len(r) for r in rows), dtype=np.int64, count=n)
+    poff = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(plen, out=poff[1:])
+    return blob, poff, af
+
+
+def layout(prefix_off, samples):
+    """Line offsets/lengths for rows = prefix + `samples` tokens, '\\n'-terminated."""
+    plen = np.diff(prefix_off)
+    line_len = (plen + 4 * samples - 1).astype(np.int64)
+    line_off = np.zeros(len(plen), dtype=np.int64)
+    np.cumsum(line_len[:-1] + 1, out=line_off[1:])
+    total = int(line_off[-1] + line_len[-1] + 1) if len(plen) else 0
+    return line_off, line_len.astype(np.int32), total
+
+
+class DeviceRows:
+    """A synthetic batch resident in HBM (torch tensors)."""
+
+    def __init__(self, torch, vcfc, n, samples, law, seed, device, row0=0):
+        blob, poff, af = prefixes(n, law, seed, row0)
+        line_off, line_len, total = layout(poff, samples)
+        dev = torch.device(device)
+        self.n, self.samples, self.law = n, samples, law
+        self.total_bytes = total
+        self.line_bytes = int(line_len.astype(np.int64).sum())
+        self.gt_bytes = 4 * samples * n   # bytes after the TAB following FORMAT, incl. '\n'
+        self.buf = torch.empty(total + 64, dtype=torch.uint8, device=dev)
+        self.line_off = torch.from_numpy(line_off).to(dev)
+        self.line_len = torch.from_numpy(line_len).to(dev)
+        d_prefix = torch.from_numpy(np.frombuffer(blob, dtype=np.uint8).copy()).to(dev)
+        d_poff = torch.from_numpy(poff).to(dev)
+        d_af = torch.from_numpy(af).to(dev) if af is not None else None
+        s = torch.cuda.current_stream(dev)
+        vcfc.synth_rows_device(self.buf.data_ptr(), self.line_off.data_ptr(), n, d_prefix.data_ptr(),
+                               d_poff.data_ptr(), d_af.data_ptr() if d_af is not None else None,
+                               samples, law, seed, s.cuda_stream)
+        torch.cuda.synchronize(dev)
+        del d_prefix, d_poff, d_af
+
+    def host_lines(self, rows):
+        """bytes of the given rows (for oracle checks)."""
+        lo = self.line_off.cpu().numpy()
+        ll = self.line_len.cpu().numpy()
+        out = []
+        for r in rows:
+            a = int(lo[r])
+            out.append(bytes(self.buf[a:a + int(ll[r])].cpu().numpy()))
+        return out
