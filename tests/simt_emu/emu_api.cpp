@@ -23,6 +23,8 @@ extern "C" int emu_encode_rows(const uint8_t *buf, const uint64_t *line_off, con
     a.rec_size = (uint32_t *)(ws + L.rec_size);
     a.partials = (uint64_t *)(ws + L.partials);
     a.err = (uint64_t *)(ws + L.err);
+    a.retry = (uint32_t *)(ws + L.retry);
+    a.retry_count = (uint32_t *)(ws + L.retry_count);
     a.slots = ws + L.slots;
     a.slots_cap = L.total - L.slots;
     emu::g.switches = 0;

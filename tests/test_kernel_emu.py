@@ -83,3 +83,31 @@ def test_wide_rows_multi_chunk(seed):
     st, out, ro, err = run(lines, lead=seed)
     want = b"".join(G.oracle_encode_line(x)[1] for x in lines)
     assert err == (1 << 64) - 1 and out == want
+
+
+def _chr22_like_rows(n, samples, seed):
+    rnd = random.Random(seed)
+    rows = []
+    for i in range(n):
+        af = rnd.choice([0.0, 0.0005, 0.002, 0.01, 0.05, 0.3, 0.9])
+        multi = rnd.random() < 0.1
+        toks = []
+        for _ in range(samples):
+            a = [1 if rnd.random() < af else 0 for _ in range(2)]
+            if multi and rnd.random() < 0.01:
+                a[rnd.randint(0, 1)] = 2
+            toks.append(b"%d|%d" % (a[0], a[1]))
+        pfx = b"22\t%d\trs%d\tA\tG\t100\tPASS\tAC=1;AF=%.4f;NS=2504\tGT\t" % (16050075 + 32 * i, i, af)
+        rows.append(pfx + b"\t".join(toks))
+    return rows
+
+
+@pytest.mark.parametrize("seed", [11, 12])
+def test_chr22_like_rows_skip_path(seed):
+    """Long 0|0 runs exercise the whole-chunk skip, 127-chunk boundaries that
+    straddle chunks, and run transitions at chunk starts."""
+    lines = _chr22_like_rows(40, 2504, seed)
+    st, out, ro, err = run(lines, lead=seed % 16)
+    assert err == (1 << 64) - 1
+    for i, ln in enumerate(lines):
+        assert out[int(ro[i]):int(ro[i + 1])] == G.oracle_encode_line(ln)[1], i

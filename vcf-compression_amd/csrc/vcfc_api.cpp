@@ -134,6 +134,8 @@ static int encode_rows_device_impl(const uint8_t *d_buf, const uint64_t *d_line_
     a.rec_size = reinterpret_cast<uint32_t *>(ws + L.rec_size);
     a.partials = reinterpret_cast<uint64_t *>(ws + L.partials);
     a.err = d_err;
+    a.retry = reinterpret_cast<uint32_t *>(ws + L.retry);
+    a.retry_count = reinterpret_cast<uint32_t *>(ws + L.retry_count);
     a.slots = ws + L.slots;
     a.slots_cap = L.total - L.slots;
     return vcfc_encode_device(a, static_cast<hipStream_t>(stream), ev) == hipSuccess ? VCFC_OK : VCFC_E_HIP;

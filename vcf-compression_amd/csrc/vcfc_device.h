@@ -29,12 +29,14 @@ struct VcfcEncodeArgs {
     uint32_t *rec_size;        // n
     uint64_t *partials;        // scan partials
     uint64_t *err;             // 1 word
+    uint32_t *retry;           // rows the fast kernel hands to the general one
+    uint32_t *retry_count;
     uint8_t *slots;            // per-row staging slots
     uint64_t slots_cap;
 };
 
 struct VcfcWorkspaceLayout {
-    uint64_t slot_off, rec_size, partials, err, slots, total;
+    uint64_t slot_off, rec_size, partials, err, retry, retry_count, slots, total;
 };
 
 // Bytes of per-row staging for a line of `len` bytes: covers the worst-case

@@ -4,8 +4,10 @@
 // of lines resident in HBM.  Pipeline (all on one stream, no host sync):
 //
 //   scan<BOUND>  slot_off[i] = sum_{k<i} slot_bytes(len_k)     (tiny)
-//   k_encode     one wave64 per row: tokenise, RLE-encode, stage the record
-//                in an LDS ring, stream it to the row's slot in 1 KiB bursts
+//   k_encode_fast     one wave64 per row: tokenise, RLE-encode, stage the
+//                     record in an LDS ring, stream it to the row's slot in
+//                     1 KiB bursts; rows of another shape are queued
+//   k_encode_general  persistent waves encode the queued rows (any shape)
 //   scan<IDENT>  rec_off[i] = sum_{k<i} rec_size_k             (tiny)
 //   k_compact    16 lanes per row: slot -> final offset, 16-byte stores
 //
@@ -73,20 +75,28 @@ __device__ __forceinline__ void ring_put(Ring &r, uint32_t pos, uint32_t b) {
     r.lds[pos & RMASK] = (uint8_t)b;
 }
 
-// Stream every complete 1 KiB burst (or, at the end, everything) to the slot.
-__device__ void ring_flush(Ring &r, bool final) {
+// Stream complete 1 KiB bursts to the slot.  A chunk adds < 1.3 KiB to a
+// ring holding < 1 KiB, so two unrolled bursts suffice (no loop: a store loop
+// of unknown trip count makes hipcc's vmcnt tracking give up on the prefetch).
+__device__ __forceinline__ void ring_burst(Ring &r, uint32_t l) {
+    const uint4 v = *reinterpret_cast<const uint4 *>(r.lds + ((r.fpos + 16u * l) & RMASK));
+    vw::gstore16(r.slot, r.fpos + 16u * l, v);
+    r.fpos += BURST;
+}
+__device__ __forceinline__ void ring_flush(Ring &r, bool final) {
     const uint32_t l = vw::lane_id();
+    r.wpos = vw::readfirst(r.wpos);
+    r.fpos = vw::readfirst(r.fpos);
     vw::wave_sync();
-    while (r.wpos - r.fpos >= BURST) {
-        const uint4 v = *reinterpret_cast<const uint4 *>(r.lds + ((r.fpos + 16u * l) & RMASK));
-        *reinterpret_cast<uint4 *>(r.slot + r.fpos + 16u * l) = v;
-        r.fpos += BURST;
+    if (r.wpos - r.fpos >= BURST) {
+        ring_burst(r, l);
+        if (r.wpos - r.fpos >= BURST) ring_burst(r, l);
     }
     if (final && r.wpos > r.fpos) {
         const uint32_t rem = r.wpos - r.fpos;  // < BURST
         if (16u * l < rem) {
             const uint4 v = *reinterpret_cast<const uint4 *>(r.lds + ((r.fpos + 16u * l) & RMASK));
-            *reinterpret_cast<uint4 *>(r.slot + r.fpos + 16u * l) = v;
+            vw::gstore16(r.slot, r.fpos + 16u * l, v);
         }
         r.fpos = r.wpos;
     }
@@ -111,208 +121,332 @@ __device__ void ring_finish(Ring &r, uint32_t req) {
 // ---------------------------------------------------------------------------
 // Fast path: clean prefix (no empty fields before the first sample) and a
 // genotype region of 3-byte tokens separated by single TABs -- the shape of
-// every GT-only VCF.  One wave streams the row in 1 KiB aligned chunks (lane l
-// owns bytes [16l, 16l+16) of a chunk), two chunks in flight.  Returns false
-// (nothing committed) if the row does not have that shape.
-__device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring &r,
-                            uint32_t *rec_bytes) {
+// every GT-only VCF.  One wave streams the row in 1 KiB aligned chunks: lane l
+// owns bytes [16l, 16l+16) of a chunk plus the next 4 bytes, so the 4 token
+// slots it classifies (slot j starts at 16l + 4j + phi) are complete in its
+// own registers.  Loads are unconditional (clamped inside the line) so two
+// chunks stay in flight behind counted vmcnt waits.  Returns false (nothing
+// committed) if the row does not have this shape.
+
+__device__ __forceinline__ uint32_t cls_mask_f(uint32_t c) { return (0x80C0A000u >> (8 * (c & 3u))) & 0xFFu; }
+// cap-1 (126 or 30) and the exact mod by cap for x < 2^24 (magic = ceil(2^32/cap))
+__device__ __forceinline__ uint32_t mod_cap(uint32_t x, bool is00) {
+    const uint32_t m = is00 ? 33818641u : 138547333u;
+    const uint32_t d = is00 ? 127u : 31u;
+    return x - vw::mulhi(x, m) * d;
+}
+// class of the token packed in the low 24 bits: 0..3 for 0|0 0|1 1|0 1|1, else ESC
+__device__ __forceinline__ uint32_t cls_f(uint32_t w) {
+    const bool gt = (w & 0xFEFFFEu) == 0x307C30u;
+    return gt ? (((w & 1u) << 1) | ((w >> 16) & 1u)) : CLS_ESC;
+}
+
+struct Chunk {
+    uint4 w;      // 16 bytes at A + 16*(chunk*64 + lane)
+    uint32_t y;   // the 4 bytes after them
+};
+
+__device__ __forceinline__ Chunk load_chunk(const uint8_t *A, uint32_t c, uint32_t l, uint32_t last_blk) {
+    uint32_t b = c * 64u + l;
+    b = b < last_blk ? b : last_blk;
+    Chunk k;
+    k.w = vw::gload16(A, b);
+    const uint32_t b2 = b + 1 < last_blk ? b + 1 : last_blk;
+    k.y = vw::gload4(A, 4u * b2);
+    return k;
+}
+
+struct FastState {
+    uint32_t nf;        // field starts seen so far (prefix phase)
+    uint32_t carryT;    // byte before this chunk is TAB / outside the line
+    int32_t gt0;        // line offset of the first sample token (-1: not found yet)
+    uint32_t T, phi;    // token count, gt0's byte phase mod 4
+    uint32_t pcls, prs; // class / run start(+1) of the previous token
+};
+
+// Prefix phase for chunk c: 0 = no sample yet, 1 = first sample starts in
+// this chunk (its tokens still to do), 2 = not the fast shape.
+__device__ __forceinline__ int fast_prefix_step(const Chunk &cur, uint32_t c, uint32_t lead, uint32_t len,
+                                                FastState &f, Ring &r) {
     const uint32_t l = vw::lane_id();
-    const uint4 *A = reinterpret_cast<const uint4 *>(reinterpret_cast<uintptr_t>(line) & ~uintptr_t(15));
+    const uint32_t bo = c * BURST + 16u * l;
+    const int32_t x0 = (int32_t)bo - (int32_t)lead;   // line offset of the lane's byte 0
+    uint32_t &nf = f.nf;
+    uint32_t &carryT = f.carryT;
+    // ---- prefix: locate the 10th field start, reject empty fields ----
+    const int32_t vlo = x0 >= 0 ? 0 : (-x0 >= 16 ? 16 : -x0);
+    const int32_t vhi0 = (int32_t)len - x0;
+    const int32_t vhi = vhi0 <= 0 ? 0 : (vhi0 >= 16 ? 16 : vhi0);
+    const uint32_t vm = vhi > vlo ? (((1u << vhi) - 1u) ^ ((1u << vlo) - 1u)) : 0u;
+    const uint32_t m = tab_mask16(cur.w) & vm;
+    const uint32_t Tm = (m | ~vm) & 0xFFFFu;
+    const uint32_t pin = vw::shr1((Tm >> 15) & 1u, carryT);
+    const uint32_t prevT = ((Tm << 1) | pin) & 0xFFFFu;
+    const uint32_t fs = ~Tm & prevT & 0xFFFFu;     // field starts
+    const uint32_t et = m & prevT;                 // TAB closing an empty field
+    carryT = vw::readlane((Tm >> 15) & 1u, 63);
+    const uint32_t cnt = (uint32_t)__builtin_popcount(fs);
+    const uint32_t inc = vw::scan_add(cnt);
+    const uint32_t exc = inc - cnt;
+    const bool has9 = nf + exc <= 9 && 9 < nf + inc;
+    uint32_t x9 = 0;
+    if (has9) {
+        uint32_t mm = fs;
+        for (uint32_t k = nf + exc; k < 9; k++) mm &= mm - 1;
+        x9 = (uint32_t)(x0 + __builtin_ctz(mm));
+    }
+    const uint64_t hb = vw::ballot(has9);
+    if (hb) x9 = vw::readlane(x9, (uint32_t)__builtin_ctzll(hb));
+    uint32_t below = 0xFFFFu;
+    if (hb) {
+        const int32_t d = (int32_t)x9 - x0;
+        below = d <= 0 ? 0u : d >= 16 ? 0xFFFFu : ((1u << d) - 1u);
+    }
+    if (vw::ballot((et & below) != 0)) return 2;
+    // prefix bytes -> ring[8 + x]: realign the lane's bytes to ring
+    // dwords (ring position of lane byte i is bo + i + 8 - lead); bytes
+    // outside [0, x9) land below 8 (header, rewritten) or at >= wpos
+    // (free, overwritten later) -- written before this chunk's tokens.
+    {
+        const uint32_t e = (8u - lead) & 3u;           // ring pos = bo + i + (dq + e)
+        const int32_t dq = (int32_t)(8u - lead) - (int32_t)e;
+        const uint32_t pw = vw::shr1(cur.w.w, 0u);
+        const uint32_t sh = (4u - e) & 3u;
+        uint32_t o0, o1, o2, o3, o4;
+        if (e == 0) { o0 = cur.w.x; o1 = cur.w.y; o2 = cur.w.z; o3 = cur.w.w; o4 = 0; }
+        else {
+            o0 = vw::alignbyte(cur.w.x, pw, sh);
+            o1 = vw::alignbyte(cur.w.y, cur.w.x, sh);
+            o2 = vw::alignbyte(cur.w.z, cur.w.y, sh);
+            o3 = vw::alignbyte(cur.w.w, cur.w.z, sh);
+            o4 = vw::alignbyte(cur.y, cur.w.w, sh);
+        }
+        // dword k holds ring bytes [bo + dq + 4k, +4)
+        uint32_t *rd = reinterpret_cast<uint32_t *>(r.lds);
+        const uint32_t base = (uint32_t)((int32_t)bo + dq);
+        if (e == 0 || l != 0) rd[((base + 0) & RMASK) >> 2] = o0;   // lane 0's was written by lane 63 before
+        rd[((base + 4) & RMASK) >> 2] = o1;
+        rd[((base + 8) & RMASK) >> 2] = o2;
+        rd[((base + 12) & RMASK) >> 2] = o3;
+        if (e != 0 && l == 63) rd[((base + 16) & RMASK) >> 2] = o4;
+    }
+    nf += vw::readlane(inc, 63);
+    if (!hb) {
+        const int32_t upto = (int32_t)((c + 1) * BURST) - (int32_t)lead;
+        r.wpos = 8u + umin32(len, upto <= 0 ? 0u : (uint32_t)upto);
+        ring_flush(r, false);
+        return 0;   // (if this was the last chunk: < 10 fields -> general path)
+    }
+    f.gt0 = (int32_t)x9;
+    r.wpos = 8u + x9;
+    const uint32_t glen = len - x9;
+    if (((glen + 1) & 3u) != 0) return 2;
+    f.T = (glen + 1) >> 2;
+    f.phi = (lead + x9) & 3u;
+    return 1;
+}
+
+// Genotype tokens whose first byte lies in chunk c; false = not the fast shape.
+__device__ __forceinline__ bool fast_gt_step(const Chunk &cur, uint32_t c, uint32_t lead, FastState &f, Ring &r) {
+    const uint32_t l = vw::lane_id();
+    const uint32_t bo = c * BURST + 16u * l;
+    const int32_t x0 = (int32_t)bo - (int32_t)lead;
+    const uint32_t T = f.T, phi = f.phi;
+    const int32_t gt0 = f.gt0;
+    uint32_t &pcls = f.pcls;
+    uint32_t &prs = f.prs;
+    // ---- genotype tokens whose first byte lies in this chunk ----
+    uint32_t d[4];
+    d[0] = vw::alignbyte(cur.w.y, cur.w.x, phi);
+    d[1] = vw::alignbyte(cur.w.z, cur.w.y, phi);
+    d[2] = vw::alignbyte(cur.w.w, cur.w.z, phi);
+    d[3] = vw::alignbyte(cur.y, cur.w.w, phi);
+    const int32_t t0 = (x0 + (int32_t)phi - gt0) >> 2;   // token index of slot 0 (exact)
+    const bool v0 = (uint32_t)(t0 + 0) < T, v1 = (uint32_t)(t0 + 1) < T;
+    const bool v2 = (uint32_t)(t0 + 2) < T, v3 = (uint32_t)(t0 + 3) < T;
+    constexpr uint32_t Z = 0x09307C30u;   // "0|0\t"
+
+    // whole chunk inside one 0|0 run: only full 127-chunks can complete
+    const bool z = v0 & v1 & v2 & v3 & (d[0] == Z) & (d[1] == Z) & (d[2] == Z) & (d[3] == Z);
+    if (pcls == 0 && vw::ballot(z) == ~0ull) {
+        const uint32_t tb = (uint32_t)vw::readfirst((uint32_t)t0);   // lane 0's first token
+        // token t has run offset o = t + 1 - prs; it completes a 127-chunk
+        // when (o + 1) % 127 == 0: count multiples of 127 in [a0+1, a0+256]
+        const uint32_t a0 = tb + 1 - prs;
+        const uint32_t kfull = (a0 + 256) / 127 - a0 / 127;
+        if (l < kfull) ring_put(r, r.wpos + l, 0x7Fu);
+        r.wpos += kfull;
+        ring_flush(r, false);
+        return true;
+    }
+
+    // validity of the shape: TAB after every token but the last, none inside
+    bool bad = false;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t x = d[j] ^ 0x09090909u;
+        const uint32_t zb = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
+        const bool vj = (uint32_t)(t0 + j) < T;
+        const bool last = (uint32_t)(t0 + j) + 1 == T;
+        bad |= vj && ((zb & 0x00808080u) != 0 || ((zb >> 31) == 0 && !last));
+    }
+    if (vw::ballot(bad)) return false;
+
+    uint32_t cl[4];
+    cl[0] = v0 ? cls_f(d[0]) : CLS_NONE;
+    cl[1] = v1 ? cls_f(d[1]) : CLS_NONE;
+    cl[2] = v2 ? cls_f(d[2]) : CLS_NONE;
+    cl[3] = v3 ? cls_f(d[3]) : CLS_NONE;
+    uint32_t p[4];
+    p[0] = vw::shr1(cl[3], pcls);
+    p[1] = cl[0];
+    p[2] = cl[1];
+    p[3] = cl[2];
+    bool s[4];
+    uint32_t u[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        s[j] = cl[j] != CLS_NONE && (cl[j] != p[j] || cl[j] == CLS_ESC);
+        u[j] = (uint32_t)(t0 + j + 1);
+    }
+    const uint32_t lane_rs = s[3] ? u[3] : s[2] ? u[2] : s[1] ? u[1] : s[0] ? u[0] : 0u;
+    const uint32_t rin = vw::umax(vw::shr1(vw::scan_max(lane_rs), 0u), prs);
+    uint32_t rr[4];
+    rr[0] = s[0] ? u[0] : rin;
+    rr[1] = s[1] ? u[1] : rr[0];
+    rr[2] = s[2] ? u[2] : rr[1];
+    rr[3] = s[3] ? u[3] : rr[2];
+    // offset-in-run mod cap for each token (m) and for the token before slot 0 (mp0)
+    uint32_t m[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) m[j] = mod_cap(u[j] - rr[j], cl[j] == 0);
+    const uint32_t mp0 = mod_cap(u[0] - 1 - rin, p[0] == 0);
+    uint32_t nb[4], info[4];
+    uint32_t lane_sum = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t mp = j == 0 ? mp0 : m[j - 1];
+        const uint32_t pj = p[j], cj = cl[j];
+        const bool live = cj != CLS_NONE;
+        const bool tab = live && pj == CLS_ESC;
+        const bool pend = live && s[j] && pj < CLS_ESC && mp != (pj == 0 ? 126u : 30u);
+        const bool full = cj < CLS_ESC && m[j] == (cj == 0 ? 126u : 30u);
+        const uint32_t own = cj == CLS_ESC ? 4u : (full ? 1u : 0u);
+        nb[j] = (tab ? 1u : 0u) + (pend ? 1u : 0u) + own;
+        // packed emission: bit0 tab, bit1 pend, bit2 full, bits 8.. pend byte
+        info[j] = (tab ? 1u : 0u) | (pend ? 2u : 0u) | (full ? 4u : 0u) | ((cls_mask_f(pj) | (mp + 1)) << 8);
+        lane_sum += nb[j];
+    }
+    const uint32_t incl = vw::scan_add(lane_sum);
+    uint32_t pos = r.wpos + incl - lane_sum;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t f = info[j];
+        if (f & 1u) ring_put(r, pos, 0x09u);
+        pos += f & 1u;
+        if (f & 2u) ring_put(r, pos, f >> 8);
+        pos += (f >> 1) & 1u;
+        if (cl[j] == CLS_ESC) {
+            ring_put(r, pos, 0xE1u);
+            ring_put(r, pos + 1, d[j] & 0xFFu);
+            ring_put(r, pos + 2, (d[j] >> 8) & 0xFFu);
+            ring_put(r, pos + 3, (d[j] >> 16) & 0xFFu);
+            pos += 4;
+        } else if (f & 4u) {
+            ring_put(r, pos, cls_mask_f(cl[j]) | (cl[j] == 0 ? 127u : 31u));
+            pos += 1;
+        }
+    }
+    r.wpos += vw::readlane(incl, 63);
+    // carry: the chunk's last token
+    const uint64_t hv = vw::ballot(v0 | v1 | v2 | v3);
+    if (hv) {
+        const uint32_t src = (uint32_t)vw::hibit64(hv);
+        const uint32_t lc = v3 ? cl[3] : v2 ? cl[2] : v1 ? cl[1] : cl[0];
+        const uint32_t lr = v3 ? rr[3] : v2 ? rr[2] : v1 ? rr[1] : rr[0];
+        pcls = vw::readlane(lc, src);
+        prs = vw::readlane(lr, src);
+    }
+    ring_flush(r, false);
+    return true;
+}
+
+__device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring &r, uint32_t *rec_bytes) {
+    const uint32_t l = vw::lane_id();
     const uint32_t lead = (uint32_t)(reinterpret_cast<uintptr_t>(line) & 15);
+    const uint8_t *A = line - lead;
     const uint32_t span = lead + len;
+    if (len == 0) return false;
+    const uint32_t last_blk = (span - 1) >> 4;   // last 16-byte block holding line bytes
     const uint32_t nch = (span + BURST - 1) / BURST;
-    const uint4 zero = make_uint4(0, 0, 0, 0);
-
-    auto load = [&](uint32_t c) -> uint4 {
-        const uint32_t bo = c * BURST + 16u * l;
-        return bo < span ? A[bo >> 4] : zero;
-    };
-
-    uint32_t nf = 0;         // field starts seen so far
-    uint32_t carryT = 1;     // byte before this chunk is TAB / outside the line
-    int32_t gt0 = -1;        // line offset of the first sample token
-    uint32_t T = 0, phi = 0;
-    uint32_t pcls = CLS_NONE, prs = 0;  // class / run start(+1) of the previous token
+    FastState f;
+    f.nf = 0; f.carryT = 1; f.gt0 = -1; f.T = 0; f.phi = 0; f.pcls = CLS_NONE; f.prs = 0;
     r.wpos = 8;
     r.fpos = 0;
 
-    uint4 cur = load(0);
-    uint4 nxt = nch > 1 ? load(1) : zero;
-    for (uint32_t c = 0; c < nch; c++) {
-        const uint4 nn = (c + 2 < nch) ? load(c + 2) : zero;
-        const uint32_t bo = c * BURST + 16u * l;   // byte offset of this lane from A
-        const int32_t x0 = (int32_t)bo - (int32_t)lead;  // line offset of byte 0
-
-        if (gt0 < 0) {
-            // ---- prefix: locate the 10th field start, reject empty fields ----
-            const int32_t vlo = x0 >= 0 ? 0 : (-x0 >= 16 ? 16 : -x0);
-            const int32_t vhi0 = (int32_t)len - x0;
-            const int32_t vhi = vhi0 <= 0 ? 0 : (vhi0 >= 16 ? 16 : vhi0);
-            const uint32_t vm = vhi > vlo ? (((1u << vhi) - 1u) ^ ((1u << vlo) - 1u)) : 0u;
-            const uint32_t m = tab_mask16(cur) & vm;
-            const uint32_t Tm = (m | ~vm) & 0xFFFFu;
-            const uint32_t pin = vw::shr1((Tm >> 15) & 1u, carryT);
-            const uint32_t prevT = ((Tm << 1) | pin) & 0xFFFFu;
-            const uint32_t fs = ~Tm & prevT & 0xFFFFu;     // field starts
-            const uint32_t et = m & prevT;                 // TAB closing an empty field
-            carryT = vw::readlane((Tm >> 15) & 1u, 63);
-            const uint32_t cnt = (uint32_t)__builtin_popcount(fs);
-            const uint32_t inc = vw::scan_add(cnt);
-            const uint32_t exc = inc - cnt;
-            const bool has9 = nf + exc <= 9 && 9 < nf + inc;
-            uint32_t x9 = 0xFFFFFFFFu;
-            if (has9) {
-                uint32_t mm = fs;
-                for (uint32_t k = nf + exc; k < 9; k++) mm &= mm - 1;
-                x9 = (uint32_t)(x0 + __builtin_ctz(mm));
-            }
-            const uint64_t hb = vw::ballot(has9);
-            if (hb) x9 = vw::readlane(x9, (uint32_t)__builtin_ctzll(hb));
-            // empty field before the first sample -> general path
-            uint32_t below = 0xFFFFu;
-            if (hb) {
-                const int32_t d = (int32_t)x9 - x0;
-                below = d <= 0 ? 0u : d >= 16 ? 0xFFFFu : ((1u << d) - 1u);
-            }
-            if (vw::ballot((et & below) != 0)) return false;
-            // copy prefix bytes [0, min(x9, len)) of this chunk to the record
-            const uint32_t lim = hb ? x9 : len;
-            for (uint32_t i = 0; i < 16; i++) {
-                const int32_t x = x0 + (int32_t)i;
-                if (x >= 0 && (uint32_t)x < lim) ring_put(r, 8u + (uint32_t)x, byte_of(cur, i));
-            }
-            nf += vw::readlane(inc, 63);
-            if (!hb) {
-                const int32_t upto = (int32_t)((c + 1) * BURST) - (int32_t)lead;
-                r.wpos = 8u + umin32(len, upto <= 0 ? 0u : (uint32_t)upto);
-                ring_flush(r, false);
-                cur = nxt;
-                nxt = nn;
-                continue;   // (if this was the last chunk: < 10 fields -> general path)
-            }
-            gt0 = (int32_t)x9;
-            r.wpos = 8u + x9;
-            const uint32_t glen = len - x9;
-            if (((glen + 1) & 3u) != 0) return false;
-            T = (glen + 1) >> 2;
-            phi = (lead + x9) & 3u;
+    // three chunk buffers: while b0 is processed, b1 and b2 are in flight
+    Chunk b0 = load_chunk(A, 0, l, last_blk);
+    Chunk b1 = load_chunk(A, 1, l, last_blk);
+    Chunk b2 = load_chunk(A, 2, l, last_blk);
+    vw::pin_loads();
+    // (readfirst marks the wave-uniform loop state as uniform for the
+    // compiler: scalar loop control, no exec-masked loop structurisation)
+    uint32_t c = 0;
+    int st = (int)vw::readfirst((uint32_t)fast_prefix_step(b0, 0, lead, len, f, r));
+    if (st == 2) return false;
+    if (st == 0) {
+        // prefix longer than one chunk (rare): walk it, then restart the
+        // three-deep prefetch at the chunk holding the first sample
+        for (;;) {
+            c = vw::readfirst(c + 1);
+            if (c >= nch) return false;   // < 10 fields
+            const Chunk t = load_chunk(A, c, l, last_blk);
+            st = (int)vw::readfirst((uint32_t)fast_prefix_step(t, c, lead, len, f, r));
+            if (st == 2) return false;
+            if (st == 1) break;
         }
-
-        // ---- genotype tokens whose first byte lies in this chunk ----
-        // slot j of lane l starts at chunk byte 16l + 4j + phi
-        const uint32_t nfill = vw::readlane(nxt.x, 0);
-        const uint32_t w4 = vw::shl1(cur.x, nfill);
-        uint32_t d[4];
-        d[0] = vw::alignbyte(cur.y, cur.x, phi);
-        d[1] = vw::alignbyte(cur.z, cur.y, phi);
-        d[2] = vw::alignbyte(cur.w, cur.z, phi);
-        d[3] = vw::alignbyte(w4, cur.w, phi);
-        const int32_t xs0 = x0 + (int32_t)phi - gt0;   // offset of slot 0 from gt0 (multiple of 4)
-        const int32_t tfirst_i = (int32_t)(c * BURST) + (int32_t)phi - (int32_t)lead - gt0;
-        const uint32_t tfirst = tfirst_i <= 0 ? 0u : (uint32_t)tfirst_i >> 2;  // first token of the chunk
-        uint32_t cl[4], tt[4];
-        bool v[4];
-        bool bad = false;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int32_t xo = xs0 + 4 * j;
-            v[j] = xo >= 0 && (uint32_t)(xo >> 2) < T;
-            tt[j] = v[j] ? (uint32_t)(xo >> 2) : 0u;
-            const uint32_t tok = d[j] & 0xFFFFFFu;
-            const bool tab_in_tok = (zero_bytes4((d[j] ^ 0x09090909u) | 0xFF000000u)) != 0;
-            const bool sep_ok = (d[j] >> 24) == 9u || tt[j] + 1 == T;
-            bad |= v[j] && (tab_in_tok || !sep_ok);
-            cl[j] = cls_of(tok);
-        }
-        if (vw::ballot(bad)) return false;
-
-        // previous-token class and run starts (values stored +1, 0 = none)
-        const uint32_t c3prev = vw::shr1(cl[3], CLS_NONE);
-        uint32_t p[4], s[4];
-        uint32_t lane_rs = 0;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint32_t pj = (tt[j] == tfirst) ? pcls : (j == 0 ? c3prev : cl[j - 1]);
-            p[j] = pj;
-            s[j] = v[j] && (cl[j] == CLS_ESC || pj == CLS_ESC || cl[j] != pj);
-            if (s[j]) lane_rs = tt[j] + 1;
-        }
-        const uint32_t rs_inc = vw::scan_max(lane_rs);
-        const uint32_t rin = vw::umax(vw::shr1(rs_inc, 0u), prs);
-
-        uint32_t nb[4], pend[4], pcnt[4], full[4], rr[4];
-        uint32_t lane_sum = 0;
-        uint32_t rprev = rin;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint32_t rj = s[j] ? tt[j] + 1 : rprev;
-            rr[j] = rj;
-            const uint32_t pj = p[j];
-            uint32_t pe = 0, pc = 0;
-            if (v[j] && s[j] && pj < CLS_ESC) {
-                const uint32_t off = (tt[j] - rprev) % cls_cap(pj);   // offset of token t-1 in its run
-                pe = off != cls_cap(pj) - 1 ? 1u : 0u;
-                pc = off + 1;
-            }
-            uint32_t fu = 0;
-            if (v[j] && cl[j] < CLS_ESC) fu = ((tt[j] + 1 - rj) % cls_cap(cl[j])) == cls_cap(cl[j]) - 1 ? 1u : 0u;
-            pend[j] = pe;
-            pcnt[j] = pc;
-            full[j] = fu;
-            const uint32_t n = v[j] ? ((pj == CLS_ESC ? 1u : 0u) + pe + (cl[j] == CLS_ESC ? 4u : fu)) : 0u;
-            nb[j] = n;
-            lane_sum += n;
-            rprev = v[j] ? rj : rprev;
-        }
-        const uint32_t inc = vw::scan_add(lane_sum);
-        uint32_t pos = r.wpos + inc - lane_sum;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            if (!v[j]) continue;
-            if (p[j] == CLS_ESC) ring_put(r, pos++, 0x09u);
-            if (pend[j]) ring_put(r, pos++, cls_mask(p[j]) | pcnt[j]);
-            if (cl[j] == CLS_ESC) {
-                ring_put(r, pos, 0xE1u);
-                ring_put(r, pos + 1, d[j] & 0xFFu);
-                ring_put(r, pos + 2, (d[j] >> 8) & 0xFFu);
-                ring_put(r, pos + 3, (d[j] >> 16) & 0xFFu);
-                pos += 4;
-            } else if (full[j]) {
-                ring_put(r, pos++, cls_mask(cl[j]) | cls_cap(cl[j]));
-            }
-        }
-        r.wpos += vw::readlane(inc, 63);
-        // carry the last token of the chunk
-        uint32_t lcls = CLS_NONE, lrs = 0;
-#pragma unroll
-        for (int j = 0; j < 4; j++)
-            if (v[j]) { lcls = cl[j]; lrs = rr[j]; }
-        const uint64_t hv = vw::ballot(lcls != CLS_NONE);
-        if (hv) {
-            const uint32_t src = (uint32_t)vw::hibit64(hv);
-            pcls = vw::readlane(lcls, src);
-            prs = vw::readlane(lrs, src);
-        }
-        ring_flush(r, false);
-        cur = nxt;
-        nxt = nn;
+        b0 = load_chunk(A, c, l, last_blk);
+        b1 = load_chunk(A, c + 1, l, last_blk);
+        b2 = load_chunk(A, c + 2, l, last_blk);
+        vw::pin_loads();
     }
-    if (gt0 < 0) return false;   // fewer than 10 fields
+    // genotype chunks, unrolled x3 over named buffers: no register copies
+    // and a single loop exit (early exits merge into the latch and make
+    // hipcc's vmcnt tracking fall back to vmcnt(0)), so two chunks stay in
+    // flight behind every step.  Loads past the row clamp to its last block.
+    bool ok = true;
+    for (;;) {
+        ok = vw::readfirst(ok && fast_gt_step(b0, c, lead, f, r));
+        b0 = load_chunk(A, c + 3, l, last_blk);
+        vw::pin_loads();
+        if (ok && c + 1 < nch) ok = vw::readfirst(fast_gt_step(b1, c + 1, lead, f, r));
+        b1 = load_chunk(A, c + 4, l, last_blk);
+        vw::pin_loads();
+        if (ok && c + 2 < nch) ok = vw::readfirst(fast_gt_step(b2, c + 2, lead, f, r));
+        b2 = load_chunk(A, c + 5, l, last_blk);
+        vw::pin_loads();
+        c = vw::readfirst(c + 3);
+        if (!ok || c >= nch) break;
+    }
+    if (!ok) return false;
+    const uint32_t T = f.T, pcls = f.pcls, prs = f.prs;
+    const int32_t gt0 = f.gt0;
     // row end: pending chunk of the last run, then '\n'
-    if (l == 0) {
-        uint32_t w = r.wpos;
-        if (pcls < CLS_ESC) {
-            const uint32_t off = (T - prs) % cls_cap(pcls);
-            if (off != cls_cap(pcls) - 1) ring_put(r, w++, cls_mask(pcls) | (off + 1));
-        }
-        ring_put(r, w, 0x0Au);
+    uint32_t extra = 0, pb = 0;
+    if (pcls < CLS_ESC) {
+        const uint32_t off = mod_cap(T - prs, pcls == 0);
+        if (off != (pcls == 0 ? 126u : 30u)) { extra = 1; pb = cls_mask_f(pcls) | (off + 1); }
     }
-    if (pcls < CLS_ESC && ((T - prs) % cls_cap(pcls)) != cls_cap(pcls) - 1) r.wpos++;
-    r.wpos++;
+    if (l == 0) {
+        if (extra) ring_put(r, r.wpos, pb);
+        ring_put(r, r.wpos + extra, 0x0Au);
+    }
+    r.wpos += extra + 1;
     ring_finish(r, (uint32_t)gt0);
     *rec_bytes = r.wpos;
     return true;
 }
+
 
 // ---------------------------------------------------------------------------
 // General path: any line.  64-byte windows, one byte per lane (plus a 3-byte
@@ -421,16 +555,10 @@ __device__ uint32_t encode_general(const uint8_t *__restrict__ line, uint32_t le
     return VCFCD_OK;
 }
 
-__global__ __launch_bounds__(256) void k_encode(VcfcEncodeArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[K1_WAVES * RING];
-    const uint32_t wave = threadIdx.x >> 6;
-    const uint64_t row = (uint64_t)blockIdx.x * K1_WAVES + wave;
-    if (row >= a.n) return;
-    const uint64_t so = a.slot_off[row];
-    const uint32_t len = a.line_len[row];
-    Ring r;
-    r.lds = lds + wave * RING;
-    r.slot = a.slots + so;
+// Row prologue shared by both encode kernels: slot bounds check + ring setup.
+__device__ __forceinline__ bool row_setup(const VcfcEncodeArgs &a, uint64_t row, uint8_t *lds, Ring &r) {
+    r.lds = lds;
+    r.slot = a.slots + a.slot_off[row];
     r.wpos = 8;
     r.fpos = 0;
     if (a.slot_off[row + 1] > a.slots_cap) {
@@ -438,15 +566,47 @@ __global__ __launch_bounds__(256) void k_encode(VcfcEncodeArgs a) {
             a.rec_size[row] = 0;
             atomicMin((unsigned long long *)a.err, (unsigned long long)((row << 8) | VCFCD_E_NOSPACE));
         }
-        return;
+        return false;
     }
-    const uint8_t *line = a.buf + a.line_off[row];
+    return true;
+}
+
+// Fast kernel: one wave per row; rows without the GT-only shape are queued
+// for k_encode_general.
+__global__ __launch_bounds__(256) void k_encode_fast(VcfcEncodeArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[K1_WAVES * RING];
+    const uint32_t wave = vw::readfirst(threadIdx.x >> 6);   // wave-uniform: scalar row/len/loop control
+    const uint64_t row = (uint64_t)blockIdx.x * K1_WAVES + wave;
+    if (row >= a.n) return;
+    Ring r;
+    if (!row_setup(a, row, lds + wave * RING, r)) return;
     uint32_t bytes = 0;
-    uint32_t st = VCFCD_OK;
-    if (!encode_fast(line, len, r, &bytes)) st = encode_general(line, len, r, &bytes);
+    const bool ok = encode_fast(a.buf + a.line_off[row], a.line_len[row], r, &bytes);
     if (vw::lane_id() == 0) {
-        a.rec_size[row] = st == VCFCD_OK ? bytes : 0u;
-        if (st != VCFCD_OK) atomicMin((unsigned long long *)a.err, (unsigned long long)((row << 8) | st));
+        if (ok) {
+            a.rec_size[row] = bytes;
+        } else {
+            const uint32_t k = atomicAdd(a.retry_count, 1u);
+            a.retry[k] = (uint32_t)row;
+        }
+    }
+}
+
+// General kernel: persistent waves drain the retry list.
+__global__ __launch_bounds__(256) void k_encode_general(VcfcEncodeArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[K1_WAVES * RING];
+    const uint32_t wave = vw::readfirst(threadIdx.x >> 6);
+    const uint32_t cnt = *a.retry_count;
+    for (uint64_t i = (uint64_t)blockIdx.x * K1_WAVES + wave; i < cnt; i += (uint64_t)gridDim.x * K1_WAVES) {
+        const uint64_t row = a.retry[i];
+        Ring r;
+        if (!row_setup(a, row, lds + wave * RING, r)) continue;
+        uint32_t bytes = 0;
+        const uint32_t st = encode_general(a.buf + a.line_off[row], a.line_len[row], r, &bytes);
+        if (vw::lane_id() == 0) {
+            a.rec_size[row] = st == VCFCD_OK ? bytes : 0u;
+            if (st != VCFCD_OK) atomicMin((unsigned long long *)a.err, (unsigned long long)((row << 8) | st));
+        }
     }
 }
 
@@ -591,6 +751,8 @@ VcfcWorkspaceLayout vcfc_encode_workspace_layout(uint64_t n, uint64_t total_line
     L.rec_size = o; o = al(o + 4 * (n + 1));
     L.partials = o; o = al(o + 8 * ((n + SCAN_TILE - 1) / SCAN_TILE + 1));
     L.err = o; o = al(o + 8);
+    L.retry = o; o = al(o + 4 * (n + 1));
+    L.retry_count = o; o = al(o + 8);
     L.slots = o; o = al(o + total_line_bytes + total_line_bytes / 2 + 64 * (n + 1));
     L.total = o;
     return L;
@@ -604,8 +766,14 @@ hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t s, hipEvent_t
     e = launch_scan<1>(a.line_len, a.n, a.partials, a.slot_off, s);
     if (e != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[1], s);
-    hipLaunchKernelGGL(k_encode, dim3((unsigned)((a.n + K1_WAVES - 1) / K1_WAVES)), dim3(64 * K1_WAVES), 0, s, a);
+    if ((e = hipMemsetAsync(a.retry_count, 0, 4, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_encode_fast, dim3((unsigned)((a.n + K1_WAVES - 1) / K1_WAVES)), dim3(64 * K1_WAVES), 0, s, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    {
+        const uint64_t want = (a.n + K1_WAVES - 1) / K1_WAVES;
+        hipLaunchKernelGGL(k_encode_general, dim3((unsigned)(want < 2048 ? want : 2048)), dim3(64 * K1_WAVES), 0, s, a);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     if (ev) (void)hipEventRecord(ev[2], s);
     e = launch_scan<0>(a.rec_size, a.n, a.partials, a.rec_off, s);
     if (e != hipSuccess) return e;

@@ -75,4 +75,29 @@ __device__ __forceinline__ int popc64(uint64_t m) { return __popcll(m); }
 // index of the highest set bit (m != 0)
 __device__ __forceinline__ int hibit64(uint64_t m) { return 63 - __clzll(m); }
 
+__device__ __forceinline__ uint32_t mulhi(uint32_t a, uint32_t b) { return __umulhi(a, b); }
+
+// Global-memory accesses with the address space made explicit, so hipcc
+// emits global_load/store (counted by vmcnt) instead of flat_* (whose
+// out-of-order completion forces vmcnt(0)+lgkmcnt(0) waits).
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const v4u g_cv4u;
+typedef __attribute__((address_space(1))) v4u g_v4u;
+typedef __attribute__((address_space(1))) const uint32_t g_cu32;
+__device__ __forceinline__ uint4 gload16(const void *base, uint32_t idx) {
+    const v4u v = ((g_cv4u *)base)[idx];
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint32_t gload4(const void *base, uint32_t idx) {
+    return ((g_cu32 *)base)[idx];
+}
+__device__ __forceinline__ void gstore16(void *base, uint64_t byte_off, uint4 v) {
+    v4u t;
+    t.x = v.x; t.y = v.y; t.z = v.z; t.w = v.w;
+    *((g_v4u *)((__attribute__((address_space(1))) uint8_t *)base + byte_off)) = t;
+}
+// Keep just-issued prefetch loads where they are: the memory clobber stops
+// LLVM from sinking them towards their (next-iteration) use, which would
+// shrink the prefetch distance to zero.  Emits no instruction.
+__device__ __forceinline__ void pin_loads() { asm volatile("" ::: "memory"); }
 }  // namespace vw
