@@ -35,6 +35,7 @@ namespace {
 constexpr int K1_WAVES = 4;            // rows per 256-thread block
 constexpr uint32_t RING = 4096;        // per-wave LDS ring (bytes)
 constexpr uint32_t RMASK = RING - 1;
+constexpr uint32_t RING_STRIDE = RING + 64;   // + one dummy byte per lane (branch-free stores)
 constexpr uint32_t BURST = 1024;       // flush granule (64 lanes x 16 B)
 constexpr uint32_t CLS_ESC = 4, CLS_NONE = 5;
 
@@ -243,36 +244,33 @@ __device__ __forceinline__ int fast_prefix_step(const Chunk &cur, uint32_t c, ui
     if (((glen + 1) & 3u) != 0) return 2;
     f.T = (glen + 1) >> 2;
     f.phi = (lead + x9) & 3u;
+    if (f.T >= (1u << 24)) return 2;   // mod_cap's magic numbers are exact below 2^24
     return 1;
 }
 
 // Genotype tokens whose first byte lies in chunk c; false = not the fast shape.
 __device__ __forceinline__ bool fast_gt_step(const Chunk &cur, uint32_t c, uint32_t lead, FastState &f, Ring &r) {
     const uint32_t l = vw::lane_id();
-    const uint32_t bo = c * BURST + 16u * l;
-    const int32_t x0 = (int32_t)bo - (int32_t)lead;
+    const int32_t x0 = (int32_t)(c * BURST + 16u * l) - (int32_t)lead;
     const uint32_t T = f.T, phi = f.phi;
-    const int32_t gt0 = f.gt0;
-    uint32_t &pcls = f.pcls;
-    uint32_t &prs = f.prs;
-    // ---- genotype tokens whose first byte lies in this chunk ----
+    constexpr uint32_t Z = 0x09307C30u;   // "0|0\t"
     uint32_t d[4];
     d[0] = vw::alignbyte(cur.w.y, cur.w.x, phi);
     d[1] = vw::alignbyte(cur.w.z, cur.w.y, phi);
     d[2] = vw::alignbyte(cur.w.w, cur.w.z, phi);
     d[3] = vw::alignbyte(cur.y, cur.w.w, phi);
-    const int32_t t0 = (x0 + (int32_t)phi - gt0) >> 2;   // token index of slot 0 (exact)
-    const bool v0 = (uint32_t)(t0 + 0) < T, v1 = (uint32_t)(t0 + 1) < T;
-    const bool v2 = (uint32_t)(t0 + 2) < T, v3 = (uint32_t)(t0 + 3) < T;
-    constexpr uint32_t Z = 0x09307C30u;   // "0|0\t"
+    const int32_t t0 = (x0 + (int32_t)phi - f.gt0) >> 2;   // token index of slot 0 (exact)
+    bool v[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) v[j] = (uint32_t)(t0 + j) < T;
 
     // whole chunk inside one 0|0 run: only full 127-chunks can complete
-    const bool z = v0 & v1 & v2 & v3 & (d[0] == Z) & (d[1] == Z) & (d[2] == Z) & (d[3] == Z);
-    if (pcls == 0 && vw::ballot(z) == ~0ull) {
+    const bool z = v[0] & v[1] & v[2] & v[3] & (d[0] == Z) & (d[1] == Z) & (d[2] == Z) & (d[3] == Z);
+    if (f.pcls == 0 && vw::ballot(z) == ~0ull) {
         const uint32_t tb = (uint32_t)vw::readfirst((uint32_t)t0);   // lane 0's first token
         // token t has run offset o = t + 1 - prs; it completes a 127-chunk
         // when (o + 1) % 127 == 0: count multiples of 127 in [a0+1, a0+256]
-        const uint32_t a0 = tb + 1 - prs;
+        const uint32_t a0 = tb + 1 - f.prs;
         const uint32_t kfull = (a0 + 256) / 127 - a0 / 127;
         if (l < kfull) ring_put(r, r.wpos + l, 0x7Fu);
         r.wpos += kfull;
@@ -280,93 +278,101 @@ __device__ __forceinline__ bool fast_gt_step(const Chunk &cur, uint32_t c, uint3
         return true;
     }
 
-    // validity of the shape: TAB after every token but the last, none inside
-    bool bad = false;
+    // classes.  "a|b\t" with a, b in {0,1} is a classed token whose shape is
+    // already right; any other valid slot (an escape, or the row's last token
+    // which has no TAB after it) gets the full shape check.
+    uint32_t cl[4];
+    bool odd = false;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-        const uint32_t x = d[j] ^ 0x09090909u;
-        const uint32_t zb = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
-        const bool vj = (uint32_t)(t0 + j) < T;
-        const bool last = (uint32_t)(t0 + j) + 1 == T;
-        bad |= vj && ((zb & 0x00808080u) != 0 || ((zb >> 31) == 0 && !last));
+        const bool isc = (d[j] & 0xFFFEFFFEu) == Z;
+        cl[j] = !v[j] ? CLS_NONE : isc ? (((d[j] & 1u) << 1) | ((d[j] >> 16) & 1u)) : CLS_ESC;
+        odd |= v[j] && !isc;
     }
-    if (vw::ballot(bad)) return false;
+    if (vw::ballot(odd)) {
+        bool bad = false;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            if (cl[j] == CLS_ESC) {
+                const uint32_t x = d[j] ^ 0x09090909u;
+                const uint32_t zb = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
+                const bool last = (uint32_t)(t0 + j) + 1 == T;
+                bad |= (zb & 0x00808080u) != 0 || ((zb >> 31) == 0 && !last);
+                cl[j] = cls_f(d[j]);   // the last token may still be a classed one
+            }
+        }
+        if (vw::ballot(bad)) return false;
+    }
 
-    uint32_t cl[4];
-    cl[0] = v0 ? cls_f(d[0]) : CLS_NONE;
-    cl[1] = v1 ? cls_f(d[1]) : CLS_NONE;
-    cl[2] = v2 ? cls_f(d[2]) : CLS_NONE;
-    cl[3] = v3 ? cls_f(d[3]) : CLS_NONE;
+    // previous-token class, run starts (t+1 encoded, 0 = none)
     uint32_t p[4];
-    p[0] = vw::shr1(cl[3], pcls);
+    p[0] = vw::shr1(cl[3], f.pcls);
     p[1] = cl[0];
     p[2] = cl[1];
     p[3] = cl[2];
     bool s[4];
-    uint32_t u[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) s[j] = v[j] && (cl[j] != p[j] || cl[j] == CLS_ESC);
+    const uint32_t u0 = (uint32_t)(t0 + 1);
+    const uint32_t lane_rs = s[3] ? u0 + 3 : s[2] ? u0 + 2 : s[1] ? u0 + 1 : s[0] ? u0 : 0u;
+    const uint32_t rin = vw::umax(vw::shr1(vw::scan_max(lane_rs), 0u), f.prs);
+    // run offset (mod cap) of the token before slot 0, then incremental
+    uint32_t mp = mod_cap((uint32_t)t0 - rin, p[0] == 0);
+    bool tab[4], pend[4], full[4];
+    uint32_t pb[4], nb[4];
+    uint32_t lane_sum = 0, lrs = rin, lm = 0;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-        s[j] = cl[j] != CLS_NONE && (cl[j] != p[j] || cl[j] == CLS_ESC);
-        u[j] = (uint32_t)(t0 + j + 1);
-    }
-    const uint32_t lane_rs = s[3] ? u[3] : s[2] ? u[2] : s[1] ? u[1] : s[0] ? u[0] : 0u;
-    const uint32_t rin = vw::umax(vw::shr1(vw::scan_max(lane_rs), 0u), prs);
-    uint32_t rr[4];
-    rr[0] = s[0] ? u[0] : rin;
-    rr[1] = s[1] ? u[1] : rr[0];
-    rr[2] = s[2] ? u[2] : rr[1];
-    rr[3] = s[3] ? u[3] : rr[2];
-    // offset-in-run mod cap for each token (m) and for the token before slot 0 (mp0)
-    uint32_t m[4];
-#pragma unroll
-    for (int j = 0; j < 4; j++) m[j] = mod_cap(u[j] - rr[j], cl[j] == 0);
-    const uint32_t mp0 = mod_cap(u[0] - 1 - rin, p[0] == 0);
-    uint32_t nb[4], info[4];
-    uint32_t lane_sum = 0;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const uint32_t mp = j == 0 ? mp0 : m[j - 1];
         const uint32_t pj = p[j], cj = cl[j];
-        const bool live = cj != CLS_NONE;
-        const bool tab = live && pj == CLS_ESC;
-        const bool pend = live && s[j] && pj < CLS_ESC && mp != (pj == 0 ? 126u : 30u);
-        const bool full = cj < CLS_ESC && m[j] == (cj == 0 ? 126u : 30u);
-        const uint32_t own = cj == CLS_ESC ? 4u : (full ? 1u : 0u);
-        nb[j] = (tab ? 1u : 0u) + (pend ? 1u : 0u) + own;
-        // packed emission: bit0 tab, bit1 pend, bit2 full, bits 8.. pend byte
-        info[j] = (tab ? 1u : 0u) | (pend ? 2u : 0u) | (full ? 4u : 0u) | ((cls_mask_f(pj) | (mp + 1)) << 8);
+        const uint32_t capm1_p = pj == 0 ? 126u : 30u, capm1_c = cj == 0 ? 126u : 30u;
+        tab[j] = v[j] && pj == CLS_ESC;
+        pend[j] = s[j] && pj < CLS_ESC && mp != capm1_p;
+        pb[j] = cls_mask_f(pj) | (mp + 1);
+        const uint32_t m = s[j] ? 0u : (mp == capm1_c ? 0u : mp + 1);
+        full[j] = cj < CLS_ESC && m == capm1_c;
+        nb[j] = ((tab[j] | pend[j]) ? 1u : 0u) + (cj == CLS_ESC ? 4u : (full[j] ? 1u : 0u));
         lane_sum += nb[j];
+        mp = m;
+        if (s[j]) lrs = u0 + j;
+        if (v[j]) lm = m;
     }
     const uint32_t incl = vw::scan_add(lane_sum);
+    // emission: the common bytes (TAB / pending run byte, full-chunk byte) are
+    // stored unconditionally -- to a per-lane dummy cell when absent -- so no
+    // branches; escape payloads (rare) in a separate pass
+    const uint32_t dummy = RING + l;
     uint32_t pos = r.wpos + incl - lane_sum;
+    uint32_t epos[4];
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-        const uint32_t f = info[j];
-        if (f & 1u) ring_put(r, pos, 0x09u);
-        pos += f & 1u;
-        if (f & 2u) ring_put(r, pos, f >> 8);
-        pos += (f >> 1) & 1u;
-        if (cl[j] == CLS_ESC) {
-            ring_put(r, pos, 0xE1u);
-            ring_put(r, pos + 1, d[j] & 0xFFu);
-            ring_put(r, pos + 2, (d[j] >> 8) & 0xFFu);
-            ring_put(r, pos + 3, (d[j] >> 16) & 0xFFu);
-            pos += 4;
-        } else if (f & 4u) {
-            ring_put(r, pos, cls_mask_f(cl[j]) | (cl[j] == 0 ? 127u : 31u));
-            pos += 1;
+        const bool e1 = tab[j] | pend[j];
+        r.lds[e1 ? (pos & RMASK) : dummy] = (uint8_t)(tab[j] ? 0x09u : pb[j]);
+        pos += e1 ? 1u : 0u;
+        epos[j] = pos;
+        r.lds[full[j] ? (pos & RMASK) : dummy] = (uint8_t)(cls_mask_f(cl[j]) | (cl[j] == 0 ? 127u : 31u));
+        pos += cl[j] == CLS_ESC ? 4u : (full[j] ? 1u : 0u);
+    }
+    if (vw::ballot(cl[0] == CLS_ESC || cl[1] == CLS_ESC || cl[2] == CLS_ESC || cl[3] == CLS_ESC)) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            if (cl[j] == CLS_ESC) {
+                ring_put(r, epos[j], 0xE1u);
+                ring_put(r, epos[j] + 1, d[j] & 0xFFu);
+                ring_put(r, epos[j] + 2, (d[j] >> 8) & 0xFFu);
+                ring_put(r, epos[j] + 3, (d[j] >> 16) & 0xFFu);
+            }
         }
     }
     r.wpos += vw::readlane(incl, 63);
-    // carry: the chunk's last token
-    const uint64_t hv = vw::ballot(v0 | v1 | v2 | v3);
+    // carry the chunk's last token (class, run start)
+    const uint64_t hv = vw::ballot(v[0] | v[1] | v[2] | v[3]);
     if (hv) {
         const uint32_t src = (uint32_t)vw::hibit64(hv);
-        const uint32_t lc = v3 ? cl[3] : v2 ? cl[2] : v1 ? cl[1] : cl[0];
-        const uint32_t lr = v3 ? rr[3] : v2 ? rr[2] : v1 ? rr[1] : rr[0];
-        pcls = vw::readlane(lc, src);
-        prs = vw::readlane(lr, src);
+        const uint32_t lc = v[3] ? cl[3] : v[2] ? cl[2] : v[1] ? cl[1] : cl[0];
+        f.pcls = vw::readlane(lc, src);
+        f.prs = vw::readlane(lrs, src);
     }
+    (void)lm;
     ring_flush(r, false);
     return true;
 }
@@ -574,12 +580,12 @@ __device__ __forceinline__ bool row_setup(const VcfcEncodeArgs &a, uint64_t row,
 // Fast kernel: one wave per row; rows without the GT-only shape are queued
 // for k_encode_general.
 __global__ __launch_bounds__(256) void k_encode_fast(VcfcEncodeArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[K1_WAVES * RING];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[K1_WAVES * RING_STRIDE];
     const uint32_t wave = vw::readfirst(threadIdx.x >> 6);   // wave-uniform: scalar row/len/loop control
     const uint64_t row = (uint64_t)blockIdx.x * K1_WAVES + wave;
     if (row >= a.n) return;
     Ring r;
-    if (!row_setup(a, row, lds + wave * RING, r)) return;
+    if (!row_setup(a, row, lds + wave * RING_STRIDE, r)) return;
     uint32_t bytes = 0;
     const bool ok = encode_fast(a.buf + a.line_off[row], a.line_len[row], r, &bytes);
     if (vw::lane_id() == 0) {
@@ -594,13 +600,13 @@ __global__ __launch_bounds__(256) void k_encode_fast(VcfcEncodeArgs a) {
 
 // General kernel: persistent waves drain the retry list.
 __global__ __launch_bounds__(256) void k_encode_general(VcfcEncodeArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[K1_WAVES * RING];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[K1_WAVES * RING_STRIDE];
     const uint32_t wave = vw::readfirst(threadIdx.x >> 6);
     const uint32_t cnt = *a.retry_count;
     for (uint64_t i = (uint64_t)blockIdx.x * K1_WAVES + wave; i < cnt; i += (uint64_t)gridDim.x * K1_WAVES) {
         const uint64_t row = a.retry[i];
         Ring r;
-        if (!row_setup(a, row, lds + wave * RING, r)) continue;
+        if (!row_setup(a, row, lds + wave * RING_STRIDE, r)) continue;
         uint32_t bytes = 0;
         const uint32_t st = encode_general(a.buf + a.line_off[row], a.line_len[row], r, &bytes);
         if (vw::lane_id() == 0) {
