@@ -320,7 +320,7 @@ __device__ __forceinline__ bool fast_gt_step(const Chunk &cur, uint32_t c, uint3
     uint32_t mp = mod_cap((uint32_t)t0 - rin, p[0] == 0);
     bool tab[4], pend[4], full[4];
     uint32_t pb[4], nb[4];
-    uint32_t lane_sum = 0, lrs = rin, lm = 0;
+    uint32_t lane_sum = 0, lrs = rin;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
         const uint32_t pj = p[j], cj = cl[j];
@@ -334,33 +334,35 @@ __device__ __forceinline__ bool fast_gt_step(const Chunk &cur, uint32_t c, uint3
         lane_sum += nb[j];
         mp = m;
         if (s[j]) lrs = u0 + j;
-        if (v[j]) lm = m;
     }
     const uint32_t incl = vw::scan_add(lane_sum);
     // emission: the common bytes (TAB / pending run byte, full-chunk byte) are
     // stored unconditionally -- to a per-lane dummy cell when absent -- so no
     // branches; escape payloads (rare) in a separate pass
     const uint32_t dummy = RING + l;
-    uint32_t pos = r.wpos + incl - lane_sum;
-    uint32_t epos[4];
+    const uint32_t pos0 = r.wpos + incl - lane_sum;
+    uint32_t pos = pos0;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
         const bool e1 = tab[j] | pend[j];
         r.lds[e1 ? (pos & RMASK) : dummy] = (uint8_t)(tab[j] ? 0x09u : pb[j]);
         pos += e1 ? 1u : 0u;
-        epos[j] = pos;
         r.lds[full[j] ? (pos & RMASK) : dummy] = (uint8_t)(cls_mask_f(cl[j]) | (cl[j] == 0 ? 127u : 31u));
         pos += cl[j] == CLS_ESC ? 4u : (full[j] ? 1u : 0u);
     }
     if (vw::ballot(cl[0] == CLS_ESC || cl[1] == CLS_ESC || cl[2] == CLS_ESC || cl[3] == CLS_ESC)) {
+        // escape payloads: walk the lane's tokens again for their positions
+        pos = pos0;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
+            pos += (tab[j] | pend[j]) ? 1u : 0u;
             if (cl[j] == CLS_ESC) {
-                ring_put(r, epos[j], 0xE1u);
-                ring_put(r, epos[j] + 1, d[j] & 0xFFu);
-                ring_put(r, epos[j] + 2, (d[j] >> 8) & 0xFFu);
-                ring_put(r, epos[j] + 3, (d[j] >> 16) & 0xFFu);
+                ring_put(r, pos, 0xE1u);
+                ring_put(r, pos + 1, d[j] & 0xFFu);
+                ring_put(r, pos + 2, (d[j] >> 8) & 0xFFu);
+                ring_put(r, pos + 3, (d[j] >> 16) & 0xFFu);
             }
+            pos += cl[j] == CLS_ESC ? 4u : (full[j] ? 1u : 0u);
         }
     }
     r.wpos += vw::readlane(incl, 63);
@@ -372,7 +374,6 @@ __device__ __forceinline__ bool fast_gt_step(const Chunk &cur, uint32_t c, uint3
         f.pcls = vw::readlane(lc, src);
         f.prs = vw::readlane(lrs, src);
     }
-    (void)lm;
     ring_flush(r, false);
     return true;
 }
@@ -579,7 +580,7 @@ __device__ __forceinline__ bool row_setup(const VcfcEncodeArgs &a, uint64_t row,
 
 // Fast kernel: one wave per row; rows without the GT-only shape are queued
 // for k_encode_general.
-__global__ __launch_bounds__(256) void k_encode_fast(VcfcEncodeArgs a) {
+__global__ __launch_bounds__(256, 8) void k_encode_fast(VcfcEncodeArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[K1_WAVES * RING_STRIDE];
     const uint32_t wave = vw::readfirst(threadIdx.x >> 6);   // wave-uniform: scalar row/len/loop control
     const uint64_t row = (uint64_t)blockIdx.x * K1_WAVES + wave;
