@@ -118,6 +118,21 @@ uint64_t vcfc_compress_bound(uint64_t in_bytes);
 int vcfc_compress_buffer(vcfc_ctx *ctx, const uint8_t *in, uint64_t n, uint8_t *out, uint64_t out_cap,
                          uint64_t *out_len, int64_t *err_line);
 
+/* ---- sparse layout: sparsify_file (reference src/sparse.cpp:290-580) -------
+ * Record i of the .vcfc goes to data_start + (300e6 + POS_i) * 16384
+ * (compute_sparse_offset, src/sparse.cpp:18-51) behind a 16-byte prefix
+ * BE(dist_to_prev) BE(dist_to_next); the 8 bytes before data_start hold the
+ * first record's offset in host byte order.  Output is a sparse file (holes
+ * between records).  The GPU plans offsets and prefixes; the host writes. */
+uint64_t vcfc_sparse_offset(uint64_t pos);
+int vcfc_sparsify_file(vcfc_ctx *ctx, const char *in_vcfc, const char *out_sparse);
+/* Device plan: records d_recs[d_rec_off[i] .. d_rec_off[i+1]); outputs
+ * d_file_off[i] and d_prefix16[16 i ..]; d_status[0] = ~0 or (row << 8 |
+ * VCFC_E_FORMAT) of the first record whose POS does not parse, d_status[1] =
+ * 1 if records overlap / are out of order (write them in order). */
+int vcfc_sparse_plan_device(const uint8_t *d_recs, const uint64_t *d_rec_off, uint64_t n, uint64_t data_start,
+                            uint64_t *d_file_off, uint8_t *d_prefix16, uint64_t *d_status, void *stream);
+
 /* ---- device-side helpers used by the benchmark ---------------------------
  * Synthetic genotype rows generated in HBM (no host round trip).  `law`:
  *   0 = random_vcf law (alleles i.i.d. 0/1/2 with p .90/.08/.02,

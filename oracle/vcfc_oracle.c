@@ -294,6 +294,25 @@ uint64_t vcfo_sparse_offset(uint64_t pos) {
     return (300000000ull + pos) * (4ull * 4096ull);
 }
 
+/* strtoul(s, &end, 10) with end required at s + n (sparse.cpp:463-467) */
+int vcfo_strtoul_whole(const uint8_t *s, size_t n, uint64_t *out) {
+    size_t i = 0;
+    while (i < n && (s[i] == ' ' || (s[i] >= '\t' && s[i] <= '\r'))) i++;
+    int neg = 0;
+    if (i < n && (s[i] == '+' || s[i] == '-')) { neg = s[i] == '-'; i++; }
+    if (i >= n || s[i] < '0' || s[i] > '9') return 0;
+    uint64_t v = 0;
+    int ovf = 0;
+    for (; i < n && s[i] >= '0' && s[i] <= '9'; i++) {
+        uint64_t d = (uint64_t)(s[i] - '0');
+        if (v > (UINT64_MAX - d) / 10) ovf = 1;
+        v = v * 10 + d;
+    }
+    if (i != n) return 0;
+    *out = ovf ? UINT64_MAX : (neg ? (uint64_t)(0 - v) : v);
+    return 1;
+}
+
 static void be64(uint8_t *o, uint64_t v) {
     for (int i = 0; i < 8; i++) o[i] = (uint8_t)(v >> (56 - 8 * i));
 }
@@ -337,19 +356,22 @@ int vcfo_sparsify(const uint8_t *in, size_t n, const char *out_path) {
         memset(rec, 0, 16);
         memcpy(rec + 16, h, 8);
         memcpy(rec + 24, h + 8, body);
-        /* CHROM, POS: first two tab-terminated fields of the body (:431-471) */
+        /* CHROM, POS: first two tab-terminated fields of the body (:431-471).
+         * An empty CHROM or POS before its TAB throws; a POS that is never
+         * TAB-terminated is never parsed and stays 0; POS must parse whole
+         * under strtoul (leading space, sign, digits; overflow saturates). */
         size_t p = 0;
         while (p < body && h[8 + p] != '\t') p++;
-        if (p == 0 || p >= body) { free(rec); close(fd); return VCFO_E_FORMAT; }
-        size_t ps = ++p;
         uint64_t pos = 0;
-        while (p < body && h[8 + p] != '\t') {
-            uint8_t d = h[8 + p];
-            if (d < '0' || d > '9') { free(rec); close(fd); return VCFO_E_FORMAT; }
-            pos = pos * 10 + (d - '0');
-            p++;
+        if (p < body) {
+            if (p == 0) { free(rec); close(fd); return VCFO_E_FORMAT; }
+            size_t ps = ++p;
+            while (p < body && h[8 + p] != '\t') p++;
+            if (p < body) {
+                if (p == ps) { free(rec); close(fd); return VCFO_E_FORMAT; }
+                if (!vcfo_strtoul_whole(h + 8 + ps, p - ps, &pos)) { free(rec); close(fd); return VCFO_E_FORMAT; }
+            }
         }
-        if (p == ps || p >= body) { free(rec); close(fd); return VCFO_E_FORMAT; }
         uint64_t voff = vcfo_sparse_offset(pos);
         uint64_t foff = voff + data_start;
         be64(rec, foff - prev);                       /* dist_to_prev (:479-488) */

@@ -24,6 +24,7 @@ int vcfo_compress(const uint8_t *in, size_t n, uint8_t *out, size_t cap,
 int vcfo_decompress(const uint8_t *in, size_t n, uint8_t *out, size_t cap, size_t *out_len);
 uint64_t vcfo_sparse_offset(uint64_t pos);
 int vcfo_sparsify(const uint8_t *in, size_t n, const char *out_path);
+int vcfo_strtoul_whole(const uint8_t *s, size_t n, uint64_t *out);
 #ifdef __cplusplus
 }
 #endif

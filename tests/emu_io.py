@@ -19,6 +19,7 @@ def lib():
         vp = ctypes.c_void_p
         L.emu_encode_rows.argtypes = [vp, vp, vp, ctypes.c_uint64, vp, ctypes.c_uint64, vp,
                                       ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+        L.emu_sparse_plan.argtypes = [vp, vp, ctypes.c_uint64, ctypes.c_uint64, vp, vp, vp]
         _lib = L
     return _lib
 
@@ -55,3 +56,16 @@ def emu_encode(buf, line_off, line_len):
                                rec_off.ctypes.data, ctypes.byref(err), ctypes.byref(sw))
     total = int(rec_off[n]) if n else 0
     return st, out[:total].tobytes(), rec_off, err.value
+
+
+def emu_sparse_plan(recs, rec_off, data_start):
+    """Run k_sparse_plan on the emulator: (file_off, prefix16 bytes, status[2])."""
+    n = len(rec_off) - 1
+    src = np.frombuffer(recs, dtype=np.uint8).copy()
+    ro = np.ascontiguousarray(rec_off, dtype=np.uint64)
+    fo = np.zeros(max(n, 1), dtype=np.uint64)
+    pf = np.zeros(16 * max(n, 1), dtype=np.uint8)
+    stt = np.zeros(2, dtype=np.uint64)
+    lib().emu_sparse_plan(src.ctypes.data, ro.ctypes.data, n, data_start, fo.ctypes.data, pf.ctypes.data,
+                          stt.ctypes.data)
+    return fo[:n], pf[:16 * n].tobytes(), stt

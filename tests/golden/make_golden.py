@@ -277,6 +277,23 @@ def main():
         manifest["decode_header_only"] = {"compress_rc": rc, "decompress_rc": rc2,
                                           "error": "VcfValidationError" if "VcfValidationError" in err2 else err2[:120]}
 
+    # ---- sparsify edge cases: duplicate / decreasing POS, records longer than
+    # the 16 KiB stride (overlapping writes), strtoul quirks in POS ----------
+    with tempfile.TemporaryDirectory() as wd:
+        rows = []
+        for pos in [b"100", b"100", b"50", b"+7", b" 9", b"0012", b"200", b"201", b"203", b"202"]:
+            n = 6000 if pos == b"200" else 3
+            toks = b"\t".join([b"2|1"] * n)
+            rows.append(b"1\t" + pos + b"\trs\tA\tG\t50\tPASS\tAC=1\tGT\t" + toks)
+        src = EDGE_HEADER + b"\n".join(rows) + b"\n"
+        rc, enc, err = ref_compress(src, wd, "spe")
+        assert rc == 0, err
+        sp = os.path.join(wd, "spe.sparse")
+        r = run_ref("sparsify", os.path.join(wd, "spe.vcfc"), sp)
+        assert r.returncode == 0, r.stderr
+        gz_write(os.path.join(HERE, "sparse_edge.vcfc.gz"), enc)
+        manifest["sparse_edge"] = sparse_digest.digest(sp)
+
     manifest["generator"] = "tests/golden/make_golden.py (reference: oracle/_ref/main built from /root/reference/src; other/random_vcf.py)"
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1, sort_keys=True)

@@ -34,3 +34,11 @@ extern "C" int emu_encode_rows(const uint8_t *buf, const uint64_t *line_off, con
     free(ws);
     return st;
 }
+
+hipError_t vcfc_sparse_plan_launch(const uint8_t *recs, const uint64_t *rec_off, uint64_t n, uint64_t data_start,
+                                   uint64_t *file_off, uint8_t *prefix, uint64_t *status, hipStream_t s);
+
+extern "C" int emu_sparse_plan(const uint8_t *recs, const uint64_t *rec_off, uint64_t n, uint64_t data_start,
+                               uint64_t *file_off, uint8_t *prefix, uint64_t *status) {
+    return (int)vcfc_sparse_plan_launch(recs, rec_off, n, data_start, file_off, prefix, status, nullptr);
+}

@@ -152,3 +152,19 @@ def test_config2_full_size_sampled(torch, vcfc):
         st, want = G.oracle_encode_line(ln)
         got = out[int(rec[i]):int(rec[i + 1])].cpu().numpy().tobytes()
         assert got == want, i
+
+
+@pytest.mark.parametrize("name,key", [("random_100x10000.vcfc.gz", "sparse_100x10000"),
+                                      ("sparse_edge.vcfc.gz", "sparse_edge")])
+def test_sparsify_matches_reference(ctx, name, key):
+    import sparse_digest
+    with tempfile.TemporaryDirectory() as d:
+        src, dst = os.path.join(d, "in.vcfc"), os.path.join(d, "out.sparse")
+        with open(src, "wb") as f:
+            f.write(G.gz(name))
+        ctx.sparsify_file(src, dst)
+        assert sparse_digest.digest(dst) == G.manifest()[key]
+        r = subprocess.run([os.path.join(REPO, "build", "main"), "sparsify", src, dst + "2"],
+                           capture_output=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        assert sparse_digest.digest(dst + "2") == G.manifest()[key]

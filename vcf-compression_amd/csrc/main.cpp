@@ -55,6 +55,30 @@ int main(int argc, char **argv) {
         }
         return 0;
     }
+    if (action == "sparsify") {
+        // src/main.cpp:4073-4085
+        if (argc < 4) return usage();
+        if (std::string(argv[2]) == argv[3]) {
+            fprintf(stderr, "terminate called after throwing an instance of 'std::runtime_error'\n"
+                            "  what():  input and output file are the same\n");
+            return 134;
+        }
+        if (!file_exists(argv[2])) printf("Input file does not exist: %s\n", argv[2]);
+        vcfc_ctx *ctx = nullptr;
+        int st = vcfc_ctx_create(0, &ctx);
+        if (st != VCFC_OK) {
+            fprintf(stderr, "vcfc: %s\n", vcfc_strerror(st));
+            return 1;
+        }
+        st = vcfc_sparsify_file(ctx, argv[2], argv[3]);
+        vcfc_ctx_destroy(ctx);
+        if (st != VCFC_OK) {
+            fprintf(stderr, "terminate called after throwing an instance of 'VcfValidationError'\n"
+                            "  what():  %s\n", vcfc_strerror(st));
+            return 134;
+        }
+        return 0;
+    }
     std::printf("Unknown action name: %s\n", action.c_str());
     return 0;
 }

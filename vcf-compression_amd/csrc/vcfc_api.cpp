@@ -14,9 +14,13 @@
 #include <string>
 #include <vector>
 
+#include <sys/uio.h>
+
 #include "vcfc.h"
 #include "vcfc_device.h"
 
+hipError_t vcfc_sparse_plan_launch(const uint8_t *recs, const uint64_t *rec_off, uint64_t n, uint64_t data_start,
+                                   uint64_t *file_off, uint8_t *prefix, uint64_t *status, hipStream_t s);
 hipError_t vcfc_synth_device(uint8_t *buf, const uint64_t *line_off, uint64_t n, const uint8_t *prefix,
                              const uint64_t *prefix_off, const float *row_af, uint32_t S, int law,
                              uint64_t seed, hipStream_t s);
@@ -58,8 +62,103 @@ struct vcfc_timer {
 struct vcfc_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    DevBuf in, off, len, out, rec, ws, err;
+    DevBuf in, off, len, out, rec, ws, err, aux;
 };
+
+namespace {
+
+// Read-only mapping of an input file.
+struct MappedFile {
+    int fd = -1;
+    const uint8_t *p = nullptr;
+    uint64_t n = 0;
+    int open_ro(const char *path) {
+        fd = open(path, O_RDONLY);
+        if (fd < 0) return VCFC_E_IO;
+        struct stat st;
+        if (fstat(fd, &st) != 0) return VCFC_E_IO;
+        n = (uint64_t)st.st_size;
+        if (n) {
+            void *m = mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fd, 0);
+            if (m == MAP_FAILED) return VCFC_E_IO;
+            madvise(m, n, MADV_SEQUENTIAL);
+            p = static_cast<const uint8_t *>(m);
+        }
+        return VCFC_OK;
+    }
+    ~MappedFile() {
+        if (p) munmap(const_cast<uint8_t *>(p), n);
+        if (fd >= 0) close(fd);
+    }
+};
+
+// Metadata + header lines of a .vcfc (decompress2_metadata_headers[_fd],
+// reference src/compress.cpp:995-1211): '##' lines then one '#' line, each
+// '\n'-terminated; sample_count = TABs after the 8th on the header line.  A
+// file with no data lines is an error there (the stale first byte '#' after
+// EOF reads as a header row after the header).
+int parse_vcfc_header(const uint8_t *in, uint64_t n, uint64_t *data_off, uint64_t *sample_count) {
+    bool got_meta = false, got_header = false;
+    uint64_t ip = 0, samples = 0;
+    for (;;) {
+        if (ip >= n) return VCFC_E_FORMAT;
+        const uint8_t c1 = in[ip];
+        if (c1 != '#') {
+            if (!got_meta || !got_header) return VCFC_E_FORMAT;
+            break;
+        }
+        if (got_header) return VCFC_E_FORMAT;
+        if (ip + 1 >= n) return VCFC_E_FORMAT;
+        const uint8_t c2 = in[ip + 1];
+        if (c2 == '#') got_meta = true;
+        else { if (!got_meta) return VCFC_E_FORMAT; got_header = true; }
+        uint64_t q = ip + 2, tabs = 0;
+        for (;;) {
+            if (q >= n) return VCFC_E_FORMAT;
+            const uint8_t c3 = in[q++];
+            if (c3 == '\n') break;
+            if (got_header && c3 == '\t' && ++tabs > 8) samples++;
+        }
+        ip = q;
+    }
+    *data_off = ip;
+    if (sample_count) *sample_count = samples;
+    return VCFC_OK;
+}
+
+// Record starts by hopping the LEN headers (read_compressed_line_length_headers,
+// src/compress.cpp:270-331; both headers must carry extension count 3,
+// src/utils.hpp:198-206).  rec[i] = offset of record i from `base`, rec[n] = end.
+int index_records(const uint8_t *base, uint64_t n, std::vector<uint64_t> &rec) {
+    rec.clear();
+    uint64_t ip = 0;
+    while (n - ip >= 8) {
+        const uint8_t *h = base + ip;
+        if ((h[0] >> 6) != 3 || (h[4] >> 6) != 3) return VCFC_E_FORMAT;
+        const uint32_t L = ((uint32_t)(h[0] & 0x3F) << 24) | ((uint32_t)h[1] << 16) | ((uint32_t)h[2] << 8) | h[3];
+        if (L < 4 || n - ip - 8 < (uint64_t)L - 4) return VCFC_E_FORMAT;
+        rec.push_back(ip);
+        ip += 8 + (L - 4);
+    }
+    rec.push_back(ip);
+    return ip == n ? VCFC_OK : VCFC_E_FORMAT;
+}
+
+int write_all_at(int fd, const void *p, uint64_t len, uint64_t off) {
+    const uint8_t *b = static_cast<const uint8_t *>(p);
+    while (len) {
+        ssize_t k = pwrite(fd, b, std::min<uint64_t>(len, 1ull << 30), (off_t)off);
+        if (k <= 0) return VCFC_E_IO;
+        b += k; len -= (uint64_t)k; off += (uint64_t)k;
+    }
+    return VCFC_OK;
+}
+
+void put_be64(uint8_t *o, uint64_t v) {
+    for (int k = 0; k < 8; k++) o[k] = (uint8_t)(v >> (56 - 8 * k));
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -273,6 +372,94 @@ int vcfc_compress_data_line(vcfc_ctx *c, const char *line, uint64_t len, int add
     memcpy(out, tmp.data(), n);
     *out_len = n;
     return VCFC_OK;
+}
+
+uint64_t vcfc_sparse_offset(uint64_t pos) { return (300000000ull + pos) * (4ull * 4096ull); }
+
+int vcfc_sparse_plan_device(const uint8_t *d_recs, const uint64_t *d_rec_off, uint64_t n, uint64_t data_start,
+                            uint64_t *d_file_off, uint8_t *d_prefix16, uint64_t *d_status, void *stream) {
+    if ((n && (!d_recs || !d_rec_off || !d_file_off || !d_prefix16)) || !d_status) return VCFC_E_ARG;
+    return vcfc_sparse_plan_launch(d_recs, d_rec_off, n, data_start, d_file_off, d_prefix16, d_status,
+                                   static_cast<hipStream_t>(stream)) == hipSuccess
+               ? VCFC_OK
+               : VCFC_E_HIP;
+}
+
+// sparsify_file (reference src/sparse.cpp:290-580).  The GPU plans offsets
+// and prefixes; the host writes one pwritev per record (the reference writes
+// one byte per syscall) or, if the plan flags overlapping/out-of-order
+// records, replays the reference's write sequence so later writes win as
+// they do there.
+int vcfc_sparsify_file(vcfc_ctx *c, const char *in_path, const char *out_path) {
+    if (!c || !in_path || !out_path) return VCFC_E_ARG;
+    if (hipSetDevice(c->device) != hipSuccess) return VCFC_E_HIP;
+    MappedFile f;
+    int st = f.open_ro(in_path);
+    if (st) return st;
+    uint64_t data_in = 0;
+    if ((st = parse_vcfc_header(f.p, f.n, &data_in, nullptr))) return st;
+    const uint8_t *recs = f.p + data_in;
+    const uint64_t rbytes = f.n - data_in;
+    std::vector<uint64_t> rec;
+    const int ist = index_records(recs, rbytes, rec);   // error after the good prefix
+    const uint64_t n = rec.size() - 1;
+    const uint64_t data_start = data_in + 8;            // header lines + 8-byte slot
+    std::vector<uint64_t> file_off(n), status(2, 0);
+    std::vector<uint8_t> prefix(16 * n);
+    if (n) {
+        const uint64_t span = rec[n];
+        if (c->in.ensure(span + 64) || c->rec.ensure(8 * (n + 1)) || c->out.ensure(16 * n) ||
+            c->off.ensure(8 * n) || c->err.ensure(16))
+            return VCFC_E_HIP;
+        hipStream_t s = c->stream;
+        if (hipMemcpyAsync(c->in.p, recs, span, hipMemcpyHostToDevice, s) ||
+            hipMemcpyAsync(c->rec.p, rec.data(), 8 * (n + 1), hipMemcpyHostToDevice, s))
+            return VCFC_E_HIP;
+        if (vcfc_sparse_plan_launch(static_cast<uint8_t *>(c->in.p), static_cast<uint64_t *>(c->rec.p), n,
+                                    data_start, static_cast<uint64_t *>(c->off.p), static_cast<uint8_t *>(c->out.p),
+                                    static_cast<uint64_t *>(c->err.p), s) != hipSuccess)
+            return VCFC_E_HIP;
+        if (hipMemcpyAsync(file_off.data(), c->off.p, 8 * n, hipMemcpyDeviceToHost, s) ||
+            hipMemcpyAsync(prefix.data(), c->out.p, 16 * n, hipMemcpyDeviceToHost, s) ||
+            hipMemcpyAsync(status.data(), c->err.p, 16, hipMemcpyDeviceToHost, s) || hipStreamSynchronize(s))
+            return VCFC_E_HIP;
+    }
+    uint64_t upto = n;   // records before the first unparsable one are written
+    if (status[0] != ~0ull && n) upto = status[0] >> 8;
+    int fd = open(out_path, O_CREAT | O_TRUNC | O_RDWR, 0600);
+    if (fd < 0) return VCFC_E_IO;
+    int w = write_all_at(fd, f.p, data_in, 0);
+    const uint8_t zero8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (!w) w = write_all_at(fd, zero8, 8, data_in);
+    const bool replay = status[1] != 0;
+    for (uint64_t i = 0; i < upto && !w; i++) {
+        uint8_t pfx[16];
+        memcpy(pfx, prefix.data() + 16 * i, 16);
+        if (i == 0) {
+            const uint64_t voff = file_off[0] - data_start;   // host byte order (sparse.cpp:511)
+            w = write_all_at(fd, &voff, 8, data_start - 8);
+        } else if (replay) {
+            uint8_t d[8];
+            put_be64(d, file_off[i] - file_off[i - 1]);
+            w = write_all_at(fd, d, 8, file_off[i - 1] + 8);
+        }
+        if (w) break;
+        if (replay) memset(pfx + 8, 0, 8);   // patched by the next record's step
+        struct iovec iov[2] = {{pfx, 16}, {const_cast<uint8_t *>(recs + rec[i]), (size_t)(rec[i + 1] - rec[i])}};
+        const uint64_t want = 16 + rec[i + 1] - rec[i];
+        ssize_t k = pwritev(fd, iov, 2, (off_t)file_off[i]);
+        if (k != (ssize_t)want) {
+            // short write: finish the record plainly
+            std::vector<uint8_t> tmp(want);
+            memcpy(tmp.data(), pfx, 16);
+            memcpy(tmp.data() + 16, recs + rec[i], want - 16);
+            w = write_all_at(fd, tmp.data(), want, file_off[i]);
+        }
+    }
+    close(fd);
+    if (w) return w;
+    if (upto < n) return VCFC_E_FORMAT;
+    return ist;
 }
 
 uint64_t vcfc_compress_bound(uint64_t in_bytes) { return in_bytes + in_bytes / 2 + 64; }

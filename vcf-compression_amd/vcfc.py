@@ -28,6 +28,7 @@ EXPORTS = [
     "vcfc_encode_rows_device", "vcfc_encode_rows", "vcfc_compress_file",
     "vcfc_compress_bound", "vcfc_compress_buffer", "vcfc_synth_rows_device",
     "vcfc_timer_create", "vcfc_timer_destroy", "vcfc_encode_rows_device_timed", "vcfc_timer_read",
+    "vcfc_sparse_offset", "vcfc_sparsify_file", "vcfc_sparse_plan_device",
 ]
 
 
@@ -72,6 +73,10 @@ def lib():
     L.vcfc_timer_destroy.restype = None
     L.vcfc_encode_rows_device_timed.argtypes = [vp, vp, vp, u64, u64, vp, u64, vp, vp, u64, vp, vp, vp]
     L.vcfc_timer_read.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64)]
+    L.vcfc_sparse_offset.restype = u64
+    L.vcfc_sparse_offset.argtypes = [u64]
+    L.vcfc_sparsify_file.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p]
+    L.vcfc_sparse_plan_device.argtypes = [vp, vp, u64, u64, vp, vp, vp, vp]
     L.vcfc_synth_rows_device.argtypes = [vp, vp, u64, vp, vp, vp, u32, ctypes.c_int, u64, vp]
     _lib = L
     return L
@@ -144,6 +149,10 @@ class Context:
         line = ctypes.c_int64(-1)
         st = lib().vcfc_compress_file(self._h, in_path.encode(), out_path.encode(), ctypes.byref(line))
         raise_for(st, "line %d" % line.value)
+
+    def sparsify_file(self, in_path, out_path):
+        """sparsify_file (reference src/sparse.cpp:290-580)."""
+        raise_for(lib().vcfc_sparsify_file(self._h, in_path.encode(), out_path.encode()))
 
     def encode_rows(self, buf, line_off, line_len):
         """Host batch: returns (status, records bytes, rec_off, err_row)."""
