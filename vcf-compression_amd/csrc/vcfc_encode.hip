@@ -76,9 +76,10 @@ __device__ __forceinline__ void ring_put(Ring &r, uint32_t pos, uint32_t b) {
     r.lds[pos & RMASK] = (uint8_t)b;
 }
 
-// Stream complete 1 KiB bursts to the slot.  A chunk adds < 1.3 KiB to a
-// ring holding < 1 KiB, so two unrolled bursts suffice (no loop: a store loop
-// of unknown trip count makes hipcc's vmcnt tracking give up on the prefetch).
+// Stream complete 1 KiB bursts to the slot.  A 2 KiB chunk adds < 2.5 KiB to
+// a ring holding < 1 KiB, so three unrolled bursts suffice (no loop: a store
+// loop of unknown trip count makes hipcc's vmcnt tracking give up on the
+// prefetch).
 __device__ __forceinline__ void ring_burst(Ring &r, uint32_t l) {
     const uint4 v = *reinterpret_cast<const uint4 *>(r.lds + ((r.fpos + 16u * l) & RMASK));
     vw::gstore16(r.slot, r.fpos + 16u * l, v);
@@ -91,7 +92,10 @@ __device__ __forceinline__ void ring_flush(Ring &r, bool final) {
     vw::wave_sync();
     if (r.wpos - r.fpos >= BURST) {
         ring_burst(r, l);
-        if (r.wpos - r.fpos >= BURST) ring_burst(r, l);
+        if (r.wpos - r.fpos >= BURST) {
+            ring_burst(r, l);
+            if (r.wpos - r.fpos >= BURST) ring_burst(r, l);
+        }
     }
     if (final && r.wpos > r.fpos) {
         const uint32_t rem = r.wpos - r.fpos;  // < BURST
@@ -122,15 +126,17 @@ __device__ void ring_finish(Ring &r, uint32_t req) {
 // ---------------------------------------------------------------------------
 // Fast path: clean prefix (no empty fields before the first sample) and a
 // genotype region of 3-byte tokens separated by single TABs -- the shape of
-// every GT-only VCF.  One wave streams the row in 1 KiB aligned chunks: lane l
-// owns bytes [16l, 16l+16) of a chunk plus the next 4 bytes, so the 4 token
-// slots it classifies (slot j starts at 16l + 4j + phi) are complete in its
+// every GT-only VCF.  One wave streams the row in 2 KiB aligned chunks: lane l
+// owns bytes [32l, 32l+32) of a chunk plus the next 4 bytes, so the 8 token
+// slots it classifies (slot j starts at 32l + 4j + phi) are complete in its
 // own registers.  Loads are unconditional (clamped inside the line) so two
 // chunks stay in flight behind counted vmcnt waits.  Returns false (nothing
 // committed) if the row does not have this shape.
+constexpr uint32_t TPL = 8;                 // token slots per lane
+constexpr uint32_t CHUNK = 64 * 4 * TPL;    // bytes per wave iteration (2 KiB)
 
 __device__ __forceinline__ uint32_t cls_mask_f(uint32_t c) { return (0x80C0A000u >> (8 * (c & 3u))) & 0xFFu; }
-// cap-1 (126 or 30) and the exact mod by cap for x < 2^24 (magic = ceil(2^32/cap))
+// exact x mod cap for x < 2^24 (cap 127 for 0|0 runs, 31 otherwise; magic = ceil(2^32/cap))
 __device__ __forceinline__ uint32_t mod_cap(uint32_t x, bool is00) {
     const uint32_t m = is00 ? 33818641u : 138547333u;
     const uint32_t d = is00 ? 127u : 31u;
@@ -141,19 +147,27 @@ __device__ __forceinline__ uint32_t cls_f(uint32_t w) {
     const bool gt = (w & 0xFEFFFEu) == 0x307C30u;
     return gt ? (((w & 1u) << 1) | ((w >> 16) & 1u)) : CLS_ESC;
 }
+// class of a token dword known to be "a|b\t" with a, b in {0,1}
+__device__ __forceinline__ uint32_t cls_classed(uint32_t w) { return ((w & 1u) << 1) | ((w >> 16) & 1u); }
 
 struct Chunk {
-    uint4 w;      // 16 bytes at A + 16*(chunk*64 + lane)
+    uint4 a, b;   // 32 bytes at A + 32*(chunk*64 + lane)
     uint32_t y;   // the 4 bytes after them
+    __device__ __forceinline__ uint32_t w(int k) const {
+        return k == 0 ? a.x : k == 1 ? a.y : k == 2 ? a.z : k == 3 ? a.w : k == 4 ? b.x : k == 5 ? b.y
+             : k == 6 ? b.z : k == 7 ? b.w : y;
+    }
 };
 
 __device__ __forceinline__ Chunk load_chunk(const uint8_t *A, uint32_t c, uint32_t l, uint32_t last_blk) {
-    uint32_t b = c * 64u + l;
-    b = b < last_blk ? b : last_blk;
+    const uint32_t b0 = c * (CHUNK / 16) + 2u * l;
+    const uint32_t c0 = b0 < last_blk ? b0 : last_blk;
+    const uint32_t c1 = b0 + 1 < last_blk ? b0 + 1 : last_blk;
+    const uint32_t c2 = b0 + 2 < last_blk ? b0 + 2 : last_blk;
     Chunk k;
-    k.w = vw::gload16(A, b);
-    const uint32_t b2 = b + 1 < last_blk ? b + 1 : last_blk;
-    k.y = vw::gload4(A, 4u * b2);
+    k.a = vw::gload16(A, c0);
+    k.b = vw::gload16(A, c1);
+    k.y = vw::gload4(A, 4u * c2);
     return k;
 }
 
@@ -170,70 +184,65 @@ struct FastState {
 __device__ __forceinline__ int fast_prefix_step(const Chunk &cur, uint32_t c, uint32_t lead, uint32_t len,
                                                 FastState &f, Ring &r) {
     const uint32_t l = vw::lane_id();
-    const uint32_t bo = c * BURST + 16u * l;
+    const uint32_t bo = c * CHUNK + 32u * l;
     const int32_t x0 = (int32_t)bo - (int32_t)lead;   // line offset of the lane's byte 0
-    uint32_t &nf = f.nf;
-    uint32_t &carryT = f.carryT;
-    // ---- prefix: locate the 10th field start, reject empty fields ----
-    const int32_t vlo = x0 >= 0 ? 0 : (-x0 >= 16 ? 16 : -x0);
+    // ---- locate the 10th field start, reject empty fields ----
+    const int32_t vlo = x0 >= 0 ? 0 : (-x0 >= 32 ? 32 : -x0);
     const int32_t vhi0 = (int32_t)len - x0;
-    const int32_t vhi = vhi0 <= 0 ? 0 : (vhi0 >= 16 ? 16 : vhi0);
-    const uint32_t vm = vhi > vlo ? (((1u << vhi) - 1u) ^ ((1u << vlo) - 1u)) : 0u;
-    const uint32_t m = tab_mask16(cur.w) & vm;
-    const uint32_t Tm = (m | ~vm) & 0xFFFFu;
-    const uint32_t pin = vw::shr1((Tm >> 15) & 1u, carryT);
-    const uint32_t prevT = ((Tm << 1) | pin) & 0xFFFFu;
-    const uint32_t fs = ~Tm & prevT & 0xFFFFu;     // field starts
-    const uint32_t et = m & prevT;                 // TAB closing an empty field
-    carryT = vw::readlane((Tm >> 15) & 1u, 63);
+    const int32_t vhi = vhi0 <= 0 ? 0 : (vhi0 >= 32 ? 32 : vhi0);
+    const uint32_t vm = vhi > vlo ? (uint32_t)(((1ull << vhi) - 1ull) ^ ((1ull << vlo) - 1ull)) : 0u;
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) m |= zero_bytes4(cur.w(k) ^ 0x09090909u) << (4 * k);
+    m &= vm;
+    const uint32_t Tm = m | ~vm;                    // TAB or outside the line
+    const uint32_t pin = vw::shr1(Tm >> 31, f.carryT);
+    const uint32_t prevT = (Tm << 1) | pin;
+    const uint32_t fs = ~Tm & prevT;                // field starts
+    const uint32_t et = m & prevT;                  // TAB closing an empty field
+    f.carryT = vw::readlane(Tm >> 31, 63);
     const uint32_t cnt = (uint32_t)__builtin_popcount(fs);
     const uint32_t inc = vw::scan_add(cnt);
     const uint32_t exc = inc - cnt;
-    const bool has9 = nf + exc <= 9 && 9 < nf + inc;
+    const bool has9 = f.nf + exc <= 9 && 9 < f.nf + inc;
     uint32_t x9 = 0;
     if (has9) {
         uint32_t mm = fs;
-        for (uint32_t k = nf + exc; k < 9; k++) mm &= mm - 1;
+        for (uint32_t k = f.nf + exc; k < 9; k++) mm &= mm - 1;
         x9 = (uint32_t)(x0 + __builtin_ctz(mm));
     }
     const uint64_t hb = vw::ballot(has9);
     if (hb) x9 = vw::readlane(x9, (uint32_t)__builtin_ctzll(hb));
-    uint32_t below = 0xFFFFu;
+    uint32_t below = ~0u;
     if (hb) {
         const int32_t d = (int32_t)x9 - x0;
-        below = d <= 0 ? 0u : d >= 16 ? 0xFFFFu : ((1u << d) - 1u);
+        below = d <= 0 ? 0u : d >= 32 ? ~0u : ((1u << d) - 1u);
     }
     if (vw::ballot((et & below) != 0)) return 2;
-    // prefix bytes -> ring[8 + x]: realign the lane's bytes to ring
-    // dwords (ring position of lane byte i is bo + i + 8 - lead); bytes
-    // outside [0, x9) land below 8 (header, rewritten) or at >= wpos
-    // (free, overwritten later) -- written before this chunk's tokens.
+    // prefix bytes -> ring[8 + x]: realign the lane's bytes to ring dwords
+    // (ring position of lane byte i is bo + i + 8 - lead); bytes outside
+    // [0, x9) land below 8 (header, rewritten) or at >= wpos (free,
+    // overwritten later) -- written before this chunk's tokens.
     {
-        const uint32_t e = (8u - lead) & 3u;           // ring pos = bo + i + (dq + e)
+        const uint32_t e = (8u - lead) & 3u;
         const int32_t dq = (int32_t)(8u - lead) - (int32_t)e;
-        const uint32_t pw = vw::shr1(cur.w.w, 0u);
+        const uint32_t pw = vw::shr1(cur.b.w, 0u);
         const uint32_t sh = (4u - e) & 3u;
-        uint32_t o0, o1, o2, o3, o4;
-        if (e == 0) { o0 = cur.w.x; o1 = cur.w.y; o2 = cur.w.z; o3 = cur.w.w; o4 = 0; }
-        else {
-            o0 = vw::alignbyte(cur.w.x, pw, sh);
-            o1 = vw::alignbyte(cur.w.y, cur.w.x, sh);
-            o2 = vw::alignbyte(cur.w.z, cur.w.y, sh);
-            o3 = vw::alignbyte(cur.w.w, cur.w.z, sh);
-            o4 = vw::alignbyte(cur.y, cur.w.w, sh);
-        }
-        // dword k holds ring bytes [bo + dq + 4k, +4)
         uint32_t *rd = reinterpret_cast<uint32_t *>(r.lds);
         const uint32_t base = (uint32_t)((int32_t)bo + dq);
-        if (e == 0 || l != 0) rd[((base + 0) & RMASK) >> 2] = o0;   // lane 0's was written by lane 63 before
-        rd[((base + 4) & RMASK) >> 2] = o1;
-        rd[((base + 8) & RMASK) >> 2] = o2;
-        rd[((base + 12) & RMASK) >> 2] = o3;
-        if (e != 0 && l == 63) rd[((base + 16) & RMASK) >> 2] = o4;
+        // dword k holds ring bytes [base + 4k, +4) = lane bytes [4k - e, 4k - e + 4)
+#pragma unroll
+        for (int k = 0; k < 9; k++) {
+            const uint32_t lo = k == 0 ? pw : cur.w(k - 1);
+            const uint32_t hi = k == 8 ? cur.y : cur.w(k);
+            const uint32_t o = e == 0 ? (k == 8 ? 0u : cur.w(k)) : vw::alignbyte(hi, lo, sh);
+            const bool wr = e == 0 ? (k < 8) : (k == 8 ? l == 63 : (k != 0 || l != 0));
+            if (wr) rd[((base + 4u * k) & RMASK) >> 2] = o;   // lane 0's k=0 dword: written by lane 63 before
+        }
     }
-    nf += vw::readlane(inc, 63);
+    f.nf += vw::readlane(inc, 63);
     if (!hb) {
-        const int32_t upto = (int32_t)((c + 1) * BURST) - (int32_t)lead;
+        const int32_t upto = (int32_t)((c + 1) * CHUNK) - (int32_t)lead;
         r.wpos = 8u + umin32(len, upto <= 0 ? 0u : (uint32_t)upto);
         ring_flush(r, false);
         return 0;   // (if this was the last chunk: < 10 fields -> general path)
@@ -251,126 +260,178 @@ __device__ __forceinline__ int fast_prefix_step(const Chunk &cur, uint32_t c, ui
 // Genotype tokens whose first byte lies in chunk c; false = not the fast shape.
 __device__ __forceinline__ bool fast_gt_step(const Chunk &cur, uint32_t c, uint32_t lead, FastState &f, Ring &r) {
     const uint32_t l = vw::lane_id();
-    const int32_t x0 = (int32_t)(c * BURST + 16u * l) - (int32_t)lead;
+    const int32_t x0 = (int32_t)(c * CHUNK + 32u * l) - (int32_t)lead;
     const uint32_t T = f.T, phi = f.phi;
     constexpr uint32_t Z = 0x09307C30u;   // "0|0\t"
-    uint32_t d[4];
-    d[0] = vw::alignbyte(cur.w.y, cur.w.x, phi);
-    d[1] = vw::alignbyte(cur.w.z, cur.w.y, phi);
-    d[2] = vw::alignbyte(cur.w.w, cur.w.z, phi);
-    d[3] = vw::alignbyte(cur.y, cur.w.w, phi);
+    uint32_t d[TPL];
+#pragma unroll
+    for (int j = 0; j < (int)TPL; j++) d[j] = vw::alignbyte(cur.w(j + 1), cur.w(j), phi);
     const int32_t t0 = (x0 + (int32_t)phi - f.gt0) >> 2;   // token index of slot 0 (exact)
-    bool v[4];
-#pragma unroll
-    for (int j = 0; j < 4; j++) v[j] = (uint32_t)(t0 + j) < T;
-
-    // whole chunk inside one 0|0 run: only full 127-chunks can complete
-    const bool z = v[0] & v[1] & v[2] & v[3] & (d[0] == Z) & (d[1] == Z) & (d[2] == Z) & (d[3] == Z);
-    if (f.pcls == 0 && vw::ballot(z) == ~0ull) {
-        const uint32_t tb = (uint32_t)vw::readfirst((uint32_t)t0);   // lane 0's first token
-        // token t has run offset o = t + 1 - prs; it completes a 127-chunk
-        // when (o + 1) % 127 == 0: count multiples of 127 in [a0+1, a0+256]
-        const uint32_t a0 = tb + 1 - f.prs;
-        const uint32_t kfull = (a0 + 256) / 127 - a0 / 127;
-        if (l < kfull) ring_put(r, r.wpos + l, 0x7Fu);
-        r.wpos += kfull;
-        ring_flush(r, false);
-        return true;
-    }
-
-    // classes.  "a|b\t" with a, b in {0,1} is a classed token whose shape is
-    // already right; any other valid slot (an escape, or the row's last token
-    // which has no TAB after it) gets the full shape check.
-    uint32_t cl[4];
-    bool odd = false;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const bool isc = (d[j] & 0xFFFEFFFEu) == Z;
-        cl[j] = !v[j] ? CLS_NONE : isc ? (((d[j] & 1u) << 1) | ((d[j] >> 16) & 1u)) : CLS_ESC;
-        odd |= v[j] && !isc;
-    }
-    if (vw::ballot(odd)) {
-        bool bad = false;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            if (cl[j] == CLS_ESC) {
-                const uint32_t x = d[j] ^ 0x09090909u;
-                const uint32_t zb = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
-                const bool last = (uint32_t)(t0 + j) + 1 == T;
-                bad |= (zb & 0x00808080u) != 0 || ((zb >> 31) == 0 && !last);
-                cl[j] = cls_f(d[j]);   // the last token may still be a classed one
-            }
-        }
-        if (vw::ballot(bad)) return false;
-    }
-
-    // previous-token class, run starts (t+1 encoded, 0 = none)
-    uint32_t p[4];
-    p[0] = vw::shr1(cl[3], f.pcls);
-    p[1] = cl[0];
-    p[2] = cl[1];
-    p[3] = cl[2];
-    bool s[4];
-#pragma unroll
-    for (int j = 0; j < 4; j++) s[j] = v[j] && (cl[j] != p[j] || cl[j] == CLS_ESC);
     const uint32_t u0 = (uint32_t)(t0 + 1);
-    const uint32_t lane_rs = s[3] ? u0 + 3 : s[2] ? u0 + 2 : s[1] ? u0 + 1 : s[0] ? u0 : 0u;
-    const uint32_t rin = vw::umax(vw::shr1(vw::scan_max(lane_rs), 0u), f.prs);
-    // run offset (mod cap) of the token before slot 0, then incremental
-    uint32_t mp = mod_cap((uint32_t)t0 - rin, p[0] == 0);
-    bool tab[4], pend[4], full[4];
-    uint32_t pb[4], nb[4];
-    uint32_t lane_sum = 0, lrs = rin;
+    // chunk-level shape (wave-uniform): every slot inside [0, T)?
+    const int32_t tf = ((int32_t)(c * CHUNK) + (int32_t)phi - (int32_t)lead - f.gt0) >> 2;
+    const bool full_range = tf >= 0 && (uint32_t)tf + 64 * TPL <= T;
+    const uint32_t dummy = RING + l;
+
+    if (full_range && f.pcls < CLS_ESC) {
+        bool allz = true, allc = true;
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const uint32_t pj = p[j], cj = cl[j];
+        for (int j = 0; j < (int)TPL; j++) {
+            allz &= d[j] == Z;
+            allc &= (d[j] & 0xFFFEFFFEu) == Z;
+        }
+        if (f.pcls == 0 && vw::ballot(!allz) == 0) {
+            // one 0|0 run through the whole chunk: only full 127-chunks complete.
+            // token t has run offset o = t + 1 - prs; count multiples of 127 in
+            // [a0 + 1, a0 + 512], a0 = offset of the chunk's first token
+            const uint32_t a0 = (uint32_t)tf + 1 - f.prs;
+            const uint32_t kfull = (a0 + 64 * TPL) / 127 - a0 / 127;
+            if (l < kfull) ring_put(r, r.wpos + l, 0x7Fu);
+            r.wpos += kfull;
+            ring_flush(r, false);
+            return true;
+        }
+        if (vw::ballot(!allc) == 0) {
+            // ---- clean chunk: every slot a classed token "a|b\t" ----
+            uint32_t cl[TPL];
+#pragma unroll
+            for (int j = 0; j < (int)TPL; j++) cl[j] = cls_classed(d[j]);
+            uint32_t p0 = vw::shr1(cl[TPL - 1], f.pcls);
+            uint32_t lane_rs = 0;
+#pragma unroll
+            for (int j = 0; j < (int)TPL; j++) {
+                const uint32_t pj = j == 0 ? p0 : cl[j - 1];
+                if (cl[j] != pj) lane_rs = u0 + j;
+            }
+            const uint32_t rin = vw::umax(vw::shr1(vw::scan_max(lane_rs), 0u), f.prs);
+            uint32_t mp = mod_cap((uint32_t)t0 - rin, p0 == 0);
+            uint32_t pend_m = 0, full_m = 0, pbs[TPL];
+            uint32_t lane_sum = 0;
+#pragma unroll
+            for (int j = 0; j < (int)TPL; j++) {
+                const uint32_t pj = j == 0 ? p0 : cl[j - 1], cj = cl[j];
+                const bool s = cj != pj;
+                const uint32_t capm1_p = pj == 0 ? 126u : 30u, capm1_c = cj == 0 ? 126u : 30u;
+                const bool pend = s && mp != capm1_p;
+                pbs[j] = cls_mask_f(pj) | (mp + 1);
+                const uint32_t m = s ? 0u : (mp == capm1_c ? 0u : mp + 1);
+                const bool full = m == capm1_c;
+                pend_m |= (pend ? 1u : 0u) << j;
+                full_m |= (full ? 1u : 0u) << j;
+                lane_sum += (pend ? 1u : 0u) + (full ? 1u : 0u);
+                mp = m;
+            }
+            const uint32_t incl = vw::scan_add(lane_sum);
+            uint32_t pos = r.wpos + incl - lane_sum;
+#pragma unroll
+            for (int j = 0; j < (int)TPL; j++) {
+                const bool pend = (pend_m >> j) & 1u, full = (full_m >> j) & 1u;
+                r.lds[pend ? (pos & RMASK) : dummy] = (uint8_t)pbs[j];
+                pos += pend ? 1u : 0u;
+                r.lds[full ? (pos & RMASK) : dummy] = (uint8_t)(cls_mask_f(cl[j]) | (cl[j] == 0 ? 127u : 31u));
+                pos += full ? 1u : 0u;
+            }
+            r.wpos += vw::readlane(incl, 63);
+            // carry the chunk's last token (lane 63, slot TPL-1)
+            uint32_t lrs = rin;
+#pragma unroll
+            for (int j = 0; j < (int)TPL; j++)
+                if (cl[j] != (j == 0 ? p0 : cl[j - 1])) lrs = u0 + j;
+            f.pcls = vw::readlane(cl[TPL - 1], 63);
+            f.prs = vw::readlane(lrs, 63);
+            ring_flush(r, false);
+            return true;
+        }
+    }
+
+    // ---- general chunk: row start/end, escapes ----
+    bool v[TPL];
+#pragma unroll
+    for (int j = 0; j < (int)TPL; j++) v[j] = (uint32_t)(t0 + j) < T;
+    uint32_t cl[TPL];
+    bool bad = false;
+#pragma unroll
+    for (int j = 0; j < (int)TPL; j++) {
+        const bool isc = (d[j] & 0xFFFEFFFEu) == Z;
+        cl[j] = !v[j] ? CLS_NONE : isc ? cls_classed(d[j]) : CLS_ESC;
+        if (cl[j] == CLS_ESC) {
+            // an escape, or the row's last token (no TAB after it): full check
+            const uint32_t x = d[j] ^ 0x09090909u;
+            const uint32_t zb = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
+            const bool last = (uint32_t)(t0 + j) + 1 == T;
+            bad |= (zb & 0x00808080u) != 0 || ((zb >> 31) == 0 && !last);
+            cl[j] = cls_f(d[j]);
+        }
+    }
+    if (vw::ballot(bad)) return false;
+    const uint32_t p0 = vw::shr1(cl[TPL - 1], f.pcls);
+    uint32_t lane_rs = 0;
+#pragma unroll
+    for (int j = 0; j < (int)TPL; j++) {
+        const uint32_t pj = j == 0 ? p0 : cl[j - 1];
+        const bool s = cl[j] != CLS_NONE && (cl[j] != pj || cl[j] == CLS_ESC);
+        if (s) lane_rs = u0 + j;
+    }
+    const uint32_t rin = vw::umax(vw::shr1(vw::scan_max(lane_rs), 0u), f.prs);
+    uint32_t mp = mod_cap((uint32_t)t0 - rin, p0 == 0);
+    uint32_t lane_sum = 0, lrs = rin;
+    uint32_t e1_m = 0, full_m = 0, b1s[TPL];
+#pragma unroll
+    for (int j = 0; j < (int)TPL; j++) {
+        const uint32_t pj = j == 0 ? p0 : cl[j - 1], cj = cl[j];
+        const bool s = cj != CLS_NONE && (cj != pj || cj == CLS_ESC);
         const uint32_t capm1_p = pj == 0 ? 126u : 30u, capm1_c = cj == 0 ? 126u : 30u;
-        tab[j] = v[j] && pj == CLS_ESC;
-        pend[j] = s[j] && pj < CLS_ESC && mp != capm1_p;
-        pb[j] = cls_mask_f(pj) | (mp + 1);
-        const uint32_t m = s[j] ? 0u : (mp == capm1_c ? 0u : mp + 1);
-        full[j] = cj < CLS_ESC && m == capm1_c;
-        nb[j] = ((tab[j] | pend[j]) ? 1u : 0u) + (cj == CLS_ESC ? 4u : (full[j] ? 1u : 0u));
-        lane_sum += nb[j];
+        const bool tab = cj != CLS_NONE && pj == CLS_ESC;
+        const bool pend = s && pj < CLS_ESC && mp != capm1_p;
+        b1s[j] = tab ? 0x09u : (cls_mask_f(pj) | (mp + 1));
+        const uint32_t m = s ? 0u : (mp == capm1_c ? 0u : mp + 1);
+        const bool full = cj < CLS_ESC && m == capm1_c;
+        e1_m |= ((tab | pend) ? 1u : 0u) << j;
+        full_m |= (full ? 1u : 0u) << j;
+        lane_sum += ((tab | pend) ? 1u : 0u) + (cj == CLS_ESC ? 4u : (full ? 1u : 0u));
         mp = m;
-        if (s[j]) lrs = u0 + j;
+        if (s) lrs = u0 + j;
     }
     const uint32_t incl = vw::scan_add(lane_sum);
-    // emission: the common bytes (TAB / pending run byte, full-chunk byte) are
-    // stored unconditionally -- to a per-lane dummy cell when absent -- so no
-    // branches; escape payloads (rare) in a separate pass
-    const uint32_t dummy = RING + l;
     const uint32_t pos0 = r.wpos + incl - lane_sum;
     uint32_t pos = pos0;
+    bool any_esc = false;
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const bool e1 = tab[j] | pend[j];
-        r.lds[e1 ? (pos & RMASK) : dummy] = (uint8_t)(tab[j] ? 0x09u : pb[j]);
+    for (int j = 0; j < (int)TPL; j++) {
+        const bool e1 = (e1_m >> j) & 1u, full = (full_m >> j) & 1u;
+        r.lds[e1 ? (pos & RMASK) : dummy] = (uint8_t)b1s[j];
         pos += e1 ? 1u : 0u;
-        r.lds[full[j] ? (pos & RMASK) : dummy] = (uint8_t)(cls_mask_f(cl[j]) | (cl[j] == 0 ? 127u : 31u));
-        pos += cl[j] == CLS_ESC ? 4u : (full[j] ? 1u : 0u);
+        r.lds[full ? (pos & RMASK) : dummy] = (uint8_t)(cls_mask_f(cl[j]) | (cl[j] == 0 ? 127u : 31u));
+        pos += cl[j] == CLS_ESC ? 4u : (full ? 1u : 0u);
+        any_esc |= cl[j] == CLS_ESC;
     }
-    if (vw::ballot(cl[0] == CLS_ESC || cl[1] == CLS_ESC || cl[2] == CLS_ESC || cl[3] == CLS_ESC)) {
+    if (vw::ballot(any_esc)) {
         // escape payloads: walk the lane's tokens again for their positions
         pos = pos0;
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            pos += (tab[j] | pend[j]) ? 1u : 0u;
+        for (int j = 0; j < (int)TPL; j++) {
+            pos += ((e1_m >> j) & 1u);
             if (cl[j] == CLS_ESC) {
                 ring_put(r, pos, 0xE1u);
                 ring_put(r, pos + 1, d[j] & 0xFFu);
                 ring_put(r, pos + 2, (d[j] >> 8) & 0xFFu);
                 ring_put(r, pos + 3, (d[j] >> 16) & 0xFFu);
             }
-            pos += cl[j] == CLS_ESC ? 4u : (full[j] ? 1u : 0u);
+            pos += cl[j] == CLS_ESC ? 4u : ((full_m >> j) & 1u);
         }
     }
     r.wpos += vw::readlane(incl, 63);
     // carry the chunk's last token (class, run start)
-    const uint64_t hv = vw::ballot(v[0] | v[1] | v[2] | v[3]);
+    bool anyv = false;
+    uint32_t lc = CLS_NONE;
+#pragma unroll
+    for (int j = 0; j < (int)TPL; j++) {
+        anyv |= v[j];
+        if (v[j]) lc = cl[j];
+    }
+    const uint64_t hv = vw::ballot(anyv);
     if (hv) {
         const uint32_t src = (uint32_t)vw::hibit64(hv);
-        const uint32_t lc = v[3] ? cl[3] : v[2] ? cl[2] : v[1] ? cl[1] : cl[0];
         f.pcls = vw::readlane(lc, src);
         f.prs = vw::readlane(lrs, src);
     }
@@ -385,7 +446,7 @@ __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring
     const uint32_t span = lead + len;
     if (len == 0) return false;
     const uint32_t last_blk = (span - 1) >> 4;   // last 16-byte block holding line bytes
-    const uint32_t nch = (span + BURST - 1) / BURST;
+    const uint32_t nch = (span + CHUNK - 1) / CHUNK;
     FastState f;
     f.nf = 0; f.carryT = 1; f.gt0 = -1; f.T = 0; f.phi = 0; f.pcls = CLS_NONE; f.prs = 0;
     r.wpos = 8;
@@ -580,7 +641,7 @@ __device__ __forceinline__ bool row_setup(const VcfcEncodeArgs &a, uint64_t row,
 
 // Fast kernel: one wave per row; rows without the GT-only shape are queued
 // for k_encode_general.
-__global__ __launch_bounds__(256, 8) void k_encode_fast(VcfcEncodeArgs a) {
+__global__ __launch_bounds__(256) void k_encode_fast(VcfcEncodeArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[K1_WAVES * RING_STRIDE];
     const uint32_t wave = vw::readfirst(threadIdx.x >> 6);   // wave-uniform: scalar row/len/loop control
     const uint64_t row = (uint64_t)blockIdx.x * K1_WAVES + wave;
