@@ -132,8 +132,9 @@ __device__ void ring_finish(Ring &r, uint32_t req) {
 // own registers.  Loads are unconditional (clamped inside the line) so two
 // chunks stay in flight behind counted vmcnt waits.  Returns false (nothing
 // committed) if the row does not have this shape.
-constexpr uint32_t TPL = 8;                 // token slots per lane
-constexpr uint32_t CHUNK = 64 * 4 * TPL;    // bytes per wave iteration (2 KiB)
+constexpr uint32_t TPL = 4;                 // token slots per lane
+constexpr uint32_t BPL = 4 * TPL;           // bytes per lane per chunk
+constexpr uint32_t CHUNK = 64 * BPL;        // bytes per wave iteration (1 KiB)
 
 __device__ __forceinline__ uint32_t cls_mask_f(uint32_t c) { return (0x80C0A000u >> (8 * (c & 3u))) & 0xFFu; }
 // exact x mod cap for x < 2^24 (cap 127 for 0|0 runs, 31 otherwise; magic = ceil(2^32/cap))
@@ -151,23 +152,20 @@ __device__ __forceinline__ uint32_t cls_f(uint32_t w) {
 __device__ __forceinline__ uint32_t cls_classed(uint32_t w) { return ((w & 1u) << 1) | ((w >> 16) & 1u); }
 
 struct Chunk {
-    uint4 a, b;   // 32 bytes at A + 32*(chunk*64 + lane)
+    uint4 a;      // BPL = 16 bytes at A + 16*(chunk*64 + lane)
     uint32_t y;   // the 4 bytes after them
     __device__ __forceinline__ uint32_t w(int k) const {
-        return k == 0 ? a.x : k == 1 ? a.y : k == 2 ? a.z : k == 3 ? a.w : k == 4 ? b.x : k == 5 ? b.y
-             : k == 6 ? b.z : k == 7 ? b.w : y;
+        return k == 0 ? a.x : k == 1 ? a.y : k == 2 ? a.z : k == 3 ? a.w : y;
     }
 };
 
 __device__ __forceinline__ Chunk load_chunk(const uint8_t *A, uint32_t c, uint32_t l, uint32_t last_blk) {
-    const uint32_t b0 = c * (CHUNK / 16) + 2u * l;
+    const uint32_t b0 = c * (CHUNK / 16) + l;
     const uint32_t c0 = b0 < last_blk ? b0 : last_blk;
     const uint32_t c1 = b0 + 1 < last_blk ? b0 + 1 : last_blk;
-    const uint32_t c2 = b0 + 2 < last_blk ? b0 + 2 : last_blk;
     Chunk k;
     k.a = vw::gload16(A, c0);
-    k.b = vw::gload16(A, c1);
-    k.y = vw::gload4(A, 4u * c2);
+    k.y = vw::gload4(A, 4u * c1);
     return k;
 }
 
@@ -184,23 +182,24 @@ struct FastState {
 __device__ __forceinline__ int fast_prefix_step(const Chunk &cur, uint32_t c, uint32_t lead, uint32_t len,
                                                 FastState &f, Ring &r) {
     const uint32_t l = vw::lane_id();
-    const uint32_t bo = c * CHUNK + 32u * l;
+    const uint32_t bo = c * CHUNK + BPL * l;
     const int32_t x0 = (int32_t)bo - (int32_t)lead;   // line offset of the lane's byte 0
+    constexpr uint32_t FULLM = (uint32_t)((1ull << BPL) - 1ull);
     // ---- locate the 10th field start, reject empty fields ----
-    const int32_t vlo = x0 >= 0 ? 0 : (-x0 >= 32 ? 32 : -x0);
+    const int32_t vlo = x0 >= 0 ? 0 : (-x0 >= (int32_t)BPL ? (int32_t)BPL : -x0);
     const int32_t vhi0 = (int32_t)len - x0;
-    const int32_t vhi = vhi0 <= 0 ? 0 : (vhi0 >= 32 ? 32 : vhi0);
+    const int32_t vhi = vhi0 <= 0 ? 0 : (vhi0 >= (int32_t)BPL ? (int32_t)BPL : vhi0);
     const uint32_t vm = vhi > vlo ? (uint32_t)(((1ull << vhi) - 1ull) ^ ((1ull << vlo) - 1ull)) : 0u;
     uint32_t m = 0;
 #pragma unroll
-    for (int k = 0; k < 8; k++) m |= zero_bytes4(cur.w(k) ^ 0x09090909u) << (4 * k);
+    for (int k = 0; k < (int)TPL; k++) m |= zero_bytes4(cur.w(k) ^ 0x09090909u) << (4 * k);
     m &= vm;
-    const uint32_t Tm = m | ~vm;                    // TAB or outside the line
-    const uint32_t pin = vw::shr1(Tm >> 31, f.carryT);
-    const uint32_t prevT = (Tm << 1) | pin;
-    const uint32_t fs = ~Tm & prevT;                // field starts
+    const uint32_t Tm = (m | ~vm) & FULLM;          // TAB or outside the line
+    const uint32_t pin = vw::shr1(Tm >> (BPL - 1), f.carryT);
+    const uint32_t prevT = ((Tm << 1) | pin) & FULLM;
+    const uint32_t fs = ~Tm & prevT & FULLM;        // field starts
     const uint32_t et = m & prevT;                  // TAB closing an empty field
-    f.carryT = vw::readlane(Tm >> 31, 63);
+    f.carryT = vw::readlane(Tm >> (BPL - 1), 63);
     const uint32_t cnt = (uint32_t)__builtin_popcount(fs);
     const uint32_t inc = vw::scan_add(cnt);
     const uint32_t exc = inc - cnt;
@@ -216,7 +215,7 @@ __device__ __forceinline__ int fast_prefix_step(const Chunk &cur, uint32_t c, ui
     uint32_t below = ~0u;
     if (hb) {
         const int32_t d = (int32_t)x9 - x0;
-        below = d <= 0 ? 0u : d >= 32 ? ~0u : ((1u << d) - 1u);
+        below = d <= 0 ? 0u : d >= (int32_t)BPL ? ~0u : ((1u << d) - 1u);
     }
     if (vw::ballot((et & below) != 0)) return 2;
     // prefix bytes -> ring[8 + x]: realign the lane's bytes to ring dwords
@@ -226,17 +225,17 @@ __device__ __forceinline__ int fast_prefix_step(const Chunk &cur, uint32_t c, ui
     {
         const uint32_t e = (8u - lead) & 3u;
         const int32_t dq = (int32_t)(8u - lead) - (int32_t)e;
-        const uint32_t pw = vw::shr1(cur.b.w, 0u);
+        const uint32_t pw = vw::shr1(cur.w(TPL - 1), 0u);
         const uint32_t sh = (4u - e) & 3u;
         uint32_t *rd = reinterpret_cast<uint32_t *>(r.lds);
         const uint32_t base = (uint32_t)((int32_t)bo + dq);
         // dword k holds ring bytes [base + 4k, +4) = lane bytes [4k - e, 4k - e + 4)
 #pragma unroll
-        for (int k = 0; k < 9; k++) {
+        for (int k = 0; k <= (int)TPL; k++) {
             const uint32_t lo = k == 0 ? pw : cur.w(k - 1);
-            const uint32_t hi = k == 8 ? cur.y : cur.w(k);
-            const uint32_t o = e == 0 ? (k == 8 ? 0u : cur.w(k)) : vw::alignbyte(hi, lo, sh);
-            const bool wr = e == 0 ? (k < 8) : (k == 8 ? l == 63 : (k != 0 || l != 0));
+            const uint32_t hi = cur.w(k);   // w(TPL) = y
+            const uint32_t o = e == 0 ? cur.w(k) : vw::alignbyte(hi, lo, sh);
+            const bool wr = e == 0 ? (k < (int)TPL) : (k == (int)TPL ? l == 63 : (k != 0 || l != 0));
             if (wr) rd[((base + 4u * k) & RMASK) >> 2] = o;   // lane 0's k=0 dword: written by lane 63 before
         }
     }
@@ -260,7 +259,7 @@ __device__ __forceinline__ int fast_prefix_step(const Chunk &cur, uint32_t c, ui
 // Genotype tokens whose first byte lies in chunk c; false = not the fast shape.
 __device__ __forceinline__ bool fast_gt_step(const Chunk &cur, uint32_t c, uint32_t lead, FastState &f, Ring &r) {
     const uint32_t l = vw::lane_id();
-    const int32_t x0 = (int32_t)(c * CHUNK + 32u * l) - (int32_t)lead;
+    const int32_t x0 = (int32_t)(c * CHUNK + BPL * l) - (int32_t)lead;
     const uint32_t T = f.T, phi = f.phi;
     constexpr uint32_t Z = 0x09307C30u;   // "0|0\t"
     uint32_t d[TPL];
