@@ -39,6 +39,28 @@ inline uint32_t scan_max(uint32_t v) {
 inline uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t s) {
     return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * (s & 3)));
 }
+inline uint32_t perm(uint32_t s0, uint32_t s1, uint32_t sel) {
+    const uint64_t v = ((uint64_t)s0 << 32) | s1;
+    uint32_t r = 0;
+    for (int i = 0; i < 4; i++) {
+        const uint32_t k = (sel >> (8 * i)) & 0xFFu;
+        uint32_t b;
+        if (k < 8) b = (uint32_t)(v >> (8 * k)) & 0xFFu;
+        else if (k == 8) b = (s1 >> 15) & 1 ? 0xFFu : 0u;
+        else if (k == 9) b = (s1 >> 31) & 1 ? 0xFFu : 0u;
+        else if (k == 10) b = (s0 >> 15) & 1 ? 0xFFu : 0u;
+        else if (k == 11) b = (s0 >> 31) & 1 ? 0xFFu : 0u;
+        else if (k == 12) b = 0u;
+        else b = 0xFFu;
+        r |= b << (8 * i);
+    }
+    return r;
+}
+inline uint32_t alignbit(uint32_t hi, uint32_t lo, uint32_t s) {
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> (s & 31));
+}
+inline int32_t sext24(int32_t v) { return (int32_t)((uint32_t)v << 8) >> 8; }
+inline int32_t mad24(int32_t a, int32_t b, int32_t x) { return (int32_t)((uint32_t)x + (uint32_t)(sext24(a) * sext24(b))); }
 inline void wave_sync() { emu::collective(emu::OP_WAVESYNC, 0, 0, 0); }
 inline int popc64(uint64_t m) { return __builtin_popcountll(m); }
 inline int hibit64(uint64_t m) { return 63 - __builtin_clzll(m); }

@@ -111,3 +111,29 @@ def test_chr22_like_rows_skip_path(seed):
     assert err == (1 << 64) - 1
     for i, ln in enumerate(lines):
         assert out[int(ro[i]):int(ro[i + 1])] == G.oracle_encode_line(ln)[1], i
+
+
+@pytest.mark.parametrize("seed", [21, 22, 23])
+def test_short_rows_and_cap_boundaries(seed):
+    """Rows whose first and last genotype chunk coincide (< 256 samples), and
+    runs whose lengths sit on and around the caps (31, 127) and the 256-slot
+    chunk, at every class: the first/last-chunk masking and the in-lane
+    full/pending byte rules."""
+    rnd = random.Random(seed)
+    classes = [b"0|0", b"0|1", b"1|0", b"1|1"]
+    lens = [1, 2, 3, 4, 5, 29, 30, 31, 32, 33, 61, 62, 63, 125, 126, 127, 128, 129, 253, 254, 255, 256, 257]
+    lines = []
+    for i in range(48):
+        toks = []
+        target = rnd.choice([1, 2, 3, 4, 5, 63, 64, 65, 255, 256, 257, 700, 1500])
+        while len(toks) < target:
+            c = rnd.choice(classes)
+            toks += [c] * rnd.choice(lens)
+        toks = toks[:target]
+        pfx = b"22\t%d\trs%d\tA\tG\t100\tPASS\t%s\tGT\t" % (100 + i, i, b"X" * rnd.randint(1, 40))
+        lines.append(pfx + b"\t".join(toks))
+    for lead in (0, 1, 2, 3, 7, 13):
+        st, out, ro, err = run(lines, lead=lead)
+        assert err == (1 << 64) - 1
+        for i, ln in enumerate(lines):
+            assert out[int(ro[i]):int(ro[i + 1])] == G.oracle_encode_line(ln)[1], (lead, i)

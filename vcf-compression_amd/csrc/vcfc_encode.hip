@@ -137,11 +137,15 @@ constexpr uint32_t BPL = 4 * TPL;           // bytes per lane per chunk
 constexpr uint32_t CHUNK = 64 * BPL;        // bytes per wave iteration (1 KiB)
 
 __device__ __forceinline__ uint32_t cls_mask_f(uint32_t c) { return (0x80C0A000u >> (8 * (c & 3u))) & 0xFFu; }
-// exact x mod cap for x < 2^24 (cap 127 for 0|0 runs, 31 otherwise; magic = ceil(2^32/cap))
+// exact x mod cap for x < 2^23 (cap 127 for 0|0 runs, 31 otherwise):
+// q = floor(x * m / 2^s) with m = ceil(2^s / cap), s = 30 / 28, whose excess
+// m*cap - 2^s (123 / 23) stays below 2^(s-23) -- all 24-bit multiplies.
+constexpr uint32_t MOD_BIAS = 3937;   // 127 * 31: keeps run offsets non-negative
 __device__ __forceinline__ uint32_t mod_cap(uint32_t x, bool is00) {
-    const uint32_t m = is00 ? 33818641u : 138547333u;
-    const uint32_t d = is00 ? 127u : 31u;
-    return x - vw::mulhi(x, m) * d;
+    x &= 0x7FFFFFu;
+    const uint64_t p = (uint64_t)x * (is00 ? 8454661u : 8659209u);
+    const uint32_t q = vw::alignbit((uint32_t)(p >> 32), (uint32_t)p, is00 ? 30u : 28u);
+    return (uint32_t)vw::mad24((int32_t)q, is00 ? -127 : -31, (int32_t)x);
 }
 // class of the token packed in the low 24 bits: 0..3 for 0|0 0|1 1|0 1|1, else ESC
 __device__ __forceinline__ uint32_t cls_f(uint32_t w) {
@@ -252,8 +256,94 @@ __device__ __forceinline__ int fast_prefix_step(const Chunk &cur, uint32_t c, ui
     if (((glen + 1) & 3u) != 0) return 2;
     f.T = (glen + 1) >> 2;
     f.phi = (lead + x9) & 3u;
-    if (f.T >= (1u << 24)) return 2;   // mod_cap's magic numbers are exact below 2^24
+    if (f.T >= (1u << 23) - 2 * MOD_BIAS) return 2;   // mod_cap is exact below 2^23
     return 1;
+}
+
+// Clean chunk: every genotype slot of the chunk in [0, T) is "a|b" with a, b in
+// {0,1} (EDGE: slots outside [0, T) are allowed and ignored).  Per lane the 4
+// slot classes live in one dword (byte j = 0x90 | class), so run starts are
+// byte compares against the predecessor's class, and the lane's output is at
+// most: a full-chunk byte of the run entering the lane (offsets reach cap-1 at
+// most once in 4 slots, and only before the lane's first start), the pending
+// byte of that run at the first start, and one pending byte per further start
+// (runs that begin and end inside the lane are shorter than any cap).
+//
+// EDGE (the row's first and last chunk): slots before token 0 take token 0's
+// class and slots past T-1 take token T-1's, which makes them continue a run
+// without starting one; full bytes there are masked.  Token 0 is treated as
+// continuing a virtual run of its own class that began at token 0 (prs = 1),
+// which emits exactly what a fresh run would.
+template <bool EDGE>
+__device__ __forceinline__ void clean_chunk(const uint32_t (&d)[TPL], int32_t t0, int32_t tf, FastState &f, Ring &r) {
+    const uint32_t l = vw::lane_id();
+    const uint32_t q01 = vw::perm(d[1], d[0], 0x06040200u), q23 = vw::perm(d[3], d[2], 0x06040200u);
+    // 2 * "a" + "b" per byte: 0x90 + class, no carries (bytes validated)
+    uint32_t cb = (vw::perm(q23, q01, 0x06040200u) << 1) + vw::perm(q23, q01, 0x07050301u);
+    if (EDGE) {
+        const uint32_t T = f.T;
+        if (f.pcls == CLS_NONE) {   // first genotype chunk (tf <= 0)
+            const uint32_t o0 = (uint32_t)(-tf);
+            f.pcls = (vw::readlane(cb, o0 >> 2) >> (8u * (o0 & 3u))) & 3u;
+            f.prs = 1;
+        }
+        const uint32_t ol = umin32((uint32_t)((int32_t)T - 1 - tf), 64u * TPL - 1u);
+        const uint32_t cL = (vw::readlane(cb, ol >> 2) >> (8u * (ol & 3u))) & 3u;
+        const int32_t nlo = t0 >= 0 ? 0 : (t0 <= -4 ? 4 : -t0);              // slots before token 0
+        const int32_t nhi = (int32_t)T - t0 >= 4 ? 4 : ((int32_t)T - t0 <= 0 ? 0 : (int32_t)T - t0);
+        const uint32_t mlo = nlo == 0 ? 0u : (~0u >> (32 - 8 * nlo));
+        const uint32_t mhi = nhi >= 4 ? 0u : (~0u << (8 * nhi));
+        cb = (cb & ~(mlo | mhi)) | ((0x90909090u | (f.pcls * 0x01010101u)) & mlo) |
+             ((0x90909090u | (cL * 0x01010101u)) & mhi);
+    }
+    // predecessor class of each slot; slot 0's comes from the previous lane
+    const uint32_t pw = vw::shr1(cb, (0x90u | f.pcls) << 24);
+    const uint32_t cp = vw::alignbyte(cb, pw, 3);
+    const uint32_t x = cb ^ cp;
+    const uint32_t sb = (x | (x >> 1)) & 0x01010101u;       // bit 8j: slot j starts a run
+    // run start (+1) of the lane's last start, wave max-scan -> run entering each lane
+    const uint32_t lane_rs = sb ? (uint32_t)(t0 + 4) - ((uint32_t)__builtin_clz(sb) >> 3) : 0u;
+    const uint32_t incl = vw::scan_max(lane_rs);
+    const uint32_t rin = vw::umax(vw::shr1(incl, 0u), f.prs);
+    const bool is00 = (cp & 3u) == 0;
+    const uint32_t cap = is00 ? 127u : 31u;
+    const uint32_t mp = mod_cap((uint32_t)(t0 + (int32_t)MOD_BIAS) - rin, is00);   // offset of slot -1, mod cap
+    const uint32_t fb1 = sb ? (uint32_t)__builtin_ctz(sb) : 32u;
+    const uint32_t j1 = fb1 >> 3;                             // first start (4: none)
+    const uint32_t MK = vw::perm(0x80C0A000u, 0x80C0A000u, cp & 0x03030303u);   // byte j: mask of slot j-1's class
+    const uint32_t jf = cap - 2u - mp;                        // slot completing a chunk of cap
+    bool full = jf < j1;
+    if (EDGE) full = full && (uint32_t)(t0 + (int32_t)jf) < f.T;
+    uint32_t rr = mp + j1;
+    rr = umin32(rr, rr - cap);                                // (mp + j1) mod cap
+    const bool pend = j1 < 4 && rr != cap - 1u;
+    uint32_t s2 = sb & (sb - 1u);
+    const uint32_t cnt = (full ? 1u : 0u) + (pend ? 1u : 0u) + (uint32_t)__builtin_popcount(s2);
+    const uint32_t incl2 = vw::scan_add(cnt);
+    uint32_t pos = r.wpos + incl2 - cnt;
+    const uint32_t dummy = RING + l;
+    r.lds[full ? (pos & RMASK) : dummy] = (uint8_t)(MK | cap);
+    pos += full ? 1u : 0u;
+    r.lds[pend ? (pos & RMASK) : dummy] = (uint8_t)(MK | (rr + 1u));
+    pos += pend ? 1u : 0u;
+    if (vw::ballot(s2 != 0)) {
+        // further starts: each closes a run that began at the previous start
+        uint32_t fp = fb1;
+#pragma unroll
+        for (int k = 0; k < (int)TPL - 1; k++) {
+            if (k > 0 && !vw::ballot(s2 != 0)) break;
+            const bool e = s2 != 0;
+            const uint32_t fk = e ? (uint32_t)__builtin_ctz(s2) : 0u;
+            r.lds[e ? (pos & RMASK) : dummy] = (uint8_t)((MK >> fk) | ((fk - fp) >> 3));
+            pos += e ? 1u : 0u;
+            fp = fk;
+            s2 &= s2 - 1u;
+        }
+    }
+    r.wpos += vw::readlane(incl2, 63);
+    f.pcls = (vw::readlane(cb, 63) >> 24) & 3u;
+    f.prs = vw::umax(vw::readlane(incl, 63), f.prs);
+    ring_flush(r, false);
 }
 
 // Genotype tokens whose first byte lies in chunk c; false = not the fast shape.
@@ -267,79 +357,45 @@ __device__ __forceinline__ bool fast_gt_step(const Chunk &cur, uint32_t c, uint3
     for (int j = 0; j < (int)TPL; j++) d[j] = vw::alignbyte(cur.w(j + 1), cur.w(j), phi);
     const int32_t t0 = (x0 + (int32_t)phi - f.gt0) >> 2;   // token index of slot 0 (exact)
     const uint32_t u0 = (uint32_t)(t0 + 1);
-    // chunk-level shape (wave-uniform): every slot inside [0, T)?
+    // first slot of the chunk (wave-uniform)
     const int32_t tf = ((int32_t)(c * CHUNK) + (int32_t)phi - (int32_t)lead - f.gt0) >> 2;
-    const bool full_range = tf >= 0 && (uint32_t)tf + 64 * TPL <= T;
+    if (tf >= (int32_t)T) return true;   // only the tail bytes of token T-1
     const uint32_t dummy = RING + l;
 
-    if (full_range && f.pcls < CLS_ESC) {
-        bool allz = true, allc = true;
-#pragma unroll
-        for (int j = 0; j < (int)TPL; j++) {
-            allz &= d[j] == Z;
-            allc &= (d[j] & 0xFFFEFFFEu) == Z;
-        }
-        if (f.pcls == 0 && vw::ballot(!allz) == 0) {
-            // one 0|0 run through the whole chunk: only full 127-chunks complete.
-            // token t has run offset o = t + 1 - prs; count multiples of 127 in
-            // [a0 + 1, a0 + 512], a0 = offset of the chunk's first token
-            const uint32_t a0 = (uint32_t)tf + 1 - f.prs;
-            const uint32_t kfull = (a0 + 64 * TPL) / 127 - a0 / 127;
-            if (l < kfull) ring_put(r, r.wpos + l, 0x7Fu);
-            r.wpos += kfull;
-            ring_flush(r, false);
-            return true;
-        }
-        if (vw::ballot(!allc) == 0) {
-            // ---- clean chunk: every slot a classed token "a|b\t" ----
-            uint32_t cl[TPL];
-#pragma unroll
-            for (int j = 0; j < (int)TPL; j++) cl[j] = cls_classed(d[j]);
-            uint32_t p0 = vw::shr1(cl[TPL - 1], f.pcls);
-            uint32_t lane_rs = 0;
+    if (f.pcls < CLS_ESC || f.pcls == CLS_NONE) {
+        if (f.pcls != CLS_NONE && tf + (int32_t)(64 * TPL) < (int32_t)T) {
+            // interior chunk: all slots are tokens, none of them the last
+            const uint32_t o01 = (d[0] ^ Z) | (d[1] ^ Z), o23 = (d[2] ^ Z) | (d[3] ^ Z);
+            const uint32_t o = o01 | o23;
+            if (f.pcls == 0 && vw::ballot(o != 0) == 0) {
+                // one 0|0 run through the whole chunk: only full 127-chunks complete.
+                // token t has run offset o = t + 1 - prs; count multiples of 127 in
+                // [a0 + 1, a0 + 256], a0 = offset of the chunk's first token
+                const uint32_t a0 = (uint32_t)tf + 1 - f.prs;
+                const uint32_t kfull = (a0 + 64 * TPL) / 127 - a0 / 127;
+                if (l < kfull) ring_put(r, r.wpos + l, 0x7Fu);
+                r.wpos += kfull;
+                ring_flush(r, false);
+                return true;
+            }
+            if (vw::ballot((o & 0xFFFEFFFEu) != 0) == 0) {
+                clean_chunk<false>(d, t0, tf, f, r);
+                return true;
+            }
+        } else {
+            // row's first / last chunk: check the slots inside [0, T) only; the
+            // last token has no TAB after it
+            bool bad = false;
 #pragma unroll
             for (int j = 0; j < (int)TPL; j++) {
-                const uint32_t pj = j == 0 ? p0 : cl[j - 1];
-                if (cl[j] != pj) lane_rs = u0 + j;
+                const int32_t t = t0 + j;
+                const uint32_t m = (uint32_t)t < T ? ((uint32_t)t + 1u == T ? 0x00FEFFFEu : 0xFFFEFFFEu) : 0u;
+                bad |= ((d[j] ^ Z) & m) != 0;
             }
-            const uint32_t rin = vw::umax(vw::shr1(vw::scan_max(lane_rs), 0u), f.prs);
-            uint32_t mp = mod_cap((uint32_t)t0 - rin, p0 == 0);
-            uint32_t pend_m = 0, full_m = 0, pbs[TPL];
-            uint32_t lane_sum = 0;
-#pragma unroll
-            for (int j = 0; j < (int)TPL; j++) {
-                const uint32_t pj = j == 0 ? p0 : cl[j - 1], cj = cl[j];
-                const bool s = cj != pj;
-                const uint32_t capm1_p = pj == 0 ? 126u : 30u, capm1_c = cj == 0 ? 126u : 30u;
-                const bool pend = s && mp != capm1_p;
-                pbs[j] = cls_mask_f(pj) | (mp + 1);
-                const uint32_t m = s ? 0u : (mp == capm1_c ? 0u : mp + 1);
-                const bool full = m == capm1_c;
-                pend_m |= (pend ? 1u : 0u) << j;
-                full_m |= (full ? 1u : 0u) << j;
-                lane_sum += (pend ? 1u : 0u) + (full ? 1u : 0u);
-                mp = m;
+            if (vw::ballot(bad) == 0) {
+                clean_chunk<true>(d, t0, tf, f, r);
+                return true;
             }
-            const uint32_t incl = vw::scan_add(lane_sum);
-            uint32_t pos = r.wpos + incl - lane_sum;
-#pragma unroll
-            for (int j = 0; j < (int)TPL; j++) {
-                const bool pend = (pend_m >> j) & 1u, full = (full_m >> j) & 1u;
-                r.lds[pend ? (pos & RMASK) : dummy] = (uint8_t)pbs[j];
-                pos += pend ? 1u : 0u;
-                r.lds[full ? (pos & RMASK) : dummy] = (uint8_t)(cls_mask_f(cl[j]) | (cl[j] == 0 ? 127u : 31u));
-                pos += full ? 1u : 0u;
-            }
-            r.wpos += vw::readlane(incl, 63);
-            // carry the chunk's last token (lane 63, slot TPL-1)
-            uint32_t lrs = rin;
-#pragma unroll
-            for (int j = 0; j < (int)TPL; j++)
-                if (cl[j] != (j == 0 ? p0 : cl[j - 1])) lrs = u0 + j;
-            f.pcls = vw::readlane(cl[TPL - 1], 63);
-            f.prs = vw::readlane(lrs, 63);
-            ring_flush(r, false);
-            return true;
         }
     }
 
@@ -372,7 +428,7 @@ __device__ __forceinline__ bool fast_gt_step(const Chunk &cur, uint32_t c, uint3
         if (s) lane_rs = u0 + j;
     }
     const uint32_t rin = vw::umax(vw::shr1(vw::scan_max(lane_rs), 0u), f.prs);
-    uint32_t mp = mod_cap((uint32_t)t0 - rin, p0 == 0);
+    uint32_t mp = mod_cap((uint32_t)(t0 + (int32_t)MOD_BIAS) - rin, p0 == 0);
     uint32_t lane_sum = 0, lrs = rin;
     uint32_t e1_m = 0, full_m = 0, b1s[TPL];
 #pragma unroll

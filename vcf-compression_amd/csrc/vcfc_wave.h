@@ -61,6 +61,16 @@ __device__ __forceinline__ uint32_t scan_max(uint32_t v) {
     v = umax(v, __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false));
     return v;
 }
+// byte select: result byte i = byte sel[i] of (s0:s1) for sel 0..7, 0x0C -> 0x00
+__device__ __forceinline__ uint32_t perm(uint32_t s0, uint32_t s1, uint32_t sel) {
+    return __builtin_amdgcn_perm(s0, s1, sel);
+}
+// ((hi:lo) >> s)[31:0], s in 0..31
+__device__ __forceinline__ uint32_t alignbit(uint32_t hi, uint32_t lo, uint32_t s) {
+    return __builtin_amdgcn_alignbit(hi, lo, s);
+}
+// x + a*b on the low 24 bits of a and b, signed (v_mad_i32_i24)
+__device__ __forceinline__ int32_t mad24(int32_t a, int32_t b, int32_t x) { return x + __mul24(a, b); }
 // ((hi:lo) >> 8*s)[31:0]
 __device__ __forceinline__ uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t s) {
     return __builtin_amdgcn_alignbyte(hi, lo, s);
