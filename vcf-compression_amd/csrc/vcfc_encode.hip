@@ -208,14 +208,17 @@ __device__ __forceinline__ int fast_prefix_step(const Chunk &cur, uint32_t c, ui
     const uint32_t inc = vw::scan_add(cnt);
     const uint32_t exc = inc - cnt;
     const bool has9 = f.nf + exc <= 9 && 9 < f.nf + inc;
-    uint32_t x9 = 0;
+    uint32_t x9l = 0;
     if (has9) {
         uint32_t mm = fs;
         for (uint32_t k = f.nf + exc; k < 9; k++) mm &= mm - 1;
-        x9 = (uint32_t)(x0 + __builtin_ctz(mm));
+        x9l = (uint32_t)(x0 + __builtin_ctz(mm));
     }
     const uint64_t hb = vw::ballot(has9);
-    if (hb) x9 = vw::readlane(x9, (uint32_t)__builtin_ctzll(hb));
+    // (a separate variable: a phi of the per-lane value would make x9 -- and
+    // gt0, T, phi, every chunk's tf -- look divergent to the compiler)
+    uint32_t x9 = 0;
+    if (hb) x9 = vw::readlane(x9l, (uint32_t)__builtin_ctzll(hb));
     uint32_t below = ~0u;
     if (hb) {
         const int32_t d = (int32_t)x9 - x0;
