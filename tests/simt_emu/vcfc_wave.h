@@ -62,6 +62,8 @@ inline uint32_t alignbit(uint32_t hi, uint32_t lo, uint32_t s) {
 inline int32_t sext24(int32_t v) { return (int32_t)((uint32_t)v << 8) >> 8; }
 inline int32_t mad24(int32_t a, int32_t b, int32_t x) { return (int32_t)((uint32_t)x + (uint32_t)(sext24(a) * sext24(b))); }
 inline void wave_sync() { emu::collective(emu::OP_WAVESYNC, 0, 0, 0); }
+// lowest set bit index; value unspecified for 0 (v_ffbl_b32: callers must not use it)
+inline uint32_t ffbl(uint32_t x) { return (uint32_t)__builtin_ctz(x); }
 inline int popc64(uint64_t m) { return __builtin_popcountll(m); }
 inline int hibit64(uint64_t m) { return 63 - __builtin_clzll(m); }
 inline uint32_t mulhi(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }

@@ -81,6 +81,8 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+// lowest set bit index; value unspecified for 0 (v_ffbl_b32: callers must not use it)
+__device__ __forceinline__ uint32_t ffbl(uint32_t x) { return (uint32_t)__builtin_ctz(x); }
 __device__ __forceinline__ int popc64(uint64_t m) { return __popcll(m); }
 // index of the highest set bit (m != 0)
 __device__ __forceinline__ int hibit64(uint64_t m) { return 63 - __clzll(m); }

@@ -17,7 +17,7 @@ import os
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(ROOT, "build", "libvcfc.so")
+LIB_PATH = os.environ.get("VCFC_LIB") or os.path.join(ROOT, "build", "libvcfc.so")
 
 OK, E_LT8COLS, E_8COLS, E_HEADER, E_NOSPACE, E_ARG, E_HIP, E_IO, E_FORMAT = range(9)
 NO_ERROR = (1 << 64) - 1
