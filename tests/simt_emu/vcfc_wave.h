@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
 
 namespace vw {
 inline uint32_t lane_id() { return emu::lane(); }
@@ -70,5 +71,15 @@ inline uint32_t mulhi(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a *
 inline uint4 gload16(const void *base, uint32_t idx) { return ((const uint4 *)base)[idx]; }
 inline uint32_t gload4(const void *base, uint32_t idx) { return ((const uint32_t *)base)[idx]; }
 inline void gstore16(void *base, uint64_t byte_off, uint4 v) { *(uint4 *)((uint8_t *)base + byte_off) = v; }
+struct brsrc { const uint8_t *base; uint32_t bytes; };
+inline brsrc make_rsrc(const void *base, uint32_t bytes) { return brsrc{(const uint8_t *)base, bytes}; }
+inline uint32_t bload_dw(brsrc r, uint32_t off) {
+    if ((uint64_t)off + 4 > r.bytes) return 0u;   // per-dword range check
+    uint32_t v; memcpy(&v, r.base + off, 4); return v;
+}
+inline uint4 bload16(brsrc r, uint32_t off) {
+    return make_uint4(bload_dw(r, off), bload_dw(r, off + 4), bload_dw(r, off + 8), bload_dw(r, off + 12));
+}
+inline uint32_t bload4(brsrc r, uint32_t off) { return bload_dw(r, off); }
 inline void pin_loads() {}
 }  // namespace vw

@@ -163,13 +163,11 @@ struct Chunk {
     }
 };
 
-__device__ __forceinline__ Chunk load_chunk(const uint8_t *A, uint32_t c, uint32_t l, uint32_t last_blk) {
-    const uint32_t b0 = c * (CHUNK / 16) + l;
-    const uint32_t c0 = b0 < last_blk ? b0 : last_blk;
-    const uint32_t c1 = b0 + 1 < last_blk ? b0 + 1 : last_blk;
+__device__ __forceinline__ Chunk load_chunk(vw::brsrc rs, uint32_t c, uint32_t lo16) {
     Chunk k;
-    k.a = vw::gload16(A, c0);
-    k.y = vw::gload4(A, 4u * c1);
+    const uint32_t off = c * CHUNK + lo16;   // lo16 = 16 * lane
+    k.a = vw::bload16(rs, off);
+    k.y = vw::bload4(rs, off + 16u);
     return k;
 }
 
@@ -352,16 +350,16 @@ __device__ __forceinline__ void clean_chunk(const uint32_t (&d)[TPL], int32_t t0
 // Genotype tokens whose first byte lies in chunk c; false = not the fast shape.
 __device__ __forceinline__ bool fast_gt_step(const Chunk &cur, uint32_t c, uint32_t lead, FastState &f, Ring &r) {
     const uint32_t l = vw::lane_id();
-    const int32_t x0 = (int32_t)(c * CHUNK + BPL * l) - (int32_t)lead;
     const uint32_t T = f.T, phi = f.phi;
     constexpr uint32_t Z = 0x09307C30u;   // "0|0\t"
     uint32_t d[TPL];
 #pragma unroll
     for (int j = 0; j < (int)TPL; j++) d[j] = vw::alignbyte(cur.w(j + 1), cur.w(j), phi);
-    const int32_t t0 = (x0 + (int32_t)phi - f.gt0) >> 2;   // token index of slot 0 (exact)
-    const uint32_t u0 = (uint32_t)(t0 + 1);
-    // first slot of the chunk (wave-uniform)
+    // token index of the chunk's first slot (wave-uniform; floor division of
+    // a multiple-of-4 offset, so each lane's is exactly TPL * l more)
     const int32_t tf = ((int32_t)(c * CHUNK) + (int32_t)phi - (int32_t)lead - f.gt0) >> 2;
+    const int32_t t0 = tf + (int32_t)(TPL * l);
+    const uint32_t u0 = (uint32_t)(t0 + 1);
     if (tf >= (int32_t)T) return true;   // only the tail bytes of token T-1
     const uint32_t dummy = RING + l;
 
@@ -503,7 +501,9 @@ __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring
     const uint8_t *A = line - lead;
     const uint32_t span = lead + len;
     if (len == 0) return false;
-    const uint32_t last_blk = (span - 1) >> 4;   // last 16-byte block holding line bytes
+    // loads past the row (prefetch overrun, last chunk) read 0: no clamping
+    const vw::brsrc rs = vw::make_rsrc(A, (span + 3u) & ~3u);
+    const uint32_t lo16 = BPL * l;
     const uint32_t nch = (span + CHUNK - 1) / CHUNK;
     FastState f;
     f.nf = 0; f.carryT = 1; f.gt0 = -1; f.T = 0; f.phi = 0; f.pcls = CLS_NONE; f.prs = 0;
@@ -511,9 +511,9 @@ __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring
     r.fpos = 0;
 
     // three chunk buffers: while b0 is processed, b1 and b2 are in flight
-    Chunk b0 = load_chunk(A, 0, l, last_blk);
-    Chunk b1 = load_chunk(A, 1, l, last_blk);
-    Chunk b2 = load_chunk(A, 2, l, last_blk);
+    Chunk b0 = load_chunk(rs, 0, lo16);
+    Chunk b1 = load_chunk(rs, 1, lo16);
+    Chunk b2 = load_chunk(rs, 2, lo16);
     vw::pin_loads();
     // (readfirst marks the wave-uniform loop state as uniform for the
     // compiler: scalar loop control, no exec-masked loop structurisation)
@@ -526,14 +526,14 @@ __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring
         for (;;) {
             c = vw::readfirst(c + 1);
             if (c >= nch) return false;   // < 10 fields
-            const Chunk t = load_chunk(A, c, l, last_blk);
+            const Chunk t = load_chunk(rs, c, lo16);
             st = (int)vw::readfirst((uint32_t)fast_prefix_step(t, c, lead, len, f, r));
             if (st == 2) return false;
             if (st == 1) break;
         }
-        b0 = load_chunk(A, c, l, last_blk);
-        b1 = load_chunk(A, c + 1, l, last_blk);
-        b2 = load_chunk(A, c + 2, l, last_blk);
+        b0 = load_chunk(rs, c, lo16);
+        b1 = load_chunk(rs, c + 1, lo16);
+        b2 = load_chunk(rs, c + 2, lo16);
         vw::pin_loads();
     }
     // genotype chunks, unrolled x3 over named buffers: no register copies
@@ -543,13 +543,13 @@ __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring
     bool ok = true;
     for (;;) {
         ok = vw::readfirst(ok && fast_gt_step(b0, c, lead, f, r));
-        b0 = load_chunk(A, c + 3, l, last_blk);
+        b0 = load_chunk(rs, c + 3, lo16);
         vw::pin_loads();
         if (ok && c + 1 < nch) ok = vw::readfirst(fast_gt_step(b1, c + 1, lead, f, r));
-        b1 = load_chunk(A, c + 4, l, last_blk);
+        b1 = load_chunk(rs, c + 4, lo16);
         vw::pin_loads();
         if (ok && c + 2 < nch) ok = vw::readfirst(fast_gt_step(b2, c + 2, lead, f, r));
-        b2 = load_chunk(A, c + 5, l, last_blk);
+        b2 = load_chunk(rs, c + 5, lo16);
         vw::pin_loads();
         c = vw::readfirst(c + 3);
         if (!ok || c >= nch) break;

@@ -108,6 +108,21 @@ __device__ __forceinline__ void gstore16(void *base, uint64_t byte_off, uint4 v)
     t.x = v.x; t.y = v.y; t.z = v.z; t.w = v.w;
     *((g_v4u *)((__attribute__((address_space(1))) uint8_t *)base + byte_off)) = t;
 }
+// Raw buffer resource over [base, base + bytes): loads at offsets past
+// `bytes` (checked per dword) return 0 instead of touching memory, so
+// prefetches past a row's end need no clamping.  The chunk offset goes in
+// the VGPR offset: gfx9 leaves the SGPR offset out of the range check.
+typedef __amdgpu_buffer_rsrc_t brsrc;
+__device__ __forceinline__ brsrc make_rsrc(const void *base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ uint4 bload16(brsrc r, uint32_t off) {
+    const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint32_t bload4(brsrc r, uint32_t off) {
+    return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+}
 // Keep just-issued prefetch loads where they are: the memory clobber stops
 // LLVM from sinking them towards their (next-iteration) use, which would
 // shrink the prefetch distance to zero.  Emits no instruction.
