@@ -18,7 +18,8 @@ def lib():
         L = ctypes.CDLL(EMU_SO)
         vp = ctypes.c_void_p
         L.emu_encode_rows.argtypes = [vp, vp, vp, ctypes.c_uint64, vp, ctypes.c_uint64, vp,
-                                      ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+                                      ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+                                      ctypes.POINTER(ctypes.c_uint32)]
         L.emu_sparse_plan.argtypes = [vp, vp, ctypes.c_uint64, ctypes.c_uint64, vp, vp, vp]
         _lib = L
     return _lib
@@ -40,9 +41,14 @@ def data_lines(vcf):
     return vcf, np.array(offs, dtype=np.uint64), np.array(lens, dtype=np.uint32)
 
 
+LAST_RETRIES = [0]
+
+
 def emu_encode(buf, line_off, line_len):
     """Run the product encode pipeline on the emulator.
-    Returns (status, records bytes, rec_off array, err_word)."""
+    Returns (status, records bytes, rec_off array, err_word); the number of
+    rows the fast kernel handed to the general kernel is left in
+    LAST_RETRIES[0]."""
     n = len(line_off)
     cap = int(sum(int(x) * 3 // 2 + 32 for x in line_len)) + 64
     out = np.zeros(cap, dtype=np.uint8)
@@ -52,8 +58,10 @@ def emu_encode(buf, line_off, line_len):
     ll = np.ascontiguousarray(line_len, dtype=np.uint32)
     err = ctypes.c_uint64(0)
     sw = ctypes.c_uint64(0)
+    rt = ctypes.c_uint32(0)
     st = lib().emu_encode_rows(src.ctypes.data, lo.ctypes.data, ll.ctypes.data, n, out.ctypes.data, cap,
-                               rec_off.ctypes.data, ctypes.byref(err), ctypes.byref(sw))
+                               rec_off.ctypes.data, ctypes.byref(err), ctypes.byref(sw), ctypes.byref(rt))
+    LAST_RETRIES[0] = rt.value
     total = int(rec_off[n]) if n else 0
     return st, out[:total].tobytes(), rec_off, err.value
 

@@ -10,7 +10,7 @@
 
 extern "C" int emu_encode_rows(const uint8_t *buf, const uint64_t *line_off, const uint32_t *line_len,
                                uint64_t n, uint8_t *out, uint64_t out_cap, uint64_t *rec_off,
-                               uint64_t *err_word, uint64_t *switches) {
+                               uint64_t *err_word, uint64_t *switches, uint32_t *retries) {
     uint64_t total = 0;
     for (uint64_t i = 0; i < n; i++) total += line_len[i];
     VcfcWorkspaceLayout L = vcfc_encode_workspace_layout(n, total);
@@ -30,6 +30,7 @@ extern "C" int emu_encode_rows(const uint8_t *buf, const uint64_t *line_off, con
     emu::g.switches = 0;
     int st = (int)vcfc_encode_device(a, nullptr);
     *err_word = *a.err;
+    if (retries) *retries = *a.retry_count;   // rows the fast kernel handed to k_encode_general
     if (switches) *switches = emu::g.switches;
     free(ws);
     return st;

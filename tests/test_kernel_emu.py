@@ -109,6 +109,7 @@ def test_chr22_like_rows_skip_path(seed):
     lines = _chr22_like_rows(40, 2504, seed)
     st, out, ro, err = run(lines, lead=seed % 16)
     assert err == (1 << 64) - 1
+    assert E.LAST_RETRIES[0] == 0   # escapes stay on the fast kernel's general step
     for i, ln in enumerate(lines):
         assert out[int(ro[i]):int(ro[i + 1])] == G.oracle_encode_line(ln)[1], i
 
@@ -135,5 +136,31 @@ def test_short_rows_and_cap_boundaries(seed):
     for lead in (0, 1, 2, 3, 7, 13):
         st, out, ro, err = run(lines, lead=lead)
         assert err == (1 << 64) - 1
+        assert E.LAST_RETRIES[0] == 0   # every row stayed on the fast kernel
+        for i, ln in enumerate(lines):
+            assert out[int(ro[i]):int(ro[i + 1])] == G.oracle_encode_line(ln)[1], (lead, i)
+
+
+@pytest.mark.parametrize("seed", [31, 32])
+def test_dense_rows_wrap_the_ring(seed):
+    """Rows whose records are many times the 4 KiB LDS ring (a start at most
+    tokens): run groups straddling the ring end, bursts every chunk."""
+    rnd = random.Random(seed)
+    classes = [b"0|0", b"0|1", b"1|0", b"1|1"]
+    lines = []
+    for i in range(6):
+        n = rnd.choice([9000, 17000, 24001])
+        p = rnd.choice([0.5, 0.9, 1.0])
+        toks, c = [], 0
+        for _ in range(n):
+            if rnd.random() < p:
+                c = rnd.randrange(4)
+            toks.append(classes[c])
+        pfx = b"22\t%d\trs%d\tA\tG\t100\tPASS\tAF=0.5\tGT\t" % (100 + i, i)
+        lines.append(pfx + b"\t".join(toks))
+    for lead in (0, 5, 10):
+        st, out, ro, err = run(lines, lead=lead)
+        assert err == (1 << 64) - 1
+        assert E.LAST_RETRIES[0] == 0
         for i, ln in enumerate(lines):
             assert out[int(ro[i]):int(ro[i + 1])] == G.oracle_encode_line(ln)[1], (lead, i)

@@ -261,146 +261,20 @@ __device__ __forceinline__ int fast_prefix_step(const Chunk &cur, uint32_t c, ui
     return 1;
 }
 
-// Clean chunk: every genotype slot of the chunk in [0, T) is "a|b" with a, b in
-// {0,1} (EDGE: slots outside [0, T) are allowed and ignored).  Per lane the 4
-// slot classes live in one dword (byte j = 0x90 | class), so run starts are
-// byte compares against the predecessor's class, and the lane's output is at
-// most: a full-chunk byte of the run entering the lane (offsets reach cap-1 at
-// most once in 4 slots, and only before the lane's first start), the pending
-// byte of that run at the first start, and one pending byte per further start
-// (runs that begin and end inside the lane are shorter than any cap).
-//
-// EDGE (the row's first and last chunk): slots before token 0 take token 0's
-// class and slots past T-1 take token T-1's, which makes them continue a run
-// without starting one; full bytes there are masked.  Token 0 is treated as
-// continuing a virtual run of its own class that began at token 0 (prs = 1),
-// which emits exactly what a fresh run would.
-template <bool EDGE>
-__device__ __forceinline__ void clean_chunk(const uint32_t (&d)[TPL], int32_t t0, int32_t tf, FastState &f, Ring &r) {
-    const uint32_t l = vw::lane_id();
-    const uint32_t q01 = vw::perm(d[1], d[0], 0x06040200u), q23 = vw::perm(d[3], d[2], 0x06040200u);
-    // 2 * "a" + "b" per byte: 0x90 + class, no carries (bytes validated)
-    uint32_t cb = (vw::perm(q23, q01, 0x06040200u) << 1) + vw::perm(q23, q01, 0x07050301u);
-    if (EDGE) {
-        const uint32_t T = f.T;
-        if (f.pcls == CLS_NONE) {   // first genotype chunk (tf <= 0)
-            const uint32_t o0 = (uint32_t)(-tf);
-            f.pcls = (vw::readlane(cb, o0 >> 2) >> (8u * (o0 & 3u))) & 3u;
-            f.prs = 1;
-        }
-        const uint32_t ol = umin32((uint32_t)((int32_t)T - 1 - tf), 64u * TPL - 1u);
-        const uint32_t cL = (vw::readlane(cb, ol >> 2) >> (8u * (ol & 3u))) & 3u;
-        const int32_t nlo = t0 >= 0 ? 0 : (t0 <= -4 ? 4 : -t0);              // slots before token 0
-        const int32_t nhi = (int32_t)T - t0 >= 4 ? 4 : ((int32_t)T - t0 <= 0 ? 0 : (int32_t)T - t0);
-        const uint32_t mlo = nlo == 0 ? 0u : (~0u >> (32 - 8 * nlo));
-        const uint32_t mhi = nhi >= 4 ? 0u : (~0u << (8 * nhi));
-        cb = (cb & ~(mlo | mhi)) | ((0x90909090u | (f.pcls * 0x01010101u)) & mlo) |
-             ((0x90909090u | (cL * 0x01010101u)) & mhi);
-    }
-    // predecessor class of each slot; slot 0's comes from the previous lane
-    const uint32_t pw = vw::shr1(cb, (0x90u | f.pcls) << 24);
-    const uint32_t cp = vw::alignbyte(cb, pw, 3);
-    const uint32_t x = cb ^ cp;
-    const uint32_t sb = (x | (x >> 1)) & 0x01010101u;       // bit 8j: slot j starts a run
-    // run start (+1) of the lane's last start, wave max-scan -> run entering each lane
-    const uint32_t lane_rs = sb ? (uint32_t)(t0 + 4) - ((uint32_t)__builtin_clz(sb) >> 3) : 0u;
-    const uint32_t incl = vw::scan_max(lane_rs);
-    const uint32_t rin = vw::umax(vw::shr1(incl, 0u), f.prs);
-    const bool is00 = (cp & 3u) == 0;
-    const uint32_t cap = is00 ? 127u : 31u;
-    const uint32_t mp = mod_cap((uint32_t)(t0 + (int32_t)MOD_BIAS) - rin, is00);   // offset of slot -1, mod cap
-    const uint32_t fb1 = sb ? (uint32_t)__builtin_ctz(sb) : 32u;
-    const uint32_t j1 = fb1 >> 3;                             // first start (4: none)
-    const uint32_t MK = vw::perm(0x80C0A000u, 0x80C0A000u, cp & 0x03030303u);   // byte j: mask of slot j-1's class
-    const uint32_t jf = cap - 2u - mp;                        // slot completing a chunk of cap
-    bool full = jf < j1;
-    if (EDGE) full = full && (uint32_t)(t0 + (int32_t)jf) < f.T;
-    uint32_t rr = mp + j1;
-    rr = umin32(rr, rr - cap);                                // (mp + j1) mod cap
-    const bool pend = j1 < 4 && rr != cap - 1u;
-    uint32_t s2 = sb & (sb - 1u);
-    const uint32_t cnt = (full ? 1u : 0u) + (pend ? 1u : 0u) + (uint32_t)__builtin_popcount(s2);
-    const uint32_t incl2 = vw::scan_add(cnt);
-    uint32_t pos = r.wpos + incl2 - cnt;
-    const uint32_t dummy = RING + l;
-    r.lds[full ? (pos & RMASK) : dummy] = (uint8_t)(MK | cap);
-    pos += full ? 1u : 0u;
-    r.lds[pend ? (pos & RMASK) : dummy] = (uint8_t)(MK | (rr + 1u));
-    pos += pend ? 1u : 0u;
-    if (vw::ballot(s2 != 0)) {
-        // further starts: each closes a run that began at the previous start
-        uint32_t fp = fb1;
-#pragma unroll
-        for (int k = 0; k < (int)TPL - 1; k++) {
-            if (k > 0 && !vw::ballot(s2 != 0)) break;
-            const bool e = s2 != 0;
-            const uint32_t fk = e ? (uint32_t)__builtin_ctz(s2) : 0u;
-            r.lds[e ? (pos & RMASK) : dummy] = (uint8_t)((MK >> fk) | ((fk - fp) >> 3));
-            pos += e ? 1u : 0u;
-            fp = fk;
-            s2 &= s2 - 1u;
-        }
-    }
-    r.wpos += vw::readlane(incl2, 63);
-    f.pcls = (vw::readlane(cb, 63) >> 24) & 3u;
-    f.prs = vw::umax(vw::readlane(incl, 63), f.prs);
-    ring_flush(r, false);
-}
-
-// Genotype tokens whose first byte lies in chunk c; false = not the fast shape.
-__device__ __forceinline__ bool fast_gt_step(const Chunk &cur, uint32_t c, uint32_t lead, FastState &f, Ring &r) {
+// General genotype step over one 1 KiB half-chunk (4 slots per lane):
+// escapes, the row's last token, anything the clean 2 KiB path rejects.
+// tf = token index of the half's first slot.  false = not the fast shape.
+__device__ bool gt_general(const Chunk &cur, int32_t tf, FastState &f, Ring &r) {
     const uint32_t l = vw::lane_id();
     const uint32_t T = f.T, phi = f.phi;
     constexpr uint32_t Z = 0x09307C30u;   // "0|0\t"
+    if (tf >= (int32_t)T) return true;
     uint32_t d[TPL];
 #pragma unroll
     for (int j = 0; j < (int)TPL; j++) d[j] = vw::alignbyte(cur.w(j + 1), cur.w(j), phi);
-    // token index of the chunk's first slot (wave-uniform; floor division of
-    // a multiple-of-4 offset, so each lane's is exactly TPL * l more)
-    const int32_t tf = ((int32_t)(c * CHUNK) + (int32_t)phi - (int32_t)lead - f.gt0) >> 2;
     const int32_t t0 = tf + (int32_t)(TPL * l);
     const uint32_t u0 = (uint32_t)(t0 + 1);
-    if (tf >= (int32_t)T) return true;   // only the tail bytes of token T-1
     const uint32_t dummy = RING + l;
-
-    if (f.pcls < CLS_ESC || f.pcls == CLS_NONE) {
-        if (f.pcls != CLS_NONE && tf + (int32_t)(64 * TPL) < (int32_t)T) {
-            // interior chunk: all slots are tokens, none of them the last
-            const uint32_t o01 = (d[0] ^ Z) | (d[1] ^ Z), o23 = (d[2] ^ Z) | (d[3] ^ Z);
-            const uint32_t o = o01 | o23;
-            if (f.pcls == 0 && vw::ballot(o != 0) == 0) {
-                // one 0|0 run through the whole chunk: only full 127-chunks complete.
-                // token t has run offset o = t + 1 - prs; count multiples of 127 in
-                // [a0 + 1, a0 + 256], a0 = offset of the chunk's first token
-                const uint32_t a0 = (uint32_t)tf + 1 - f.prs;
-                const uint32_t kfull = (a0 + 64 * TPL) / 127 - a0 / 127;
-                if (l < kfull) ring_put(r, r.wpos + l, 0x7Fu);
-                r.wpos += kfull;
-                ring_flush(r, false);
-                return true;
-            }
-            if (vw::ballot((o & 0xFFFEFFFEu) != 0) == 0) {
-                clean_chunk<false>(d, t0, tf, f, r);
-                return true;
-            }
-        } else {
-            // row's first / last chunk: check the slots inside [0, T) only; the
-            // last token has no TAB after it
-            bool bad = false;
-#pragma unroll
-            for (int j = 0; j < (int)TPL; j++) {
-                const int32_t t = t0 + j;
-                const uint32_t m = (uint32_t)t < T ? ((uint32_t)t + 1u == T ? 0x00FEFFFEu : 0xFFFEFFFEu) : 0u;
-                bad |= ((d[j] ^ Z) & m) != 0;
-            }
-            if (vw::ballot(bad) == 0) {
-                clean_chunk<true>(d, t0, tf, f, r);
-                return true;
-            }
-        }
-    }
-
-    // ---- general chunk: row start/end, escapes ----
     bool v[TPL];
 #pragma unroll
     for (int j = 0; j < (int)TPL; j++) v[j] = (uint32_t)(t0 + j) < T;
@@ -495,67 +369,253 @@ __device__ __forceinline__ bool fast_gt_step(const Chunk &cur, uint32_t c, uint3
     return true;
 }
 
+
+// ---------------------------------------------------------------------------
+// Genotype phase: 2 KiB chunks of the genotype region, based at the 4-byte
+// word holding token 0 (phase phi), so slot j of lane l is token
+// 512 C + 8 l + j and no slot precedes token 0.  Lane l owns bytes
+// [32 l, 32 l + 32) plus a 4-byte look-ahead.
+constexpr uint32_t TPL8 = 8;
+constexpr uint32_t BPL8 = 4 * TPL8;
+constexpr uint32_t CHUNK8 = 64 * BPL8;   // 2 KiB
+constexpr uint32_t SLOTS8 = 64 * TPL8;   // 512 tokens per chunk
+
+struct Chunk8 {
+    uint4 a, b;
+    uint32_t y;
+    __device__ __forceinline__ uint32_t w(int k) const {
+        return k == 0 ? a.x : k == 1 ? a.y : k == 2 ? a.z : k == 3 ? a.w :
+               k == 4 ? b.x : k == 5 ? b.y : k == 6 ? b.z : k == 7 ? b.w : y;
+    }
+};
+__device__ __forceinline__ Chunk8 load_chunk8(vw::brsrc rs, uint32_t C, uint32_t lo32) {
+    Chunk8 k;
+    const uint32_t off = C * CHUNK8 + lo32;   // lo32 = 32 * lane
+    k.a = vw::bload16(rs, off);
+    k.b = vw::bload16(rs, off + 16u);
+    k.y = vw::bload4(rs, off + 32u);
+    return k;
+}
+
+// class bytes of four classed tokens: byte j = 0x90 + class ("2a + b", no carries)
+__device__ __forceinline__ uint32_t class_bytes(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3) {
+    const uint32_t q01 = vw::perm(d1, d0, 0x06040200u), q23 = vw::perm(d3, d2, 0x06040200u);
+    return (vw::perm(q23, q01, 0x06040200u) << 1) + vw::perm(q23, q01, 0x07050301u);
+}
+// bytes 0..3 of lo and hi (one flag or value per slot) -> 4-bit stride: slot j at bit 4j
+__device__ __forceinline__ uint32_t stride4(uint32_t lo, uint32_t hi) {
+    return vw::perm(hi, lo, 0x06040200u) | (vw::perm(hi, lo, 0x07050301u) << 4);
+}
+
+// Clean chunk: every slot in [0, T) is "a|b" with a, b in {0,1}.  The lane's
+// output is at most: a full-chunk byte of the run entering the lane (run
+// offsets reach cap-1 at most once in 8 slots, and only before the lane's
+// first start), the pending byte of that run at the first start, and one
+// pending byte per further start (runs that begin and end inside the lane
+// are shorter than any cap).  The first chunk treats token 0 as continuing a
+// virtual run of its own class begun at token 0 (prs = 1): same output as a
+// fresh run.  EDGE (last chunk): slots past T-1 take token T-1's class, so
+// they continue its run without starting one; their full bytes are masked.
+template <bool EDGE>
+__device__ __forceinline__ void clean8(const uint32_t (&d)[TPL8], int32_t t0, int32_t tf, FastState &f, Ring &r) {
+    uint32_t cbL = class_bytes(d[0], d[1], d[2], d[3]);
+    uint32_t cbH = class_bytes(d[4], d[5], d[6], d[7]);
+    if (f.pcls == CLS_NONE) {   // first chunk
+        f.pcls = vw::readlane(cbL, 0) & 3u;
+        f.prs = 1;
+    }
+    const uint32_t T = f.T;
+    if (EDGE) {
+        const uint32_t ol = (uint32_t)((int32_t)T - 1 - tf);   // < SLOTS8 (caller)
+        const uint32_t cw = vw::readlane((ol & 4u) ? cbH : cbL, ol >> 3);
+        const uint32_t cL = (cw >> (8u * (ol & 3u))) & 3u;
+        const int32_t nv = (int32_t)T - t0;                      // valid slots in the lane
+        const uint32_t fill = 0x90909090u | (cL * 0x01010101u);
+        const uint32_t mL = nv >= 4 ? 0u : (nv <= 0 ? ~0u : (~0u << (8 * nv)));
+        const uint32_t mH = nv >= 8 ? 0u : (nv <= 4 ? ~0u : (~0u << (8 * (nv - 4))));
+        cbL = (cbL & ~mL) | (fill & mL);
+        cbH = (cbH & ~mH) | (fill & mH);
+    }
+    // predecessor class of each slot; slot 0's comes from the previous lane
+    const uint32_t pw = vw::shr1(cbH, (0x90u | f.pcls) << 24);
+    const uint32_t cpL = vw::alignbyte(cbL, pw, 3), cpH = vw::alignbyte(cbH, cbL, 3);
+    const uint32_t xL = cbL ^ cpL, xH = cbH ^ cpH;
+    const uint32_t sb = stride4((xL | (xL >> 1)) & 0x01010101u, (xH | (xH >> 1)) & 0x01010101u);   // bit 4j: slot j starts a run
+    const uint32_t cp4 = stride4(cpL & 0x03030303u, cpH & 0x03030303u);   // class of slot j-1 at bits 4j
+    // run start (+1) of the lane's last start; wave max-scan -> run entering each lane
+    const uint32_t lane_rs = sb ? (uint32_t)(t0 + 8) - ((uint32_t)__builtin_clz(sb) >> 2) : 0u;
+    const uint32_t incl = vw::scan_max(lane_rs);
+    const uint32_t rin = vw::umax(vw::shr1(incl, 0u), f.prs);
+    const uint32_t p0 = cpL & 3u;
+    const bool is00 = p0 == 0;
+    const uint32_t cap = is00 ? 127u : 31u;
+    const uint32_t mp = mod_cap((uint32_t)(t0 + (int32_t)MOD_BIAS) - rin, is00);   // offset of slot -1, mod cap
+    const uint32_t fb1 = sb ? (uint32_t)__builtin_ctz(sb) : 32u;
+    const uint32_t j1 = fb1 >> 2;                              // first start (8: none)
+    const uint32_t m0 = vw::perm(0x80C0A000u, 0x80C0A000u, p0);   // low byte: mask of p0's class
+    const uint32_t jf = cap - 2u - mp;                         // slot completing a chunk of cap
+    bool full = jf < j1;
+    if (EDGE) full = full && (uint32_t)(t0 + (int32_t)jf) < T;
+    uint32_t rr = mp + j1;
+    rr = umin32(rr, rr - cap);                                 // (mp + j1) mod cap (j1 < cap)
+    const bool pend = j1 < TPL8 && rr != cap - 1u;
+    uint32_t s2 = sb & (sb - 1u);
+    const uint32_t n2 = (uint32_t)__builtin_popcount(s2);
+    const uint32_t cnt = (full ? 1u : 0u) + (pend ? 1u : 0u) + n2;
+    const uint32_t incl2 = vw::scan_add(cnt);
+    uint32_t pos = r.wpos + incl2 - cnt;
+    if (full) ring_put(r, pos, m0 | cap);
+    pos += full ? 1u : 0u;
+    if (pend) ring_put(r, pos, m0 | (rr + 1u));
+    pos += pend ? 1u : 0u;
+    if (vw::ballot(s2 != 0)) {
+        // further starts: each closes a run begun at the previous start.  The
+        // group's bytes go to base + k (immediate offsets); a group running
+        // past the ring end lands in the 64-byte tail and is moved below.
+        const uint32_t base = pos & RMASK;
+        uint32_t fp = fb1;
+#pragma unroll
+        for (int k = 0; k < (int)TPL8 - 1; k++) {
+            if (k > 0 && !vw::ballot(s2 != 0)) break;
+            if (s2 != 0) {
+                const uint32_t fk = vw::ffbl(s2);
+                const uint32_t cls = (cp4 >> fk) & 3u;
+                r.lds[base + k] = (uint8_t)(vw::perm(0x80C0A000u, 0x80C0A000u, cls) | ((fk - fp) >> 2));
+                fp = fk;
+            }
+            s2 &= s2 - 1u;
+        }
+        const bool wrap = base + n2 > RING;
+        if (vw::ballot(wrap)) {
+            if (wrap) {
+                for (uint32_t q = RING; q < base + n2; q++) r.lds[q - RING] = r.lds[q];
+            }
+        }
+    }
+    r.wpos += vw::readlane(incl2, 63);
+    f.pcls = (vw::readlane(cbH, 63) >> 24) & 3u;
+    f.prs = vw::umax(vw::readlane(incl, 63), f.prs);
+    ring_flush(r, false);
+}
+
+// Genotype chunk C (2 KiB) on the skip / clean paths.  false = not handled
+// (nothing written): the chunk needs the general step.
+__device__ __forceinline__ bool gt_step8(const Chunk8 &cur, uint32_t C, FastState &f, Ring &r) {
+    const uint32_t l = vw::lane_id();
+    const uint32_t T = f.T, phi = f.phi;
+    constexpr uint32_t Z = 0x09307C30u;   // "0|0\t"
+    const int32_t tf = (int32_t)(C * SLOTS8);
+    if (tf >= (int32_t)T) return true;
+    uint32_t d[TPL8];
+#pragma unroll
+    for (int j = 0; j < (int)TPL8; j++) d[j] = vw::alignbyte(cur.w(j + 1), cur.w(j), phi);
+    const int32_t t0 = tf + (int32_t)(TPL8 * l);
+    if (f.pcls < CLS_ESC || f.pcls == CLS_NONE) {
+        if (tf + (int32_t)SLOTS8 < (int32_t)T) {
+            // interior chunk: every slot a token, none of them the last
+            const uint32_t o = ((d[0] ^ Z) | (d[1] ^ Z)) | ((d[2] ^ Z) | (d[3] ^ Z)) |
+                               ((d[4] ^ Z) | (d[5] ^ Z)) | ((d[6] ^ Z) | (d[7] ^ Z));
+            if (f.pcls == 0 && vw::ballot(o != 0) == 0) {
+                // one 0|0 run through the whole chunk: only full 127-chunks
+                // complete.  Token t has run offset t + 1 - prs; count the
+                // multiples of 127 in [a0 + 1, a0 + 512].
+                const uint32_t a0 = (uint32_t)tf + 1 - f.prs;
+                const uint32_t kfull = (a0 + SLOTS8) / 127 - a0 / 127;
+                if (l < kfull) ring_put(r, r.wpos + l, 0x7Fu);
+                r.wpos += kfull;
+                ring_flush(r, false);
+                return true;
+            }
+            if (vw::ballot((o & 0xFFFEFFFEu) != 0) == 0) {
+                clean8<false>(d, t0, tf, f, r);
+                return true;
+            }
+        } else {
+            // last chunk: slots past T-1 are ignored; token T-1 has no TAB after it
+            bool bad = false;
+#pragma unroll
+            for (int j = 0; j < (int)TPL8; j++) {
+                const int32_t t = t0 + j;
+                const uint32_t m = (uint32_t)t < T ? ((uint32_t)t + 1u == T ? 0x00FEFFFEu : 0xFFFEFFFEu) : 0u;
+                bad |= ((d[j] ^ Z) & m) != 0;
+            }
+            if (vw::ballot(bad) == 0) {
+                clean8<true>(d, t0, tf, f, r);
+                return true;
+            }
+        }
+    }
+    return false;   // escapes or odd bytes: the caller runs gt_general on this chunk
+}
+
 __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring &r, uint32_t *rec_bytes) {
     const uint32_t l = vw::lane_id();
     const uint32_t lead = (uint32_t)(reinterpret_cast<uintptr_t>(line) & 15);
     const uint8_t *A = line - lead;
     const uint32_t span = lead + len;
     if (len == 0) return false;
-    // loads past the row (prefetch overrun, last chunk) read 0: no clamping
-    const vw::brsrc rs = vw::make_rsrc(A, (span + 3u) & ~3u);
-    const uint32_t lo16 = BPL * l;
     const uint32_t nch = (span + CHUNK - 1) / CHUNK;
+    const uint32_t lo16 = BPL * l;
     FastState f;
     f.nf = 0; f.carryT = 1; f.gt0 = -1; f.T = 0; f.phi = 0; f.pcls = CLS_NONE; f.prs = 0;
     r.wpos = 8;
     r.fpos = 0;
 
-    // three chunk buffers: while b0 is processed, b1 and b2 are in flight
-    Chunk b0 = load_chunk(rs, 0, lo16);
-    Chunk b1 = load_chunk(rs, 1, lo16);
-    Chunk b2 = load_chunk(rs, 2, lo16);
-    vw::pin_loads();
-    // (readfirst marks the wave-uniform loop state as uniform for the
-    // compiler: scalar loop control, no exec-masked loop structurisation)
+    // prefix phase: 1 KiB chunks of the line until the first sample starts
+    // (loads past the row read 0: no clamping)
+    const vw::brsrc rsA = vw::make_rsrc(A, (span + 3u) & ~3u);
     uint32_t c = 0;
-    int st = (int)vw::readfirst((uint32_t)fast_prefix_step(b0, 0, lead, len, f, r));
-    if (st == 2) return false;
-    if (st == 0) {
-        // prefix longer than one chunk (rare): walk it, then restart the
-        // three-deep prefetch at the chunk holding the first sample
-        for (;;) {
-            c = vw::readfirst(c + 1);
-            if (c >= nch) return false;   // < 10 fields
-            const Chunk t = load_chunk(rs, c, lo16);
-            st = (int)vw::readfirst((uint32_t)fast_prefix_step(t, c, lead, len, f, r));
-            if (st == 2) return false;
-            if (st == 1) break;
-        }
-        b0 = load_chunk(rs, c, lo16);
-        b1 = load_chunk(rs, c + 1, lo16);
-        b2 = load_chunk(rs, c + 2, lo16);
-        vw::pin_loads();
-    }
-    // genotype chunks, unrolled x3 over named buffers: no register copies
-    // and a single loop exit (early exits merge into the latch and make
-    // hipcc's vmcnt tracking fall back to vmcnt(0)), so two chunks stay in
-    // flight behind every step.  Loads past the row clamp to its last block.
-    bool ok = true;
+    Chunk b = load_chunk(rsA, 0, lo16);
+    int st;
     for (;;) {
-        ok = vw::readfirst(ok && fast_gt_step(b0, c, lead, f, r));
-        b0 = load_chunk(rs, c + 3, lo16);
-        vw::pin_loads();
-        if (ok && c + 1 < nch) ok = vw::readfirst(fast_gt_step(b1, c + 1, lead, f, r));
-        b1 = load_chunk(rs, c + 4, lo16);
-        vw::pin_loads();
-        if (ok && c + 2 < nch) ok = vw::readfirst(fast_gt_step(b2, c + 2, lead, f, r));
-        b2 = load_chunk(rs, c + 5, lo16);
-        vw::pin_loads();
-        c = vw::readfirst(c + 3);
-        if (!ok || c >= nch) break;
+        st = (int)vw::readfirst((uint32_t)fast_prefix_step(b, c, lead, len, f, r));
+        if (st != 0) break;
+        c = vw::readfirst(c + 1);
+        if (c >= nch) return false;   // < 10 fields
+        b = load_chunk(rsA, c, lo16);
     }
-    if (!ok) return false;
-    const uint32_t T = f.T, pcls = f.pcls, prs = f.prs;
+    if (st == 2) return false;
+
+    // genotype phase: runs of clean chunks, three chunks in flight, broken
+    // by the (rare) chunks that need the general step.  The inner loop has a
+    // single exit (early exits merge into the latch and make hipcc's vmcnt
+    // tracking fall back to vmcnt(0)); the general step sits outside it so
+    // its registers do not add to the prefetch buffers'.
+    const uint32_t phi = f.phi, T = f.T;
+    const vw::brsrc rsG = vw::make_rsrc(line + f.gt0 - phi, (phi + len - (uint32_t)f.gt0 + 3u) & ~3u);
+    const uint32_t ncG = (T + SLOTS8 - 1) / SLOTS8;
+    const uint32_t lo32 = BPL8 * l;
+    uint32_t C0 = 0;
+    for (;;) {
+        Chunk8 b0 = load_chunk8(rsG, C0, lo32);
+        Chunk8 b1 = load_chunk8(rsG, C0 + 1, lo32);
+        Chunk8 b2 = load_chunk8(rsG, C0 + 2, lo32);
+        vw::pin_loads();
+        uint32_t C = C0, gen = C0;
+        bool ok = true;
+        for (;;) {
+            if (ok) { ok = vw::readfirst(gt_step8(b0, C, f, r)); gen = C; }
+            b0 = load_chunk8(rsG, C + 3, lo32);
+            vw::pin_loads();
+            if (ok && C + 1 < ncG) { ok = vw::readfirst(gt_step8(b1, C + 1, f, r)); gen = C + 1; }
+            b1 = load_chunk8(rsG, C + 4, lo32);
+            vw::pin_loads();
+            if (ok && C + 2 < ncG) { ok = vw::readfirst(gt_step8(b2, C + 2, f, r)); gen = C + 2; }
+            b2 = load_chunk8(rsG, C + 5, lo32);
+            vw::pin_loads();
+            C = vw::readfirst(C + 3);
+            if (!ok || C >= ncG) break;
+        }
+        if (ok) break;
+        // chunk `gen`: the general step over its two 1 KiB halves
+        for (uint32_t h = 0; h < 2; h++) {
+            const Chunk hc = load_chunk(rsG, 2 * gen + h, lo16);
+            if (!vw::readfirst(gt_general(hc, (int32_t)(gen * SLOTS8 + h * 64 * TPL), f, r))) return false;
+        }
+        C0 = vw::readfirst(gen + 1);
+        if (C0 >= ncG) break;
+    }
+    const uint32_t pcls = f.pcls, prs = f.prs;
     const int32_t gt0 = f.gt0;
     // row end: pending chunk of the last run, then '\n'
     uint32_t extra = 0, pb = 0;
@@ -574,7 +634,6 @@ __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring
 }
 
 
-// ---------------------------------------------------------------------------
 // General path: any line.  64-byte windows, one byte per lane (plus a 3-byte
 // look-ahead for the token-length test), ballot/scan bookkeeping.  Handles
 // empty fields anywhere, 9-column rows, tokens of any length, CR, and the
