@@ -302,7 +302,7 @@ __device__ bool gt_general(const Chunk &cur, int32_t tf, FastState &f, Ring &r) 
         const bool s = cl[j] != CLS_NONE && (cl[j] != pj || cl[j] == CLS_ESC);
         if (s) lane_rs = u0 + j;
     }
-    const uint32_t rin = vw::umax(vw::shr1(vw::scan_max(lane_rs), 0u), f.prs);
+    const uint32_t rin = vw::umax(vw::shr1z(vw::scan_max(lane_rs)), f.prs);
     uint32_t mp = mod_cap((uint32_t)(t0 + (int32_t)MOD_BIAS) - rin, p0 == 0);
     uint32_t lane_sum = 0, lrs = rin;
     uint32_t e1_m = 0, full_m = 0, b1s[TPL];
@@ -445,7 +445,7 @@ __device__ __forceinline__ void clean8(const uint32_t (&d)[TPL8], int32_t t0, in
     // run start (+1) of the lane's last start; wave max-scan -> run entering each lane
     const uint32_t lane_rs = sb ? (uint32_t)(t0 + 8) - ((uint32_t)__builtin_clz(sb) >> 2) : 0u;
     const uint32_t incl = vw::scan_max(lane_rs);
-    const uint32_t rin = vw::umax(vw::shr1(incl, 0u), f.prs);
+    const uint32_t rin = vw::umax(vw::shr1z(incl), f.prs);
     const uint32_t p0 = cpL & 3u;
     const bool is00 = p0 == 0;
     const uint32_t cap = is00 ? 127u : 31u;

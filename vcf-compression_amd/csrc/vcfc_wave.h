@@ -32,6 +32,10 @@ __device__ __forceinline__ uint32_t readfirst(uint32_t v) {
 __device__ __forceinline__ uint32_t shr1(uint32_t v, uint32_t fill) {
     return __builtin_amdgcn_update_dpp(fill, v, 0x138, 0xf, 0xf, false);
 }
+// lane i receives lane i-1's value; lane 0 receives 0 (one v_mov_b32_dpp)
+__device__ __forceinline__ uint32_t shr1z(uint32_t v) {
+    return __builtin_amdgcn_update_dpp(0u, v, 0x138, 0xf, 0xf, true);
+}
 // lane i receives lane i+1's value; lane 63 receives `fill` (DPP wave_shl:1)
 __device__ __forceinline__ uint32_t shl1(uint32_t v, uint32_t fill) {
     return __builtin_amdgcn_update_dpp(fill, v, 0x130, 0xf, 0xf, false);
@@ -40,14 +44,25 @@ __device__ __forceinline__ uint32_t shl1(uint32_t v, uint32_t fill) {
 __device__ __forceinline__ uint32_t shfl(uint32_t v, uint32_t src) {
     return __builtin_amdgcn_ds_bpermute(src << 2, v);
 }
-// inclusive add scan over the wave
+// inclusive add scan over the wave.  Written out in asm: hipcc does not
+// always fold the update_dpp + add pairs into v_add_u32_dpp (3 VALU per step
+// instead of 1).  s_nop 1 covers the VALU-write -> DPP-read hazard (2 wait
+// states), including the producer of v before the block.
 __device__ __forceinline__ uint32_t scan_add(uint32_t v) {
-    v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false);
-    v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false);
-    v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false);
-    v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false);
-    v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);
-    v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false);
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_add_u32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "s_nop 1\n\t"
+        "v_add_u32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "s_nop 1\n\t"
+        "v_add_u32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "s_nop 1\n\t"
+        "v_add_u32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "s_nop 1\n\t"
+        "v_add_u32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_add_u32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf"
+        : "+v"(v));
     return v;
 }
 __device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
