@@ -118,6 +118,18 @@ uint64_t vcfc_compress_bound(uint64_t in_bytes);
 int vcfc_compress_buffer(vcfc_ctx *ctx, const uint8_t *in, uint64_t n, uint8_t *out, uint64_t out_cap,
                          uint64_t *out_len, int64_t *err_line);
 
+/* ---- decoder: decompress2_fd (reference src/compress.cpp:1214-1257,
+ * decompress2_data_line :741-986) ----------------------------------------
+ * .vcfc bytes -> VCF text, byte-identical to the reference's `main
+ * decompress`.  The sample count comes from the header line (as in the
+ * reference).  On VCFC_E_FORMAT (where the reference throws) the output holds
+ * the header and every line the reference writes before throwing.
+ * vcfc_decompress_buffer: VCFC_E_NOSPACE if out_cap is short; *out_len is
+ * then the size needed. */
+int vcfc_decompress_buffer(vcfc_ctx *ctx, const uint8_t *in, uint64_t in_bytes, uint8_t *out, uint64_t out_cap,
+                           uint64_t *out_len);
+int vcfc_decompress_file(vcfc_ctx *ctx, const char *in_vcfc, const char *out_vcf);
+
 /* ---- sparse layout: sparsify_file (reference src/sparse.cpp:290-580) -------
  * Record i of the .vcfc goes to data_start + (300e6 + POS_i) * 16384
  * (compute_sparse_offset, src/sparse.cpp:18-51) behind a 16-byte prefix

@@ -223,14 +223,18 @@ int vcfo_decompress(const uint8_t *in, size_t n, uint8_t *out, size_t cap, size_
             DEMIT(c3);
         }
     }
-    /* data lines: decompress2_data_line :741-986 */
+    /* data lines: decompress2_data_line :741-986.  decompress2_fd writes the
+     * header lines once they all parse, then each line as it completes
+     * (:1222-1250): on an error the output holds exactly those bytes. */
+    size_t committed = o;
+#define FAIL() do { *out_len = committed; return VCFO_E_FORMAT; } while (0)
     for (;;) {
         if (n - ip < 8) break;                     /* 0 or partial header: stop (:768-774) */
         const uint8_t *h = in + ip;
-        if ((h[0] >> 6) != 3 || (h[4] >> 6) != 3) return VCFO_E_FORMAT; /* utils.hpp:200-206 */
+        if ((h[0] >> 6) != 3 || (h[4] >> 6) != 3) FAIL(); /* utils.hpp:200-206 */
         uint32_t req = ((uint32_t)(h[4] & 0x3F) << 24) | ((uint32_t)h[5] << 16) | ((uint32_t)h[6] << 8) | h[7];
         ip += 8;
-        if (req == 0 || n - ip < req) return VCFO_E_FORMAT;
+        if (req == 0 || n - ip < req) FAIL();
         size_t tabs = 0;
         /* linebuf.append(buf): C string, stops at the first NUL (:798) */
         int nul = 0;
@@ -241,10 +245,10 @@ int vcfo_decompress(const uint8_t *in, size_t n, uint8_t *out, size_t cap, size_
             if (!nul) DEMIT(b);
         }
         ip += req;
-        if (tabs != 9 && !(tabs == 8 && sample_count == 0)) return VCFO_E_FORMAT;
+        if (tabs != 9 && !(tabs == 8 && sample_count == 0)) FAIL();
         uint64_t got = 0;
         while (got < sample_count) {
-            if (ip >= n) return VCFO_E_FORMAT;
+            if (ip >= n) FAIL();
             uint8_t b = in[ip++];
             if ((b & 0x80) == 0) {
                 uint32_t cnt = b & 0x7F;
@@ -254,11 +258,11 @@ int vcfo_decompress(const uint8_t *in, size_t n, uint8_t *out, size_t cap, size_
             } else if ((b & 0xE0) == 0xE0) {
                 uint32_t ucount = b & 0x1F, u = 0;
                 while (u < ucount) {
-                    if (ip >= n) return VCFO_E_FORMAT;
+                    if (ip >= n) FAIL();
                     uint8_t x = in[ip++];
                     if (x == '\n') {
                         u++; got++;
-                        if (u != ucount) return VCFO_E_FORMAT;
+                        if (u != ucount) FAIL();
                         ip--;                     /* fseek(-1): re-read as the line end */
                     } else if (x == '\t') {
                         u++; got++;
@@ -277,10 +281,12 @@ int vcfo_decompress(const uint8_t *in, size_t n, uint8_t *out, size_t cap, size_
                 }
             }
         }
-        if (ip >= n) return VCFO_E_FORMAT;
-        if (in[ip++] != '\n') return VCFO_E_FORMAT;
+        if (ip >= n) FAIL();
+        if (in[ip++] != '\n') FAIL();
         DEMIT('\n');
+        committed = o;
     }
+#undef FAIL
     *out_len = o;
     return VCFO_OK;
 }

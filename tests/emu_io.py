@@ -21,6 +21,8 @@ def lib():
                                       ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
                                       ctypes.POINTER(ctypes.c_uint32)]
         L.emu_sparse_plan.argtypes = [vp, vp, ctypes.c_uint64, ctypes.c_uint64, vp, vp, vp]
+        L.emu_decompress.argtypes = [ctypes.c_char_p, ctypes.c_uint64, vp, ctypes.c_uint64,
+                                     ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint64]
         _lib = L
     return _lib
 
@@ -77,3 +79,12 @@ def emu_sparse_plan(recs, rec_off, data_start):
     lib().emu_sparse_plan(src.ctypes.data, ro.ctypes.data, n, data_start, fo.ctypes.data, pf.ctypes.data,
                           stt.ctypes.data)
     return fo[:n], pf[:16 * n].tobytes(), stt
+
+
+def emu_decompress(data, out_batch=1 << 16, cap=None):
+    """Run the product decode driver + kernels on the emulator: (status, bytes)."""
+    cap = cap or len(data) * 600 + 4096
+    out = np.zeros(cap, dtype=np.uint8)
+    n = ctypes.c_uint64(0)
+    st = lib().emu_decompress(data, len(data), out.ctypes.data, cap, ctypes.byref(n), out_batch)
+    return st, out[:n.value].tobytes()

@@ -6,6 +6,7 @@
 #include <cstring>
 #include <vector>
 #include "vcfc_device.h"
+#include "vcfc_decode_driver.h"
 #include "emu.h"
 
 extern "C" int emu_encode_rows(const uint8_t *buf, const uint64_t *line_off, const uint32_t *line_len,
@@ -42,4 +43,37 @@ hipError_t vcfc_sparse_plan_launch(const uint8_t *recs, const uint64_t *rec_off,
 extern "C" int emu_sparse_plan(const uint8_t *recs, const uint64_t *rec_off, uint64_t n, uint64_t data_start,
                                uint64_t *file_off, uint8_t *prefix, uint64_t *status) {
     return (int)vcfc_sparse_plan_launch(recs, rec_off, n, data_start, file_off, prefix, status, nullptr);
+}
+
+// The product decode driver (csrc/vcfc_decode_driver.h) over host memory:
+// header parse + decode_section with small output batches (exercises the
+// batching).  Returns the driver status; *out_len = bytes produced.
+namespace {
+struct HostBuffers : vcfc_dec::Buffers {
+    std::vector<uint8_t> b[N_SLOTS];
+    void *get(int slot, uint64_t bytes) override {
+        if (b[slot].size() < bytes) b[slot].assign(bytes, 0xCD);   // poison
+        return b[slot].data();
+    }
+};
+}  // namespace
+
+extern "C" int emu_decompress(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len,
+                              uint64_t out_batch) {
+    uint64_t data_off = 0, S = 0;
+    *out_len = 0;
+    int st = vcfc_dec::parse_header(in, n, &data_off, &S);
+    if (st) return st;
+    uint64_t o = 0;
+    auto sink = [&](const uint8_t *p, uint64_t k) {
+        if (o + k > cap) return false;
+        memcpy(out + o, p, k);
+        o += k;
+        return true;
+    };
+    sink(in, data_off);
+    HostBuffers B;
+    st = vcfc_dec::decode_section(in + data_off, n - data_off, S, B, nullptr, sink, out_batch);
+    *out_len = o;
+    return st;
 }

@@ -21,6 +21,7 @@ struct dim3 {
 struct uint4 { uint32_t x, y, z, w; };
 struct uint2 { uint32_t x, y; };
 inline uint4 make_uint4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) { return uint4{a, b, c, d}; }
+inline uint2 make_uint2(uint32_t a, uint32_t b) { return uint2{a, b}; }
 
 #define threadIdx (emu::g.cur->tid)
 #define blockIdx (emu::g.bid)
@@ -37,6 +38,9 @@ inline const char *hipGetErrorString(hipError_t) { return "emu"; }
 inline hipError_t hipMemsetAsync(void *p, int v, size_t n, hipStream_t) { memset(p, v, n); return hipSuccess; }
 inline hipError_t hipMemcpyAsync(void *d, const void *s, size_t n, int, hipStream_t) { memmove(d, s, n); return hipSuccess; }
 #define hipMemcpyDeviceToDevice 3
+#define hipMemcpyHostToDevice 1
+#define hipMemcpyDeviceToHost 2
+inline hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
 
 inline void __syncthreads() { emu::collective(emu::OP_SYNCTHREADS, 0, 0, 0); }
 

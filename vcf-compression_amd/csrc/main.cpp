@@ -1,5 +1,5 @@
 // main.cpp -- CLI with the reference's argv contract (src/main.cpp:4028-4185)
-// for the encode path: `main compress <in.vcf> <out.vcfc>`.  Data lines are
+// for the codec path: `main compress|decompress|sparsify <in> <out>`.  Data lines are
 // encoded on the GPU through libvcfc.so.  Error messages mirror the
 // reference's exceptions (which terminate the reference process).
 #include <cstdio>
@@ -47,6 +47,34 @@ int main(int argc, char **argv) {
         if (st == VCFC_E_8COLS) {
             fprintf(stderr, "terminate called after throwing an instance of 'std::length_error'\n"
                             "  what():  vector::_M_default_append (input line %lld)\n", (long long)err_line);
+            return 134;
+        }
+        if (st != VCFC_OK) {
+            fprintf(stderr, "Error in compression of file: %s\n", vcfc_strerror(st));
+            return 1;
+        }
+        return 0;
+    }
+    if (action == "decompress") {
+        // src/main.cpp:4038-4056 -> decompress2_fd (src/compress.cpp:1214)
+        if (argc < 4) return usage();
+        if (!file_exists(argv[2])) printf("Input file does not exist: %s\n", argv[2]);
+        if (std::string(argv[2]) == argv[3]) {
+            fprintf(stderr, "terminate called after throwing an instance of 'std::runtime_error'\n"
+                            "  what():  input and output file are the same\n");
+            return 134;
+        }
+        vcfc_ctx *ctx = nullptr;
+        int st = vcfc_ctx_create(0, &ctx);
+        if (st != VCFC_OK) {
+            fprintf(stderr, "vcfc: %s\n", vcfc_strerror(st));
+            return 1;
+        }
+        st = vcfc_decompress_file(ctx, argv[2], argv[3]);
+        vcfc_ctx_destroy(ctx);
+        if (st == VCFC_E_FORMAT) {
+            fprintf(stderr, "terminate called after throwing an instance of 'VcfValidationError'\n"
+                            "  what():  %s\n", vcfc_strerror(st));
             return 134;
         }
         if (st != VCFC_OK) {

@@ -17,6 +17,7 @@
 #include <sys/uio.h>
 
 #include "vcfc.h"
+#include "vcfc_decode_driver.h"
 #include "vcfc_device.h"
 
 hipError_t vcfc_sparse_plan_launch(const uint8_t *recs, const uint64_t *rec_off, uint64_t n, uint64_t data_start,
@@ -92,38 +93,9 @@ struct MappedFile {
     }
 };
 
-// Metadata + header lines of a .vcfc (decompress2_metadata_headers[_fd],
-// reference src/compress.cpp:995-1211): '##' lines then one '#' line, each
-// '\n'-terminated; sample_count = TABs after the 8th on the header line.  A
-// file with no data lines is an error there (the stale first byte '#' after
-// EOF reads as a header row after the header).
+// Metadata + header lines of a .vcfc: vcfc_dec::parse_header.
 int parse_vcfc_header(const uint8_t *in, uint64_t n, uint64_t *data_off, uint64_t *sample_count) {
-    bool got_meta = false, got_header = false;
-    uint64_t ip = 0, samples = 0;
-    for (;;) {
-        if (ip >= n) return VCFC_E_FORMAT;
-        const uint8_t c1 = in[ip];
-        if (c1 != '#') {
-            if (!got_meta || !got_header) return VCFC_E_FORMAT;
-            break;
-        }
-        if (got_header) return VCFC_E_FORMAT;
-        if (ip + 1 >= n) return VCFC_E_FORMAT;
-        const uint8_t c2 = in[ip + 1];
-        if (c2 == '#') got_meta = true;
-        else { if (!got_meta) return VCFC_E_FORMAT; got_header = true; }
-        uint64_t q = ip + 2, tabs = 0;
-        for (;;) {
-            if (q >= n) return VCFC_E_FORMAT;
-            const uint8_t c3 = in[q++];
-            if (c3 == '\n') break;
-            if (got_header && c3 == '\t' && ++tabs > 8) samples++;
-        }
-        ip = q;
-    }
-    *data_off = ip;
-    if (sample_count) *sample_count = samples;
-    return VCFC_OK;
+    return vcfc_dec::parse_header(in, n, data_off, sample_count);
 }
 
 // Record starts by hopping the LEN headers (read_compressed_line_length_headers,
@@ -157,6 +129,17 @@ int write_all_at(int fd, const void *p, uint64_t len, uint64_t off) {
 void put_be64(uint8_t *o, uint64_t v) {
     for (int k = 0; k < 8; k++) o[k] = (uint8_t)(v >> (56 - 8 * k));
 }
+
+// The decoder's device buffers live in the context.
+struct CtxDecodeBuffers : vcfc_dec::Buffers {
+    vcfc_ctx *c;
+    explicit CtxDecodeBuffers(vcfc_ctx *cc) : c(cc) {}
+    void *get(int slot, uint64_t bytes) override {
+        DevBuf *b = slot == IN ? &c->in : slot == REC ? &c->rec : slot == WS ? &c->ws : slot == OUT ? &c->out
+                  : slot == LINE_OFF ? &c->off : &c->err;
+        return b->ensure(bytes) == hipSuccess ? b->p : nullptr;
+    }
+};
 
 }  // namespace
 
@@ -597,6 +580,59 @@ int vcfc_compress_file(vcfc_ctx *c, const char *in_path, const char *out_path, i
     }
     close(ofd);
     return s;
+}
+
+// ---- decoder: decompress2_fd, reference
+// src/compress.cpp:1214-1257 ------------------------------------------------
+
+int vcfc_decompress_buffer(vcfc_ctx *c, const uint8_t *in, uint64_t n, uint8_t *out, uint64_t out_cap,
+                           uint64_t *out_len) {
+    if (!c || (!in && n) || (!out && out_cap) || !out_len) return VCFC_E_ARG;
+    *out_len = 0;
+    if (hipSetDevice(c->device) != hipSuccess) return VCFC_E_HIP;
+    uint64_t data_off = 0, S = 0;
+    int st = parse_vcfc_header(in, n, &data_off, &S);
+    if (st) return st;   // the reference writes nothing before its header check passes
+    uint64_t o = 0;
+    bool fits = true;
+    auto sink = [&](const uint8_t *p, uint64_t k) {
+        if (fits && o + k <= out_cap) memcpy(out + o, p, k);
+        else fits = false;
+        o += k;
+        return true;
+    };
+    sink(in, data_off);
+    CtxDecodeBuffers B(c);
+    st = vcfc_dec::decode_section(in + data_off, n - data_off, S, B, c->stream, sink);
+    *out_len = o;
+    if (!fits) return VCFC_E_NOSPACE;
+    return st;
+}
+
+int vcfc_decompress_file(vcfc_ctx *c, const char *in_path, const char *out_path) {
+    if (!c || !in_path || !out_path) return VCFC_E_ARG;
+    if (hipSetDevice(c->device) != hipSuccess) return VCFC_E_HIP;
+    MappedFile f;
+    int st = f.open_ro(in_path);
+    if (st) return st;
+    // the reference opens (truncates) the output before reading the headers
+    int fd = open(out_path, O_CREAT | O_TRUNC | O_WRONLY, 0644);
+    if (fd < 0) return VCFC_E_IO;
+    uint64_t data_off = 0, S = 0;
+    st = parse_vcfc_header(f.p, f.n, &data_off, &S);
+    uint64_t o = 0;
+    auto sink = [&](const uint8_t *p, uint64_t k) {
+        if (write_all_at(fd, p, k, o)) return false;
+        o += k;
+        return true;
+    };
+    if (!st && !sink(f.p, data_off)) st = VCFC_E_IO;
+    if (!st) {
+        CtxDecodeBuffers B(c);
+        st = vcfc_dec::decode_section(f.p + data_off, f.n - data_off, S, B, c->stream, sink);
+    }
+    close(fd);
+    return st;
 }
 
 }  // extern "C"

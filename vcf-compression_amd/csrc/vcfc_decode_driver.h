@@ -1,0 +1,175 @@
+// vcfc_decode_driver.h -- host driver of the GPU decoder,
+// shared by the C ABI (vcfc_api.cpp) and the CPU emulator harness
+// (tests/simt_emu/emu_api.cpp), so the same control flow is tested on both.
+//
+// It mirrors decompress2_fd's data-line loop (reference
+// src/compress.cpp:1214-1257 + decompress2_data_line :741-986):
+//   1. hop the LEN headers on the host to find record starts;
+//   2. plan every record on the GPU (line sizes, statuses, first failure);
+//   3. write the lines before the first failure in output batches;
+//   4. where a record's byte-serial parse ends off its LEN hop, or hopping
+//      stopped early, decode the rest the reference's way (k_dec_stream);
+//   5. VCFC_E_FORMAT where the reference throws, after sinking every line
+//      the reference would have written first.
+#pragma once
+#include <cstdint>
+#include <functional>
+#include <vector>
+
+#include "vcfc_device.h"
+
+namespace vcfc_dec {
+
+constexpr int ST_OK = 0, ST_E_HIP = 6, ST_E_IO = 7, ST_E_FORMAT = 8;   // = include/vcfc.h codes
+
+// Device buffers, owned by the caller (one slot each; contents not kept).
+struct Buffers {
+    virtual ~Buffers() {}
+    enum { IN = 0, REC, WS, OUT, LINE_OFF, SMALL, N_SLOTS };
+    virtual void *get(int slot, uint64_t bytes) = 0;   // nullptr on failure
+};
+
+// Appends decoded bytes (host memory); false aborts with ST_E_IO.
+using Sink = std::function<bool(const uint8_t *, uint64_t)>;
+
+// Metadata + header lines of a .vcfc (decompress2_metadata_headers[_fd],
+// reference src/compress.cpp:995-1211): '##' lines then one '#' line, each
+// '\n'-terminated; sample_count = TABs after the 8th on the header line.  A
+// file with no data lines is an error there (the stale first byte '#' after
+// EOF reads as a header row after the header).
+inline int parse_header(const uint8_t *in, uint64_t n, uint64_t *data_off, uint64_t *sample_count) {
+    bool got_meta = false, got_header = false;
+    uint64_t ip = 0, samples = 0;
+    for (;;) {
+        if (ip >= n) return ST_E_FORMAT;
+        const uint8_t c1 = in[ip];
+        if (c1 != '#') {
+            if (!got_meta || !got_header) return ST_E_FORMAT;
+            break;
+        }
+        if (got_header) return ST_E_FORMAT;
+        if (ip + 1 >= n) return ST_E_FORMAT;
+        const uint8_t c2 = in[ip + 1];
+        if (c2 == '#') got_meta = true;
+        else { if (!got_meta) return ST_E_FORMAT; got_header = true; }
+        uint64_t q = ip + 2, tabs = 0;
+        for (;;) {
+            if (q >= n) return ST_E_FORMAT;
+            const uint8_t c3 = in[q++];
+            if (c3 == '\n') break;
+            if (got_header && c3 == '\t' && ++tabs > 8) samples++;
+        }
+        ip = q;
+    }
+    *data_off = ip;
+    if (sample_count) *sample_count = samples;
+    return ST_OK;
+}
+
+// Record starts by LEN hops from 0 (read_compressed_line_length_headers,
+// compress.cpp:270-331): records lying wholly inside [0, n) whose two
+// headers carry extension bits 11 (utils.hpp:198-206) and LEN >= 4.
+// rec.back() = where hopping stopped (n, or a record the byte-serial path
+// must look at: short tail, bad header bits, LEN past the end).
+inline void hop(const uint8_t *in, uint64_t n, std::vector<uint64_t> &rec) {
+    rec.clear();
+    uint64_t p = 0;
+    while (n - p >= 8) {
+        const uint8_t *h = in + p;
+        if ((h[0] >> 6) != 3u || (h[4] >> 6) != 3u) break;
+        const uint64_t L = ((uint64_t)(h[0] & 0x3Fu) << 24) | ((uint64_t)h[1] << 16) | ((uint64_t)h[2] << 8) | h[3];
+        if (L < 4 || L + 4 > n - p) break;
+        rec.push_back(p);
+        p += 4 + L;
+    }
+    rec.push_back(p);
+}
+
+// Decode a .vcfc data section (host bytes h_in[0, n); uploaded here).
+inline int decode_section(const uint8_t *h_in, uint64_t n, uint64_t S, Buffers &B, hipStream_t s, const Sink &sink,
+                          uint64_t out_batch = 1ull << 30) {
+    std::vector<uint64_t> rec;
+    hop(h_in, n, rec);
+    const uint64_t nrec = rec.size() - 1;
+    uint8_t *d_in = static_cast<uint8_t *>(B.get(Buffers::IN, n + 64));
+    uint64_t *d_small = static_cast<uint64_t *>(B.get(Buffers::SMALL, 64));
+    if (!d_in || !d_small) return ST_E_HIP;
+    if (n && hipMemcpyAsync(d_in, h_in, n, hipMemcpyHostToDevice, s) != hipSuccess) return ST_E_HIP;
+    uint64_t p_stream = rec.back();   // byte-serial continuation point (if >= 8 bytes remain there)
+    bool failed = false;
+    if (nrec) {
+        const VcfcDecodeLayout L = vcfc_decode_workspace_layout(nrec);
+        uint64_t *d_rec = static_cast<uint64_t *>(B.get(Buffers::REC, 8 * (nrec + 1)));
+        uint8_t *ws = static_cast<uint8_t *>(B.get(Buffers::WS, L.total));
+        uint64_t *d_loff = static_cast<uint64_t *>(B.get(Buffers::LINE_OFF, 8 * (nrec + 1)));
+        if (!d_rec || !ws || !d_loff) return ST_E_HIP;
+        if (hipMemcpyAsync(d_rec, rec.data(), 8 * (nrec + 1), hipMemcpyHostToDevice, s) != hipSuccess) return ST_E_HIP;
+        VcfcDecodeArgs a;
+        a.in = d_in; a.n_bytes = n; a.rec_start = d_rec; a.n = nrec; a.S = S;
+        a.out = nullptr; a.out_cap = 0; a.line_off = d_loff;
+        a.st = reinterpret_cast<uint32_t *>(ws + L.st);
+        a.line_size = reinterpret_cast<uint32_t *>(ws + L.line_size);
+        a.end = reinterpret_cast<uint64_t *>(ws + L.end);
+        a.seq_list = reinterpret_cast<uint32_t *>(ws + L.seq_list);
+        a.seq_count = reinterpret_cast<uint32_t *>(ws + L.seq_count);
+        a.err = reinterpret_cast<uint64_t *>(ws + L.err);
+        a.partials = reinterpret_cast<uint64_t *>(ws + L.partials);
+        if (vcfc_decode_plan(a, s) != hipSuccess) return ST_E_HIP;
+        uint64_t err = 0;
+        if (hipMemcpyAsync(&err, a.err, 8, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+            return ST_E_HIP;
+        uint64_t n_lines = nrec;
+        if (err != VCFCD_NO_ERROR) {
+            const uint64_t k = err >> 8;
+            const uint32_t code = (uint32_t)(err & 0xFF);
+            if (code == 2) {   // parse of record k ends off its hop: keep its line, continue byte-serially
+                n_lines = k + 1;
+                if (hipMemcpyAsync(&p_stream, a.end + k, 8, hipMemcpyDeviceToHost, s) != hipSuccess) return ST_E_HIP;
+            } else {
+                n_lines = k;
+                failed = true;
+            }
+        }
+        std::vector<uint64_t> loff(n_lines + 1);
+        if (hipMemcpyAsync(loff.data(), d_loff, 8 * (n_lines + 1), hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return ST_E_HIP;
+        std::vector<uint8_t> host;
+        for (uint64_t i0 = 0; i0 < n_lines;) {
+            uint64_t i1 = i0 + 1;
+            while (i1 < n_lines && loff[i1 + 1] - loff[i0] <= out_batch) i1++;
+            const uint64_t bytes = loff[i1] - loff[i0];
+            uint8_t *d_out = static_cast<uint8_t *>(B.get(Buffers::OUT, bytes + 64));
+            if (!d_out) return ST_E_HIP;
+            a.out = d_out - loff[i0];   // lines are written at out + line_off[i]
+            a.out_cap = loff[i1];
+            if (vcfc_decode_write(a, i0, i1, s) != hipSuccess) return ST_E_HIP;
+            host.resize(bytes);
+            if (hipMemcpyAsync(host.data(), d_out, bytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                hipStreamSynchronize(s) != hipSuccess)
+                return ST_E_HIP;
+            if (!sink(host.data(), bytes)) return ST_E_IO;
+            i0 = i1;
+        }
+    }
+    if (failed) return ST_E_FORMAT;
+    if (n - p_stream < 8) return ST_OK;   // clean end (:768-774)
+    // byte-serial continuation: count, then write
+    uint64_t st[3] = {0, 0, 0};
+    if (vcfc_decode_stream(d_in, n, p_stream, S, nullptr, d_small, s) != hipSuccess ||
+        hipMemcpyAsync(st, d_small, 24, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+        return ST_E_HIP;
+    if (st[1]) {
+        uint8_t *d_out = static_cast<uint8_t *>(B.get(Buffers::OUT, st[1] + 64));
+        if (!d_out) return ST_E_HIP;
+        std::vector<uint8_t> host(st[1]);
+        if (vcfc_decode_stream(d_in, n, p_stream, S, d_out, d_small, s) != hipSuccess ||
+            hipMemcpyAsync(host.data(), d_out, st[1], hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return ST_E_HIP;
+        if (!sink(host.data(), st[1])) return ST_E_IO;
+    }
+    return st[0] == 2 ? ST_E_FORMAT : ST_OK;
+}
+
+}  // namespace vcfc_dec

@@ -52,3 +52,40 @@ VcfcWorkspaceLayout vcfc_encode_workspace_layout(uint64_t n, uint64_t total_line
 // If `ev` is non-null, ev[0..4] are recorded before the slot scan, after it,
 // after k_encode, after the size scan and after k_compact.
 hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t stream, hipEvent_t *ev = nullptr);
+
+// ---------------------------------------------------------------------------
+// Decoder (vcfc_decode.hip).  Records of one batch, located by LEN hops.
+struct VcfcDecodeArgs {
+    const uint8_t *in;          // data section bytes (device)
+    uint64_t n_bytes;           // bytes available from `in` (the byte-serial parse may read past a record)
+    const uint64_t *rec_start;  // n + 1 record offsets into `in` (rec_start[n] = end of the hopped range)
+    uint64_t n;                 // records
+    uint64_t S;                 // samples declared by the header line
+    uint8_t *out;               // decoded lines, concatenated
+    uint64_t out_cap;
+    uint64_t *line_off;         // n + 1 exclusive offsets of the lines in `out`
+    // workspace (vcfc_decode_workspace_layout)
+    uint32_t *st;               // per-record plan status
+    uint32_t *line_size;        // per-record line bytes
+    uint64_t *end;              // byte-serial parse end (queued records)
+    uint32_t *seq_list;         // records queued for the byte-serial path
+    uint32_t *seq_count;
+    uint64_t *err;              // min over records of (i << 8 | code): 2 = parse ends off the hop, 3 = reference error
+    uint64_t *partials;         // scan partials
+};
+
+struct VcfcDecodeLayout {
+    uint64_t st, line_size, end, seq_list, seq_count, err, partials, total;
+};
+
+VcfcDecodeLayout vcfc_decode_workspace_layout(uint64_t n);
+// plan: statuses, sizes, line offsets (no host synchronisation)
+hipError_t vcfc_decode_plan(const VcfcDecodeArgs &a, hipStream_t s);
+// write lines [first, last) at a.out + line_off[i] (their plan status must not be an error)
+hipError_t vcfc_decode_write(const VcfcDecodeArgs &a, uint64_t first, uint64_t last, hipStream_t s);
+// one-lane byte-serial decode of in[p, n): out == nullptr counts; st[0..2] =
+// {0 clean end | 2 reference error, bytes, lines}
+hipError_t vcfc_decode_stream(const uint8_t *in, uint64_t n, uint64_t p, uint64_t S, uint8_t *out, uint64_t *st,
+                              hipStream_t s);
+// exclusive u32 -> u64 scan with out[n] = total (shared with the encoder)
+hipError_t vcfc_scan_u32(const uint32_t *in, uint64_t n, uint64_t *partials, uint64_t *out, hipStream_t s);

@@ -969,3 +969,8 @@ hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t s, hipEvent_t
     if (ev) (void)hipEventRecord(ev[4], s);
     return hipSuccess;
 }
+
+hipError_t vcfc_scan_u32(const uint32_t *in, uint64_t n, uint64_t *partials, uint64_t *out, hipStream_t s) {
+    if (n == 0) return hipMemsetAsync(out, 0, 8, s);
+    return launch_scan<0>(in, n, partials, out, s);
+}

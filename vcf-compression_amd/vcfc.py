@@ -3,6 +3,7 @@
 Mirrors the reference's operator interface for the encode path:
   compress_data_line(line, add_newline=True)   (reference src/compress.hpp:20-23)
   compress_file(in_path, out_path)             (reference src/compress.cpp:205-257)
+  decompress / decompress_file                 (reference src/compress.cpp:1214-1257)
 Errors raise VcfValidationError / RuntimeError like the reference's exceptions
 (src/utils.hpp:117-123, src/compress.cpp:9-11,231-234).
 
@@ -29,6 +30,7 @@ EXPORTS = [
     "vcfc_compress_bound", "vcfc_compress_buffer", "vcfc_synth_rows_device",
     "vcfc_timer_create", "vcfc_timer_destroy", "vcfc_encode_rows_device_timed", "vcfc_timer_read",
     "vcfc_sparse_offset", "vcfc_sparsify_file", "vcfc_sparse_plan_device",
+    "vcfc_decompress_buffer", "vcfc_decompress_file",
 ]
 
 
@@ -77,6 +79,8 @@ def lib():
     L.vcfc_sparse_offset.argtypes = [u64]
     L.vcfc_sparsify_file.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p]
     L.vcfc_sparse_plan_device.argtypes = [vp, vp, u64, u64, vp, vp, vp, vp]
+    L.vcfc_decompress_buffer.argtypes = [vp, vp, u64, vp, u64, ctypes.POINTER(u64)]
+    L.vcfc_decompress_file.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p]
     L.vcfc_synth_rows_device.argtypes = [vp, vp, u64, vp, vp, vp, u32, ctypes.c_int, u64, vp]
     _lib = L
     return L
@@ -149,6 +153,32 @@ class Context:
         line = ctypes.c_int64(-1)
         st = lib().vcfc_compress_file(self._h, in_path.encode(), out_path.encode(), ctypes.byref(line))
         raise_for(st, "line %d" % line.value)
+
+    def decompress_buffer(self, data, cap=None):
+        """.vcfc bytes -> VCF bytes, as decompress2_fd (reference
+        src/compress.cpp:1214-1257).  Returns (status, bytes): on
+        VCFC_E_FORMAT the bytes are what the reference writes before it
+        throws."""
+        src = np.frombuffer(data, dtype=np.uint8)
+        cap = cap if cap is not None else 16 * len(data) + 4096
+        while True:
+            out = np.empty(max(cap, 1), dtype=np.uint8)
+            n = ctypes.c_uint64(0)
+            st = lib().vcfc_decompress_buffer(self._h, src.ctypes.data, len(data), out.ctypes.data, cap,
+                                              ctypes.byref(n))
+            if st == E_NOSPACE and n.value > cap:
+                cap = n.value
+                continue
+            return st, out[:n.value].tobytes()
+
+    def decompress(self, data):
+        """Like decompress_buffer, raising where the reference throws."""
+        st, out = self.decompress_buffer(data)
+        raise_for(st)
+        return out
+
+    def decompress_file(self, in_path, out_path):
+        raise_for(lib().vcfc_decompress_file(self._h, in_path.encode(), out_path.encode()))
 
     def sparsify_file(self, in_path, out_path):
         """sparsify_file (reference src/sparse.cpp:290-580)."""
