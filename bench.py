@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--cpu-rows", type=int, default=120_000, help="rows in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify-rows", type=int, default=64, help="rows checked against the CPU path")
+    ap.add_argument("--mode", choices=["encode", "decode"], default="encode",
+                    help="encode = the headline (BASELINE metric); decode = row f1 (config 5 building block)")
     return ap.parse_args()
 
 
@@ -99,8 +101,77 @@ def load_pmc(workload_key):
     return None
 
 
+def bench_decode(args, torch, vcfc, workload):
+    """Row f1: decode the same synthetic batch (device-resident records made
+    by the GPU encoder) back to VCF lines; every output byte is checked
+    against the original rows on the GPU.  One GPU (replicas only)."""
+    import numpy as np
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    n, S = args.rows, args.samples
+    rows = workload.DeviceRows(torch, vcfc, n, S, args.law, seed=1000, device=dev)
+    ws_bytes = vcfc.workspace_size(n, rows.line_bytes)
+    cap = vcfc.encode_bound(n, rows.line_bytes)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    recs = torch.empty(cap, dtype=torch.uint8, device=dev)
+    rec = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    err = torch.empty(1, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    vcfc.encode_rows_device(rows.buf.data_ptr(), rows.line_off.data_ptr(), rows.line_len.data_ptr(), n,
+                            rows.line_bytes, recs.data_ptr(), cap, rec.data_ptr(), ws.data_ptr(), ws_bytes,
+                            err.data_ptr(), stream)
+    torch.cuda.synchronize(dev)
+    rec_bytes = int(rec[n].item())
+    del ws
+    dws_bytes = vcfc.decode_workspace_size(n)
+    dws = torch.empty(dws_bytes, dtype=torch.uint8, device=dev)
+    out_cap = rows.total_bytes + 64
+    out = torch.empty(out_cap, dtype=torch.uint8, device=dev)
+    loff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+
+    def step():
+        vcfc.decode_records_device(recs.data_ptr(), rec_bytes, rec.data_ptr(), n, S, out.data_ptr(), out_cap,
+                                   loff.data_ptr(), dws.data_ptr(), dws_bytes, err.data_ptr(), stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record()
+    for _ in range(args.steps):
+        step()
+    e1.record()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    ev_ms = e0.elapsed_time(e1) / args.steps
+    e = int(err.cpu().numpy().view(np.uint64)[0])
+    total = int(loff[n].item())
+    identical = e == vcfc.NO_ERROR and total == rows.total_bytes and bool(torch.equal(out[:total], rows.buf[:total]))
+    alg = rec_bytes + total
+    res = {"metric": "decoded GT bytes/sec, 2504-sample x 1M-variant .vcfc (row f1)",
+           "value": round(rows.gt_bytes * args.steps / elapsed / 1e9, 2), "unit": "GB/s", "n_gpus": 1,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+           "higher_is_better": True, "scaling": "replicas", "vs_baseline": None, "dtype": "u8",
+           "data": "synthetic (generated and encoded in HBM)",
+           "config": {"workload": "%s %d samples x %d variants" % ("chr22-shaped" if args.law == 1 else
+                                                                   "random_vcf-law", S, n),
+                      "record_bytes": rec_bytes, "line_bytes": total},
+           "roofline": {"kernel": "k_dec_plan + k_dec_write", "bound": "hbm",
+                        "achieved": round(alg / (ev_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(alg / (ev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                        "algorithmic_bytes_per_launch": alg, "avg_launch_ms": round(ev_ms, 4)},
+           "output_identical_to_input_rows": identical}
+    print(json.dumps(res), flush=True)
+
+
 def main():
     args = parse()
+    if args.mode == "decode":
+        import torch
+        import vcfc
+        import workload
+        return bench_decode(args, torch, vcfc, workload)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -130,6 +130,20 @@ int vcfc_decompress_buffer(vcfc_ctx *ctx, const uint8_t *in, uint64_t in_bytes, 
                            uint64_t *out_len);
 int vcfc_decompress_file(vcfc_ctx *ctx, const char *in_vcfc, const char *out_vcf);
 
+/* Device-resident batch: records d_in[d_rec_start[i], d_rec_start[i+1]) for
+ * i < n (e.g. an encoder batch's rec_off), `samples` from the header line.
+ * Enqueued on `stream` with no host synchronisation.  Lines land at
+ * d_out + d_line_off[i] (n + 1 offsets, d_line_off[n] = total).  d_err:
+ * ~0, or min over records of (i << 8 | 2) where a record's byte-serial parse
+ * ends off its LEN (the file decoder then continues byte-serially) or
+ * (i << 8 | 3) where the reference throws; such records get no line, and
+ * lines past the first one are not meaningful.  (i << 8 | 0xFF): out_cap
+ * too small. */
+uint64_t vcfc_decode_workspace_size(uint64_t n_records);
+int vcfc_decode_records_device(const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_rec_start, uint64_t n,
+                               uint64_t samples, uint8_t *d_out, uint64_t out_cap, uint64_t *d_line_off,
+                               void *d_ws, uint64_t ws_bytes, uint64_t *d_err, void *stream);
+
 /* ---- sparse layout: sparsify_file (reference src/sparse.cpp:290-580) -------
  * Record i of the .vcfc goes to data_start + (300e6 + POS_i) * 16384
  * (compute_sparse_offset, src/sparse.cpp:18-51) behind a 16-byte prefix

@@ -635,4 +635,28 @@ int vcfc_decompress_file(vcfc_ctx *c, const char *in_path, const char *out_path)
     return st;
 }
 
+uint64_t vcfc_decode_workspace_size(uint64_t n_records) { return vcfc_decode_workspace_layout(n_records).total; }
+
+int vcfc_decode_records_device(const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_rec_start, uint64_t n,
+                               uint64_t samples, uint8_t *d_out, uint64_t out_cap, uint64_t *d_line_off, void *d_ws,
+                               uint64_t ws_bytes, uint64_t *d_err, void *stream) {
+    if ((n && (!d_in || !d_rec_start || !d_out || !d_ws)) || !d_line_off || !d_err) return VCFC_E_ARG;
+    const VcfcDecodeLayout L = vcfc_decode_workspace_layout(n);
+    if (ws_bytes < L.total) return VCFC_E_NOSPACE;
+    uint8_t *ws = static_cast<uint8_t *>(d_ws);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    VcfcDecodeArgs a;
+    a.in = d_in; a.n_bytes = in_bytes; a.rec_start = d_rec_start; a.n = n; a.S = samples;
+    a.out = d_out; a.out_cap = out_cap; a.line_off = d_line_off;
+    a.st = reinterpret_cast<uint32_t *>(ws + L.st);
+    a.line_size = reinterpret_cast<uint32_t *>(ws + L.line_size);
+    a.end = reinterpret_cast<uint64_t *>(ws + L.end);
+    a.seq_list = reinterpret_cast<uint32_t *>(ws + L.seq_list);
+    a.seq_count = reinterpret_cast<uint32_t *>(ws + L.seq_count);
+    a.err = d_err;
+    a.partials = reinterpret_cast<uint64_t *>(ws + L.partials);
+    if (vcfc_decode_plan(a, s) != hipSuccess) return VCFC_E_HIP;
+    return vcfc_decode_write(a, 0, n, s) == hipSuccess ? VCFC_OK : VCFC_E_HIP;
+}
+
 }  // extern "C"

@@ -246,6 +246,7 @@ __global__ __launch_bounds__(256) void k_dec_write(VcfcDecodeArgs a, uint64_t fi
         return;
     }
     uint8_t *line = a.out + L0;
+    if (a.st[i] == DS_ERR) return;   // no line (size 0); the reference throws here
     if (a.st[i] != DS_SIMPLE) {
         if (l == 0) {
             uint64_t size, end;

@@ -30,7 +30,8 @@ EXPORTS = [
     "vcfc_compress_bound", "vcfc_compress_buffer", "vcfc_synth_rows_device",
     "vcfc_timer_create", "vcfc_timer_destroy", "vcfc_encode_rows_device_timed", "vcfc_timer_read",
     "vcfc_sparse_offset", "vcfc_sparsify_file", "vcfc_sparse_plan_device",
-    "vcfc_decompress_buffer", "vcfc_decompress_file",
+    "vcfc_decompress_buffer", "vcfc_decompress_file", "vcfc_decode_workspace_size",
+    "vcfc_decode_records_device",
 ]
 
 
@@ -81,6 +82,9 @@ def lib():
     L.vcfc_sparse_plan_device.argtypes = [vp, vp, u64, u64, vp, vp, vp, vp]
     L.vcfc_decompress_buffer.argtypes = [vp, vp, u64, vp, u64, ctypes.POINTER(u64)]
     L.vcfc_decompress_file.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p]
+    L.vcfc_decode_workspace_size.restype = u64
+    L.vcfc_decode_workspace_size.argtypes = [u64]
+    L.vcfc_decode_records_device.argtypes = [vp, u64, vp, u64, u64, vp, u64, vp, vp, u64, vp, vp]
     L.vcfc_synth_rows_device.argtypes = [vp, vp, u64, vp, vp, vp, u32, ctypes.c_int, u64, vp]
     _lib = L
     return L
@@ -240,6 +244,16 @@ class StageTimer:
             lib().vcfc_timer_destroy(self._h)
         except Exception:
             pass
+
+
+def decode_workspace_size(n_records):
+    return int(lib().vcfc_decode_workspace_size(n_records))
+
+
+def decode_records_device(d_in, in_bytes, d_rec_start, n, samples, d_out, out_cap, d_line_off, d_ws, ws_bytes,
+                          d_err, stream=0):
+    raise_for(lib().vcfc_decode_records_device(d_in, in_bytes, d_rec_start, n, samples, d_out, out_cap, d_line_off,
+                                               d_ws, ws_bytes, d_err, stream))
 
 
 def synth_rows_device(d_buf, d_line_off, n, d_prefix, d_prefix_off, d_row_af, samples, law, seed, stream=0):
