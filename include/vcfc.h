@@ -138,11 +138,14 @@ int vcfc_decompress_file(vcfc_ctx *ctx, const char *in_vcfc, const char *out_vcf
  * ends off its LEN (the file decoder then continues byte-serially) or
  * (i << 8 | 3) where the reference throws; such records get no line, and
  * lines past the first one are not meaningful.  (i << 8 | 0xFF): out_cap
- * too small. */
+ * too small.  exact = 0 plans from the headers and REQ bytes only and
+ * assumes every sample section is "simple" (3-byte tokens, exactly
+ * `samples` of them); the writer checks that and reports (i << 8 | 4) where
+ * it was wrong: call again with exact = 1. */
 uint64_t vcfc_decode_workspace_size(uint64_t n_records);
 int vcfc_decode_records_device(const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_rec_start, uint64_t n,
                                uint64_t samples, uint8_t *d_out, uint64_t out_cap, uint64_t *d_line_off,
-                               void *d_ws, uint64_t ws_bytes, uint64_t *d_err, void *stream);
+                               void *d_ws, uint64_t ws_bytes, uint64_t *d_err, int exact, void *stream);
 
 /* ---- sparse layout: sparsify_file (reference src/sparse.cpp:290-580) -------
  * Record i of the .vcfc goes to data_start + (300e6 + POS_i) * 16384

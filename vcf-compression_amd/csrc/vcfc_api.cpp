@@ -639,7 +639,7 @@ uint64_t vcfc_decode_workspace_size(uint64_t n_records) { return vcfc_decode_wor
 
 int vcfc_decode_records_device(const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_rec_start, uint64_t n,
                                uint64_t samples, uint8_t *d_out, uint64_t out_cap, uint64_t *d_line_off, void *d_ws,
-                               uint64_t ws_bytes, uint64_t *d_err, void *stream) {
+                               uint64_t ws_bytes, uint64_t *d_err, int exact, void *stream) {
     if ((n && (!d_in || !d_rec_start || !d_out || !d_ws)) || !d_line_off || !d_err) return VCFC_E_ARG;
     const VcfcDecodeLayout L = vcfc_decode_workspace_layout(n);
     if (ws_bytes < L.total) return VCFC_E_NOSPACE;
@@ -655,7 +655,7 @@ int vcfc_decode_records_device(const uint8_t *d_in, uint64_t in_bytes, const uin
     a.seq_count = reinterpret_cast<uint32_t *>(ws + L.seq_count);
     a.err = d_err;
     a.partials = reinterpret_cast<uint64_t *>(ws + L.partials);
-    if (vcfc_decode_plan(a, s) != hipSuccess) return VCFC_E_HIP;
+    if (vcfc_decode_plan(a, exact != 0, s) != hipSuccess) return VCFC_E_HIP;
     return vcfc_decode_write(a, 0, n, s) == hipSuccess ? VCFC_OK : VCFC_E_HIP;
 }
 

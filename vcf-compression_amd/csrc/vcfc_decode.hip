@@ -14,9 +14,10 @@
 //   k_dec_seq    one lane per queued record: byte-serial parse (size, end,
 //                reference error).
 //   scan         line offsets (the encoder's exclusive scan).
-//   k_dec_write  one wave per record: simple records by an item-driven fill
-//                (each run byte writes its tokens as repeated 4-byte words);
-//                queued records by the byte-serial writer on lane 0.
+//   k_dec_write  one wave per record: simple records fill LDS tiles of
+//                4-byte token words item by item, then stream each tile out
+//                with contiguous 16-byte stores; queued records by the
+//                byte-serial writer on lane 0.
 //   k_dec_stream one lane: byte-serial decode of a byte range.
 //
 // A record is simple when: header bits and REQ are sane; REQ holds exactly 9
@@ -34,6 +35,9 @@
 namespace {
 
 constexpr int DEC_WAVES = 4;   // records per 256-thread block
+constexpr uint32_t SB = 2048;              // sample bytes staged per piece (k_dec_write)
+constexpr uint32_t SBUF = SB + 48;         // + look-ahead, 16-B alignment slack, last block's overhang
+constexpr uint32_t TB = 512;               // token words per LDS tile (k_dec_write): 8 per lane
 
 // per-record status after planning
 constexpr uint32_t DS_SIMPLE = 0;   // line = REQ' + 4S bytes, item fill
@@ -43,6 +47,9 @@ constexpr uint32_t DS_ERR = 3;      // the reference throws at this record
 
 // result of dec_line_seq
 constexpr int DL_OK = 0, DL_END = 1, DL_ERR = 2;
+
+__device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
+__device__ __forceinline__ uint32_t umin32(uint32_t a, uint32_t b) { return a < b ? a : b; }
 
 __device__ __forceinline__ uint32_t be30(const uint8_t *h) {
     return ((uint32_t)(h[0] & 0x3Fu) << 24) | ((uint32_t)h[1] << 16) | ((uint32_t)h[2] << 8) | h[3];
@@ -125,57 +132,97 @@ __device__ int dec_line_seq(const uint8_t *in, uint64_t n, uint64_t p, uint64_t 
     return DL_OK;
 }
 
-// Wave-parallel scan of a record's sample items (see the header comment).
-// Visits each item start with (lane-local) byte b, position k, tokens before
-// it (gb) and its count; returns false if the record is not simple.
-struct ItemScan {
-    const uint8_t *in;
-    uint64_t s0, s1;   // sample section [s0, s1); in[s1] is the record's LF
+// Record-relative positions below are 32-bit: a record is staged from the
+// 16-byte block holding its first byte (rbase), and no record reaches 4 GiB.
+
+// Wave-parallel scan of a record's sample items (see the header comment),
+// one window of 64 bytes of the sample section [s0, s1) per call (byte s1
+// is the record's LF).  Lane l looks at byte b0 + l (`v`, already read by
+// the caller; valid if < b).  State carries across windows.
+struct ItemState {
+    uint32_t got = 0;
+    uint64_t pcarry = 0, tcarry = 0;
+    bool bad = false;
+};
+struct ItemLane {
+    bool start;      // this lane's byte starts an item
+    uint32_t cnt;    // its tokens
+    uint32_t gb;     // tokens before it
 };
 
-template <class F>
-__device__ __forceinline__ bool scan_items(const ItemScan &sc, uint64_t S, uint64_t *got_out, F &&visit) {
+__device__ __forceinline__ ItemLane scan_window(uint32_t v, uint32_t b0, uint32_t b, uint32_t s1, ItemState &st) {
     const uint32_t l = vw::lane_id();
-    uint64_t got = 0, pcarry = 0, tcarry = 0;
-    bool bad = false;
-    for (uint64_t b0 = sc.s0; b0 < sc.s1; b0 += 64) {
-        const uint64_t k = b0 + l;
-        const bool valid = k < sc.s1;
-        const uint32_t b = valid ? sc.in[k] : 0u;
-        const uint64_t E = vw::ballot(valid && b == 0xE1u);
-        // payload: the 3 bytes after an escape flag; terminator: the 4th
-        const uint64_t P = (E << 1) | (E << 2) | (E << 3) | pcarry;
-        const uint64_t TM = (E << 4) | tcarry;
-        const uint64_t e = E >> 60;
-        pcarry = (e >> 1) | (e >> 2) | (e >> 3);
-        tcarry = e;
-        const bool is_p = (P >> l) & 1ull, is_t = (TM >> l) & 1ull;
-        bool lb = false;
-        if (valid) {
-            if (is_p) lb = b >= 0x80u || b == '\t' || b == '\n';
-            else if (is_t) lb = b != '\t';
-            else lb = (b & 0xE0u) == 0xE0u && (b != 0xE1u || k + 4 > sc.s1);   // escape needs 3 bytes + TAB/final LF
-        }
-        const bool start = valid && !is_p && !is_t;
-        const uint32_t cnt = !start ? 0u : b == 0xE1u ? 1u : b < 0x80u ? b : (b & 0x1Fu);
-        lb = lb || (start && cnt == 0);
-        bad = bad || vw::ballot(lb) != 0;
-        const uint32_t inc = vw::scan_add(cnt);
-        const uint64_t gb = got + (inc - cnt);
-        if (!bad && start) visit(b, k, gb, cnt);
-        got += vw::readlane(inc, 63);
+    const uint32_t k = b0 + l;
+    const bool valid = k < b;
+    const uint64_t E = vw::ballot(valid && v == 0xE1u);
+    // payload: the 3 bytes after an escape flag; terminator: the 4th
+    const uint64_t P = (E << 1) | (E << 2) | (E << 3) | st.pcarry;
+    const uint64_t TM = (E << 4) | st.tcarry;
+    const uint64_t e = E >> 60;
+    st.pcarry = (e >> 1) | (e >> 2) | (e >> 3);
+    st.tcarry = e;
+    const bool is_p = (P >> l) & 1ull, is_t = (TM >> l) & 1ull;
+    bool lb = false;
+    if (valid) {
+        if (is_p) lb = v >= 0x80u || v == '\t' || v == '\n';
+        else if (is_t) lb = v != '\t';
+        else lb = (v & 0xE0u) == 0xE0u && (v != 0xE1u || k + 4 > s1);   // escape needs 3 bytes + TAB/final LF
     }
-    *got_out = got;
-    return !bad && got == S;
+    ItemLane r;
+    r.start = valid && !is_p && !is_t;
+    r.cnt = !r.start ? 0u : v == 0xE1u ? 1u : v < 0x80u ? v : (v & 0x1Fu);
+    lb = lb || (r.start && r.cnt == 0);
+    st.bad = st.bad || vw::ballot(lb) != 0;
+    const uint32_t inc = vw::scan_add(r.cnt);
+    r.gb = st.got + (inc - r.cnt);
+    st.got += vw::readlane(inc, 63);
+    return r;
 }
 
-// REQ bytes: TAB count and the C-string length (first NUL).
-__device__ __forceinline__ void scan_req(const uint8_t *r, uint32_t req, uint32_t *tabs, uint32_t *slen) {
+// A record staged through LDS in pieces of up to SB bytes (plus 8 bytes of
+// look-ahead), loaded with 16-byte buffer loads: one load latency per piece
+// instead of one per 64-byte window, and no global load between the
+// writer's stores (vmcnt counts loads and stores together).  One buffer
+// resource per record keeps offsets 32-bit for any input size; its range
+// is rounded up to whole dwords (a dword only partly in range reads as 0; at
+// most 3 bytes past the record are read, inside the input or its slack).
+// Positions are relative to rbase = the record start rounded down to 16.
+struct Staged {
+    uint8_t *lds;
+    vw::brsrc rsr;
+    uint32_t re, cbase, cend;
+    __device__ void init(uint8_t *l, const uint8_t *rec16, uint32_t rend) {
+        lds = l;
+        re = rend;
+        rsr = vw::make_rsrc(rec16, (re + 3u) & ~3u);
+        cbase = cend = 0;
+    }
+    // make [p, min(p + SB, re)) resident (wave-uniform p)
+    __device__ void load(uint32_t p) {
+        const uint32_t l = vw::lane_id();
+        vw::wave_sync();   // everyone is done with the previous piece
+        cbase = p & ~15u;
+        cend = umin32(p + SB, re);
+        const uint32_t lim = umin32(cend + 8, re);
+        for (uint32_t o = 16u * l; cbase + o < lim; o += 1024)
+            *reinterpret_cast<uint4 *>(lds + o) = vw::bload16(rsr, cbase + o);
+        vw::wave_sync();
+    }
+    // window [k0, k0 + 64) (clipped to re) resident
+    __device__ __forceinline__ void need(uint32_t k0) {
+        if (k0 < cbase || umin32(k0 + 64, re) > cend) load(k0);
+    }
+    __device__ __forceinline__ uint32_t at(uint32_t k) const { return lds[k - cbase]; }
+};
+
+// REQ bytes [r0, r0 + req): TAB count and the C-string length (first NUL).
+__device__ __forceinline__ void scan_req(Staged &sg, uint32_t r0, uint32_t req, uint32_t *tabs, uint32_t *slen) {
     const uint32_t l = vw::lane_id();
     uint32_t t = 0, z = req;
     for (uint32_t b0 = 0; b0 < req; b0 += 64) {
+        sg.need(r0 + b0);
         const uint32_t k = b0 + l;
-        const uint32_t b = k < req ? r[k] : 0xFFu;
+        const uint32_t b = k < req ? sg.at(r0 + k) : 0xFFu;
         t += (uint32_t)vw::popc64(vw::ballot(b == '\t'));
         const uint64_t zm = vw::ballot(b == 0);
         if (zm && z == req) z = b0 + (uint32_t)__builtin_ctzll(zm);
@@ -184,29 +231,48 @@ __device__ __forceinline__ void scan_req(const uint8_t *r, uint32_t req, uint32_
     *slen = z;
 }
 
+// FULL = 0 ("light"): the sample section is not scanned; a record whose
+// header, REQ and final LF look right is assumed simple, and k_dec_write
+// verifies the assumption while it writes (code 4 in err: rerun exactly).
+template <bool FULL>
 __global__ __launch_bounds__(256) void k_dec_plan(VcfcDecodeArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t sbuf[DEC_WAVES * SBUF];
     const uint32_t wave = vw::readfirst(threadIdx.x >> 6);
     const uint64_t i = (uint64_t)blockIdx.x * DEC_WAVES + wave;
     if (i >= a.n) return;
-    const uint64_t rs = a.rec_start[i], re = a.rec_start[i + 1];
+    const uint32_t l = vw::lane_id();
+    const uint64_t rs_abs = a.rec_start[i], re_abs = a.rec_start[i + 1];
     bool simple = false;
     uint64_t size = 0;
-    if (re - rs >= 10 && a.S > 0) {
-        const uint8_t *h = a.in + rs;
-        const uint32_t req = be30(h + 4);
-        if ((h[0] >> 6) == 3u && (h[4] >> 6) == 3u && req > 0 && 9 + (uint64_t)req < re - rs &&
-            a.in[re - 1] == '\n') {
+    if (re_abs - rs_abs >= 10 && re_abs - rs_abs < (1ull << 31) && a.S > 0 && a.S < (1ull << 31)) {
+        const uint64_t rbase = rs_abs & ~15ull;
+        const uint32_t rs = (uint32_t)(rs_abs - rbase), re = (uint32_t)(re_abs - rbase);
+        Staged sg;
+        sg.init(sbuf + wave * SBUF, a.in + rbase, re);
+        sg.load(rs);
+        const uint32_t h0 = sg.at(rs), h4 = sg.at(rs + 4);
+        const uint32_t req = ((h4 & 0x3Fu) << 24) | (sg.at(rs + 5) << 16) | (sg.at(rs + 6) << 8) | sg.at(rs + 7);
+        if ((h0 >> 6) == 3u && (h4 >> 6) == 3u && req > 0 && 9 + (uint64_t)req < re - rs) {
             uint32_t tabs, slen;
-            scan_req(h + 8, req, &tabs, &slen);
-            if (tabs == 9) {
-                uint64_t got;
-                ItemScan sc{a.in, rs + 8 + req, re - 1};
-                simple = scan_items(sc, a.S, &got, [](uint32_t, uint64_t, uint64_t, uint32_t) {});
+            scan_req(sg, rs + 8, req, &tabs, &slen);
+            sg.need(re - 1);
+            if (tabs == 9 && sg.at(re - 1) == '\n') {
+                simple = true;
+                if (FULL) {
+                    ItemState st;
+                    const uint32_t s0 = rs + 8 + req, s1 = re - 1;
+                    for (uint32_t cur = s0; cur < s1 && !st.bad; cur += 64) {
+                        sg.need(cur);
+                        const uint32_t b = umin32(cur + 64, s1);
+                        (void)scan_window(sg.at(umin32(cur + l, b - 1)), cur, b, s1, st);
+                    }
+                    simple = !st.bad && st.got == a.S;
+                }
                 size = slen + 4 * a.S;
             }
         }
     }
-    if (vw::lane_id() == 0) {
+    if (l == 0) {
         a.st[i] = simple ? DS_SIMPLE : DS_SEQ;
         a.line_size[i] = simple ? (uint32_t)size : 0u;
         if (!simple) {
@@ -235,11 +301,13 @@ __global__ __launch_bounds__(256) void k_dec_seq(VcfcDecodeArgs a) {
 }
 
 __global__ __launch_bounds__(256) void k_dec_write(VcfcDecodeArgs a, uint64_t first, uint64_t last) {
+    __shared__ __attribute__((aligned(16))) uint8_t sbuf[DEC_WAVES * SBUF];
+    __shared__ __attribute__((aligned(16))) uint32_t tbuf[DEC_WAVES * TB];
     const uint32_t wave = vw::readfirst(threadIdx.x >> 6);
     const uint64_t i = first + (uint64_t)blockIdx.x * DEC_WAVES + wave;
     if (i >= last) return;
     const uint32_t l = vw::lane_id();
-    const uint64_t rs = a.rec_start[i];
+    const uint64_t rs_abs = a.rec_start[i];
     const uint64_t L0 = a.line_off[i];
     if (a.line_off[i + 1] > a.out_cap) {
         if (l == 0) atomicMin((unsigned long long *)a.err, (unsigned long long)((i << 8) | 0xFFu));
@@ -250,38 +318,101 @@ __global__ __launch_bounds__(256) void k_dec_write(VcfcDecodeArgs a, uint64_t fi
     if (a.st[i] != DS_SIMPLE) {
         if (l == 0) {
             uint64_t size, end;
-            (void)dec_line_seq(a.in, a.n_bytes, rs, a.S, line, &size, &end);
+            (void)dec_line_seq(a.in, a.n_bytes, rs_abs, a.S, line, &size, &end);
         }
         return;
     }
-    const uint8_t *h = a.in + rs;
-    const uint32_t req = be30(h + 4);
-    const uint64_t re = a.rec_start[i + 1];
-    const uint32_t slen = (uint32_t)(a.line_off[i + 1] - L0 - 4 * a.S);   // REQ' = line - 4S
-    for (uint32_t k = l; k < slen; k += 64) line[k] = h[8 + k];
+    const uint64_t rbase = rs_abs & ~15ull;
+    const uint32_t rs = (uint32_t)(rs_abs - rbase), re = (uint32_t)(a.rec_start[i + 1] - rbase);
+    const uint32_t S = (uint32_t)a.S;
+    Staged sg;
+    sg.init(sbuf + wave * SBUF, a.in + rbase, re);
+    sg.load(rs);
+    const uint32_t req = ((sg.at(rs + 4) & 0x3Fu) << 24) | (sg.at(rs + 5) << 16) | (sg.at(rs + 6) << 8) | sg.at(rs + 7);
+    const uint32_t slen = (uint32_t)(a.line_off[i + 1] - L0 - 4ull * S);   // REQ' = line - 4S
+    for (uint32_t b0 = 0; b0 < slen; b0 += 64) {
+        sg.need(rs + 8 + b0);
+        if (b0 + l < slen) line[b0 + l] = (uint8_t)sg.at(rs + 8 + b0 + l);
+    }
     uint8_t *tok = line + slen;
-    const uint64_t S = a.S;
-    uint64_t got;
-    ItemScan sc{a.in, rs + 8 + req, re - 1};
-    scan_items(sc, S, &got, [&](uint32_t b, uint64_t k, uint64_t gb, uint32_t cnt) {
-        // the item's token as a little-endian word "a|b\t"
-        uint32_t w;
-        if (b == 0xE1u) {
-            w = (uint32_t)a.in[k + 1] | ((uint32_t)a.in[k + 2] << 8) | ((uint32_t)a.in[k + 3] << 16);
-        } else if (b < 0x80u) {
-            w = 0x307C30u;
-        } else {
-            const uint32_t m = b & 0xE0u;
-            w = (m == 0xA0u ? 0x30u : 0x31u) | 0x7C00u | ((m == 0xC0u ? 0x30u : 0x31u) << 16);
+    // Token tiles of TB four-byte words "a|b\t".  Each item writes only its
+    // word at its first token's slot in the LDS tile (W); a tile then fills
+    // every slot from the last item start at or before it ("last non-zero":
+    // in-lane, then across lanes by a max-scan of lane indices and one
+    // ds_bpermute) and goes out as contiguous 16-byte stores.  Work per tile
+    // does not depend on run lengths.
+    uint32_t *W = tbuf + wave * TB;
+    constexpr uint32_t PL = TB / 64;   // slots per lane
+    for (uint32_t q = 0; q < PL; q += 4) *reinterpret_cast<uint4 *>(W + PL * l + q) = make_uint4(0, 0, 0, 0);
+    uint32_t j0 = 0, carry = 0;   // tile start; word of the item holding token j0
+    auto tile_out = [&](uint32_t n_tok) {
+        vw::wave_sync();
+        uint32_t w[PL];
+#pragma unroll
+        for (uint32_t q = 0; q < PL; q += 4) {
+            const uint4 v = *reinterpret_cast<const uint4 *>(W + PL * l + q);
+            w[q] = v.x; w[q + 1] = v.y; w[q + 2] = v.z; w[q + 3] = v.w;
+            *reinterpret_cast<uint4 *>(W + PL * l + q) = make_uint4(0, 0, 0, 0);
         }
-        w |= 0x09000000u;
-        uint8_t *p = tok + 4 * gb;
-        uint32_t j = 0;
-        for (; j + 4 <= cnt; j += 4) vw::gstore16(p, 4ull * j, make_uint4(w, w, w, w));
-        if (cnt & 2u) { *reinterpret_cast<uint2 *>(p + 4ull * j) = make_uint2(w, w); j += 2; }
-        if (cnt & 1u) *reinterpret_cast<uint32_t *>(p + 4ull * j) = w;
-        if (gb + cnt == S) tok[4 * S - 1] = '\n';   // same lane, after its words
-    });
+        uint32_t lastw = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < PL; q++) {
+            lastw = w[q] ? w[q] : lastw;
+            w[q] = lastw;
+        }
+        // word entering the lane: the last start in an earlier lane, else carry
+        const uint32_t src = vw::shr1z(vw::scan_max(lastw ? l + 1 : 0u));
+        const uint32_t inw = vw::shfl(lastw, src ? src - 1 : 0u);
+        const uint32_t enter = src ? inw : carry;
+#pragma unroll
+        for (uint32_t q = 0; q < PL; q++) w[q] = w[q] ? w[q] : enter;
+        const uint32_t t0 = j0 + PL * l;
+#pragma unroll
+        for (uint32_t q = 0; q < PL; q++)
+            if (t0 + q + 1 == S) w[q] = (w[q] & 0x00FFFFFFu) | 0x0A000000u;   // the line's LF
+        if (t0 + PL <= j0 + n_tok) {
+#pragma unroll
+            for (uint32_t q = 0; q < PL; q += 4)
+                vw::gstore16(tok, 4ull * (t0 + q), make_uint4(w[q], w[q + 1], w[q + 2], w[q + 3]));
+        } else {
+            for (uint32_t q = 0; q < PL; q++)
+                if (t0 + q < j0 + n_tok) *reinterpret_cast<uint32_t *>(tok + 4ull * (t0 + q)) = w[q];
+        }
+        carry = vw::readlane(w[PL - 1], 63);
+        vw::wave_sync();
+    };
+    const uint32_t s0 = rs + 8 + req, s1 = re - 1;
+    ItemState st;
+    for (uint32_t cur = s0; cur < s1; cur += 64) {
+        sg.need(cur);
+        const uint32_t b = umin32(cur + 64, s1);
+        const uint32_t v = sg.at(umin32(cur + l, b - 1));
+        const ItemLane it = scan_window(v, cur, b, s1, st);
+        uint32_t w = 0;
+        if (it.start) {
+            if (v == 0xE1u) {
+                const uint32_t q = cur + l + 1;   // payload: inside the piece or its look-ahead
+                w = sg.at(q) | (sg.at(q + 1) << 8) | (sg.at(q + 2) << 16);
+            } else if (v < 0x80u) {
+                w = 0x307C30u;
+            } else {
+                const uint32_t m = v & 0xE0u;
+                w = (m == 0xA0u ? 0x30u : 0x31u) | 0x7C00u | ((m == 0xC0u ? 0x30u : 0x31u) << 16);
+            }
+            w |= 0x09000000u;
+        }
+        for (;;) {
+            if (it.start && it.gb >= j0 && it.gb < j0 + TB) W[it.gb - j0] = w;
+            if (st.got < j0 + TB || j0 + TB > S) break;   // the tile is not complete yet
+            tile_out(TB);
+            j0 += TB;
+        }
+    }
+    if (j0 < S) tile_out(S - j0);
+    // a light plan assumed this record simple: check it (tokens past S were
+    // never stored; the line's bytes are rewritten by the exact rerun)
+    if ((st.bad || st.got != S) && l == 0)
+        atomicMin((unsigned long long *)a.err, (unsigned long long)((i << 8) | 4u));
 }
 
 // Byte-serial decode of [p, n): mode 0 counts (lines, bytes, end state),
@@ -322,12 +453,14 @@ VcfcDecodeLayout vcfc_decode_workspace_layout(uint64_t n) {
     return L;
 }
 
-hipError_t vcfc_decode_plan(const VcfcDecodeArgs &a, hipStream_t s) {
+hipError_t vcfc_decode_plan(const VcfcDecodeArgs &a, bool exact, hipStream_t s) {
     hipError_t e = hipMemsetAsync(a.err, 0xFF, 8, s);
     if (e != hipSuccess) return e;
     if ((e = hipMemsetAsync(a.seq_count, 0, 4, s)) != hipSuccess) return e;
     if (a.n == 0) return hipMemsetAsync(a.line_off, 0, 8, s);
-    hipLaunchKernelGGL(k_dec_plan, dim3((unsigned)((a.n + DEC_WAVES - 1) / DEC_WAVES)), dim3(64 * DEC_WAVES), 0, s, a);
+    const dim3 grid((unsigned)((a.n + DEC_WAVES - 1) / DEC_WAVES)), block(64 * DEC_WAVES);
+    if (exact) hipLaunchKernelGGL(k_dec_plan<true>, grid, block, 0, s, a);
+    else hipLaunchKernelGGL(k_dec_plan<false>, grid, block, 0, s, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const uint64_t want = (a.n + 255) / 256;
     hipLaunchKernelGGL(k_dec_seq, dim3((unsigned)(want < 1024 ? want : 1024)), dim3(256), 0, s, a);

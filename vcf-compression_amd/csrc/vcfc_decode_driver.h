@@ -114,26 +114,41 @@ inline int decode_section(const uint8_t *h_in, uint64_t n, uint64_t S, Buffers &
         a.seq_count = reinterpret_cast<uint32_t *>(ws + L.seq_count);
         a.err = reinterpret_cast<uint64_t *>(ws + L.err);
         a.partials = reinterpret_cast<uint64_t *>(ws + L.partials);
-        if (vcfc_decode_plan(a, s) != hipSuccess) return ST_E_HIP;
-        uint64_t err = 0;
-        if (hipMemcpyAsync(&err, a.err, 8, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
-            return ST_E_HIP;
-        uint64_t n_lines = nrec;
-        if (err != VCFCD_NO_ERROR) {
-            const uint64_t k = err >> 8;
-            const uint32_t code = (uint32_t)(err & 0xFF);
-            if (code == 2) {   // parse of record k ends off its hop: keep its line, continue byte-serially
-                n_lines = k + 1;
-                if (hipMemcpyAsync(&p_stream, a.end + k, 8, hipMemcpyDeviceToHost, s) != hipSuccess) return ST_E_HIP;
-            } else {
-                n_lines = k;
-                failed = true;
+        // plan (light first: header + REQ only), then write in output
+        // batches; a batch whose write finds a record the light plan got
+        // wrong is re-planned exactly (lines already sunk keep their bytes:
+        // every line before the first wrong record had the right size)
+        bool exact = false;
+        uint64_t n_lines = 0;
+        std::vector<uint64_t> loff;
+        auto plan = [&]() -> int {
+            if (vcfc_decode_plan(a, exact, s) != hipSuccess) return ST_E_HIP;
+            uint64_t err = 0;
+            if (hipMemcpyAsync(&err, a.err, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                hipStreamSynchronize(s) != hipSuccess)
+                return ST_E_HIP;
+            n_lines = nrec;
+            failed = false;
+            p_stream = rec.back();
+            if (err != VCFCD_NO_ERROR) {
+                const uint64_t k = err >> 8;
+                const uint32_t code = (uint32_t)(err & 0xFF);
+                if (code == 2) {   // parse of record k ends off its hop: keep its line, continue byte-serially
+                    n_lines = k + 1;
+                    if (hipMemcpyAsync(&p_stream, a.end + k, 8, hipMemcpyDeviceToHost, s) != hipSuccess) return ST_E_HIP;
+                } else {
+                    n_lines = k;
+                    failed = true;
+                }
             }
-        }
-        std::vector<uint64_t> loff(n_lines + 1);
-        if (hipMemcpyAsync(loff.data(), d_loff, 8 * (n_lines + 1), hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipStreamSynchronize(s) != hipSuccess)
-            return ST_E_HIP;
+            loff.resize(n_lines + 1);
+            if (hipMemcpyAsync(loff.data(), d_loff, 8 * (n_lines + 1), hipMemcpyDeviceToHost, s) != hipSuccess ||
+                hipStreamSynchronize(s) != hipSuccess)
+                return ST_E_HIP;
+            return ST_OK;
+        };
+        int pst = plan();
+        if (pst) return pst;
         std::vector<uint8_t> host;
         for (uint64_t i0 = 0; i0 < n_lines;) {
             uint64_t i1 = i0 + 1;
@@ -143,7 +158,16 @@ inline int decode_section(const uint8_t *h_in, uint64_t n, uint64_t S, Buffers &
             if (!d_out) return ST_E_HIP;
             a.out = d_out - loff[i0];   // lines are written at out + line_off[i]
             a.out_cap = loff[i1];
-            if (vcfc_decode_write(a, i0, i1, s) != hipSuccess) return ST_E_HIP;
+            uint64_t err = 0;
+            if (vcfc_decode_write(a, i0, i1, s) != hipSuccess ||
+                hipMemcpyAsync(&err, a.err, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                hipStreamSynchronize(s) != hipSuccess)
+                return ST_E_HIP;
+            if (err != VCFCD_NO_ERROR && (err & 0xFF) == 4 && !exact) {
+                exact = true;
+                if ((pst = plan())) return pst;
+                continue;   // same i0, exact sizes
+            }
             host.resize(bytes);
             if (hipMemcpyAsync(host.data(), d_out, bytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
                 hipStreamSynchronize(s) != hipSuccess)

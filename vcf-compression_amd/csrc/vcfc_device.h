@@ -70,7 +70,8 @@ struct VcfcDecodeArgs {
     uint64_t *end;              // byte-serial parse end (queued records)
     uint32_t *seq_list;         // records queued for the byte-serial path
     uint32_t *seq_count;
-    uint64_t *err;              // min over records of (i << 8 | code): 2 = parse ends off the hop, 3 = reference error
+    uint64_t *err;              // min over records of (i << 8 | code): 2 = parse ends off the hop, 3 = reference error,
+                                // 4 = light plan was wrong (rerun exactly), 0xFF = out_cap short
     uint64_t *partials;         // scan partials
 };
 
@@ -79,8 +80,11 @@ struct VcfcDecodeLayout {
 };
 
 VcfcDecodeLayout vcfc_decode_workspace_layout(uint64_t n);
-// plan: statuses, sizes, line offsets (no host synchronisation)
-hipError_t vcfc_decode_plan(const VcfcDecodeArgs &a, hipStream_t s);
+// plan: statuses, sizes, line offsets (no host synchronisation).  exact =
+// false scans only headers and REQ and assumes the sample sections are
+// simple; k_dec_write then reports (i << 8 | 4) in err for a record where
+// that was wrong, and the batch must be planned again with exact = true.
+hipError_t vcfc_decode_plan(const VcfcDecodeArgs &a, bool exact, hipStream_t s);
 // write lines [first, last) at a.out + line_off[i] (their plan status must not be an error)
 hipError_t vcfc_decode_write(const VcfcDecodeArgs &a, uint64_t first, uint64_t last, hipStream_t s);
 // one-lane byte-serial decode of in[p, n): out == nullptr counts; st[0..2] =

@@ -84,7 +84,7 @@ def lib():
     L.vcfc_decompress_file.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p]
     L.vcfc_decode_workspace_size.restype = u64
     L.vcfc_decode_workspace_size.argtypes = [u64]
-    L.vcfc_decode_records_device.argtypes = [vp, u64, vp, u64, u64, vp, u64, vp, vp, u64, vp, vp]
+    L.vcfc_decode_records_device.argtypes = [vp, u64, vp, u64, u64, vp, u64, vp, vp, u64, vp, ctypes.c_int, vp]
     L.vcfc_synth_rows_device.argtypes = [vp, vp, u64, vp, vp, vp, u32, ctypes.c_int, u64, vp]
     _lib = L
     return L
@@ -251,9 +251,9 @@ def decode_workspace_size(n_records):
 
 
 def decode_records_device(d_in, in_bytes, d_rec_start, n, samples, d_out, out_cap, d_line_off, d_ws, ws_bytes,
-                          d_err, stream=0):
+                          d_err, stream=0, exact=False):
     raise_for(lib().vcfc_decode_records_device(d_in, in_bytes, d_rec_start, n, samples, d_out, out_cap, d_line_off,
-                                               d_ws, ws_bytes, d_err, stream))
+                                               d_ws, ws_bytes, d_err, int(exact), stream))
 
 
 def synth_rows_device(d_buf, d_line_off, n, d_prefix, d_prefix_off, d_row_af, samples, law, seed, stream=0):
