@@ -136,47 +136,80 @@ __device__ int dec_line_seq(const uint8_t *in, uint64_t n, uint64_t p, uint64_t 
 // 16-byte block holding its first byte (rbase), and no record reaches 4 GiB.
 
 // Wave-parallel scan of a record's sample items (see the header comment),
-// one window of 64 bytes of the sample section [s0, s1) per call (byte s1
-// is the record's LF).  Lane l looks at byte b0 + l (`v`, already read by
-// the caller; valid if < b).  State carries across windows.
+// one window of 256 bytes per call: lane l holds the dword of bytes
+// [b0 + 4l, b0 + 4l + 4) (b0 4-aligned); bytes outside [s0, b) are not part
+// of the sample section (s0 may lie inside the first dword; byte s1 is the
+// record's LF).  Escape flag bytes (0xE1) mark the next 3 bytes as payload
+// and the 4th as its terminator; those may spill into the next lane (DPP)
+// or the next window (carry).  State carries across windows.
 struct ItemState {
     uint32_t got = 0;
-    uint64_t pcarry = 0, tcarry = 0;
+    uint32_t ecarry = 0;   // escape flags of the previous window's lane 63
     bool bad = false;
 };
 struct ItemLane {
-    bool start;      // this lane's byte starts an item
-    uint32_t cnt;    // its tokens
-    uint32_t gb;     // tokens before it
+    uint32_t start;    // bit j: byte j of the lane's dword starts an item
+    uint32_t cnt[4];   // tokens of each byte's item (0 if not a start)
+    uint32_t gb[4];    // tokens before each byte's item
 };
 
-__device__ __forceinline__ ItemLane scan_window(uint32_t v, uint32_t b0, uint32_t b, uint32_t s1, ItemState &st) {
+__device__ __forceinline__ ItemLane scan_window(uint32_t v4, uint32_t b0, uint32_t s0, uint32_t b, uint32_t s1,
+                                                ItemState &st) {
     const uint32_t l = vw::lane_id();
-    const uint32_t k = b0 + l;
-    const bool valid = k < b;
-    const uint64_t E = vw::ballot(valid && v == 0xE1u);
-    // payload: the 3 bytes after an escape flag; terminator: the 4th
-    const uint64_t P = (E << 1) | (E << 2) | (E << 3) | st.pcarry;
-    const uint64_t TM = (E << 4) | st.tcarry;
-    const uint64_t e = E >> 60;
-    st.pcarry = (e >> 1) | (e >> 2) | (e >> 3);
-    st.tcarry = e;
-    const bool is_p = (P >> l) & 1ull, is_t = (TM >> l) & 1ull;
-    bool lb = false;
-    if (valid) {
-        if (is_p) lb = v >= 0x80u || v == '\t' || v == '\n';
-        else if (is_t) lb = v != '\t';
-        else lb = (v & 0xE0u) == 0xE0u && (v != 0xE1u || k + 4 > s1);   // escape needs 3 bytes + TAB/final LF
+    const uint32_t k0 = b0 + 4 * l;
+    uint32_t valid = 0, e = 0, by[4];
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+        by[j] = (v4 >> (8 * j)) & 0xFFu;
+        const bool vj = k0 + j >= s0 && k0 + j < b;
+        valid |= (vj ? 1u : 0u) << j;
+        e |= (vj && by[j] == 0xE1u ? 1u : 0u) << j;
     }
+    const uint32_t ep = vw::shr1(e, st.ecarry);     // escape flags of the previous lane
+    st.ecarry = vw::readlane(e, 63);
+    const uint32_t c = (e << 4) | ep;               // previous lane's bytes below this lane's
+    const uint32_t P = ((c << 1) | (c << 2) | (c << 3)) >> 4 & 0xFu;   // payload bytes
+    const uint32_t T = ep;                          // terminator bytes (4 after a flag)
     ItemLane r;
-    r.start = valid && !is_p && !is_t;
-    r.cnt = !r.start ? 0u : v == 0xE1u ? 1u : v < 0x80u ? v : (v & 0x1Fu);
-    lb = lb || (r.start && r.cnt == 0);
+    r.start = valid & ~P & ~T;
+    bool lb = false;
+    uint32_t sum = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+        const uint32_t x = by[j];
+        const bool vj = (valid >> j) & 1u, pj = (P >> j) & 1u, tj = (T >> j) & 1u, sj = (r.start >> j) & 1u;
+        if (vj && pj && !tj) lb = lb || x >= 0x80u || x == '\t' || x == '\n';
+        if (vj && tj) lb = lb || x != '\t';
+        if (sj) lb = lb || ((x & 0xE0u) == 0xE0u && (x != 0xE1u || k0 + j + 4 > s1));   // escape: 3 bytes + TAB/final LF
+        const uint32_t cj = !sj ? 0u : x == 0xE1u ? 1u : x < 0x80u ? x : (x & 0x1Fu);
+        lb = lb || (sj && cj == 0);
+        r.cnt[j] = cj;
+        r.gb[j] = sum;
+        sum += cj;
+    }
     st.bad = st.bad || vw::ballot(lb) != 0;
-    const uint32_t inc = vw::scan_add(r.cnt);
-    r.gb = st.got + (inc - r.cnt);
+    const uint32_t inc = vw::scan_add(sum);
+    const uint32_t base = st.got + (inc - sum);
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) r.gb[j] += base;
     st.got += vw::readlane(inc, 63);
     return r;
+}
+
+// item word "a|b\t" (little-endian) of the item starting with byte x at
+// position k (escapes: its 3 payload bytes)
+template <class G>
+__device__ __forceinline__ uint32_t item_word(uint32_t x, uint32_t k, G &&at) {
+    uint32_t w;
+    if (x == 0xE1u) {
+        w = at(k + 1) | (at(k + 2) << 8) | (at(k + 3) << 16);
+    } else if (x < 0x80u) {
+        w = 0x307C30u;
+    } else {
+        const uint32_t m = x & 0xE0u;
+        w = (m == 0xA0u ? 0x30u : 0x31u) | 0x7C00u | ((m == 0xC0u ? 0x30u : 0x31u) << 16);
+    }
+    return w | 0x09000000u;
 }
 
 // A record staged through LDS in pieces of up to SB bytes (plus 8 bytes of
@@ -208,11 +241,13 @@ struct Staged {
             *reinterpret_cast<uint4 *>(lds + o) = vw::bload16(rsr, cbase + o);
         vw::wave_sync();
     }
-    // window [k0, k0 + 64) (clipped to re) resident
-    __device__ __forceinline__ void need(uint32_t k0) {
-        if (k0 < cbase || umin32(k0 + 64, re) > cend) load(k0);
+    // window [k0, k0 + w) (clipped to re) resident
+    __device__ __forceinline__ void need(uint32_t k0, uint32_t w = 64) {
+        if (k0 < cbase || umin32(k0 + w, re) > cend) load(k0);
     }
     __device__ __forceinline__ uint32_t at(uint32_t k) const { return lds[k - cbase]; }
+    // the dword at 4-aligned k (bytes past the staged data read as garbage)
+    __device__ __forceinline__ uint32_t at4(uint32_t k) const { return *reinterpret_cast<const uint32_t *>(lds + (k - cbase)); }
 };
 
 // REQ bytes [r0, r0 + req): TAB count and the C-string length (first NUL).
@@ -261,10 +296,10 @@ __global__ __launch_bounds__(256) void k_dec_plan(VcfcDecodeArgs a) {
                 if (FULL) {
                     ItemState st;
                     const uint32_t s0 = rs + 8 + req, s1 = re - 1;
-                    for (uint32_t cur = s0; cur < s1 && !st.bad; cur += 64) {
-                        sg.need(cur);
-                        const uint32_t b = umin32(cur + 64, s1);
-                        (void)scan_window(sg.at(umin32(cur + l, b - 1)), cur, b, s1, st);
+                    for (uint32_t cur = s0 & ~3u; cur < s1 && !st.bad; cur += 256) {
+                        sg.need(cur, 256 + 8);
+                        const uint32_t b = umin32(cur + 256, s1);
+                        (void)scan_window(sg.at4(cur + 4 * l), cur, s0, b, s1, st);
                     }
                     simple = !st.bad && st.got == a.S;
                 }
@@ -383,26 +418,18 @@ __global__ __launch_bounds__(256) void k_dec_write(VcfcDecodeArgs a, uint64_t fi
     };
     const uint32_t s0 = rs + 8 + req, s1 = re - 1;
     ItemState st;
-    for (uint32_t cur = s0; cur < s1; cur += 64) {
-        sg.need(cur);
-        const uint32_t b = umin32(cur + 64, s1);
-        const uint32_t v = sg.at(umin32(cur + l, b - 1));
-        const ItemLane it = scan_window(v, cur, b, s1, st);
-        uint32_t w = 0;
-        if (it.start) {
-            if (v == 0xE1u) {
-                const uint32_t q = cur + l + 1;   // payload: inside the piece or its look-ahead
-                w = sg.at(q) | (sg.at(q + 1) << 8) | (sg.at(q + 2) << 16);
-            } else if (v < 0x80u) {
-                w = 0x307C30u;
-            } else {
-                const uint32_t m = v & 0xE0u;
-                w = (m == 0xA0u ? 0x30u : 0x31u) | 0x7C00u | ((m == 0xC0u ? 0x30u : 0x31u) << 16);
-            }
-            w |= 0x09000000u;
-        }
+    auto at = [&](uint32_t k) { return sg.at(k); };
+    for (uint32_t cur = s0 & ~3u; cur < s1; cur += 256) {
+        sg.need(cur, 256 + 8);
+        const uint32_t b = umin32(cur + 256, s1);
+        const ItemLane it = scan_window(sg.at4(cur + 4 * l), cur, s0, b, s1, st);
+        uint32_t w[4];
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++) w[j] = (it.start >> j) & 1u ? item_word(sg.at(cur + 4 * l + j), cur + 4 * l + j, at) : 0u;
         for (;;) {
-            if (it.start && it.gb >= j0 && it.gb < j0 + TB) W[it.gb - j0] = w;
+#pragma unroll
+            for (uint32_t j = 0; j < 4; j++)
+                if (((it.start >> j) & 1u) && it.gb[j] >= j0 && it.gb[j] < j0 + TB) W[it.gb[j] - j0] = w[j];
             if (st.got < j0 + TB || j0 + TB > S) break;   // the tile is not complete yet
             tile_out(TB);
             j0 += TB;
