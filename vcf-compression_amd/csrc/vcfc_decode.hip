@@ -37,7 +37,7 @@ namespace {
 constexpr int DEC_WAVES = 4;   // records per 256-thread block
 constexpr uint32_t SB = 2048;              // sample bytes staged per piece (k_dec_write)
 constexpr uint32_t SBUF = SB + 48;         // + look-ahead, 16-B alignment slack, last block's overhang
-constexpr uint32_t TB = 512;               // token words per LDS tile (k_dec_write): 8 per lane
+constexpr uint32_t TB = 256;               // token words per LDS tile (k_dec_write): 4 per lane
 
 // per-record status after planning
 constexpr uint32_t DS_SIMPLE = 0;   // line = REQ' + 4S bytes, item fill
@@ -402,9 +402,11 @@ __global__ __launch_bounds__(256) void k_dec_write(VcfcDecodeArgs a, uint64_t fi
 #pragma unroll
         for (uint32_t q = 0; q < PL; q++) w[q] = w[q] ? w[q] : enter;
         const uint32_t t0 = j0 + PL * l;
+        if (j0 + n_tok == S) {   // the line's last tile: its LF replaces the last TAB
 #pragma unroll
-        for (uint32_t q = 0; q < PL; q++)
-            if (t0 + q + 1 == S) w[q] = (w[q] & 0x00FFFFFFu) | 0x0A000000u;   // the line's LF
+            for (uint32_t q = 0; q < PL; q++)
+                if (t0 + q + 1 == S) w[q] = (w[q] & 0x00FFFFFFu) | 0x0A000000u;
+        }
         if (t0 + PL <= j0 + n_tok) {
 #pragma unroll
             for (uint32_t q = 0; q < PL; q += 4)
