@@ -9,6 +9,8 @@
  *   vcfo_decompress    <- decompress2_fd          src/compress.cpp:1214-1257
  *                         + decompress2_metadata_headers_fd :1108-1211
  *                         + decompress2_data_line            :741-986
+ *   vcfo_query         <- query_compressed_file   src/main.cpp:3777-3929
+ *                         + parse_coordinate_string :3993-4026, matches :75-86
  *   vcfo_sparse_offset <- SparsificationConfiguration::compute_sparse_offset
  *                                                 src/sparse.cpp:18-51
  *   vcfo_sparsify      <- sparsify_file           src/sparse.cpp:290-580
@@ -189,13 +191,16 @@ static const char GTS[4][3] = {{'0','|','0'},{'0','|','1'},{'1','|','0'},{'1','|
 
 #define DEMIT(b) do { if (o >= cap) return VCFO_E_NOSPACE; out[o++] = (uint8_t)(b); } while (0)
 
-int vcfo_decompress(const uint8_t *in, size_t n, uint8_t *out, size_t cap, size_t *out_len) {
-    size_t ip = 0, o = 0;
+/* decompress2_metadata_headers_fd (:1108-1211): '##' lines, then one '#'
+ * line; sample count = TABs past the 8th on the header line.  Copies the
+ * lines to out (when non-NULL).  Returns VCFO_OK with *data at the first
+ * data byte, or VCFO_E_FORMAT (the reference throws before writing). */
+static int parse_headers(const uint8_t *in, size_t n, uint8_t *out, size_t cap, size_t *o_io,
+                         size_t *data, uint64_t *samples) {
+    size_t ip = 0, o = *o_io;
     int got_meta = 0, got_header = 0;
     uint64_t sample_count = 0;
     uint8_t c1 = 0;
-    *out_len = 0;
-    /* decompress2_metadata_headers_fd :1108-1211 */
     for (;;) {
         if (ip < n) c1 = in[ip++];
         else if (!got_header || !got_meta) return VCFO_E_FORMAT; /* "File ended before a header or metadata line" */
@@ -213,80 +218,186 @@ int vcfo_decompress(const uint8_t *in, size_t n, uint8_t *out, size_t cap, size_
         uint8_t c2 = in[ip++];
         if (c2 == '#') got_meta = 1;
         else { if (!got_meta) return VCFO_E_FORMAT; got_header = 1; }
-        DEMIT(c1); DEMIT(c2);
+        if (out) { DEMIT(c1); DEMIT(c2); } else o += 2;
         size_t tabs = 0;
         for (;;) {
             if (ip >= n) return VCFO_E_FORMAT;
             uint8_t c3 = in[ip++];
-            if (c3 == '\n') { DEMIT(c3); break; }
+            if (c3 == '\n') { if (out) DEMIT(c3); else o++; break; }
             if (got_header && c3 == '\t') { tabs++; if (tabs > 8) sample_count++; }
-            DEMIT(c3);
+            if (out) DEMIT(c3); else o++;
         }
     }
-    /* data lines: decompress2_data_line :741-986.  decompress2_fd writes the
-     * header lines once they all parse, then each line as it completes
-     * (:1222-1250): on an error the output holds exactly those bytes. */
-    size_t committed = o;
-#define FAIL() do { *out_len = committed; return VCFO_E_FORMAT; } while (0)
-    for (;;) {
-        if (n - ip < 8) break;                     /* 0 or partial header: stop (:768-774) */
-        const uint8_t *h = in + ip;
-        if ((h[0] >> 6) != 3 || (h[4] >> 6) != 3) FAIL(); /* utils.hpp:200-206 */
-        uint32_t req = ((uint32_t)(h[4] & 0x3F) << 24) | ((uint32_t)h[5] << 16) | ((uint32_t)h[6] << 8) | h[7];
-        ip += 8;
-        if (req == 0 || n - ip < req) FAIL();
-        size_t tabs = 0;
-        /* linebuf.append(buf): C string, stops at the first NUL (:798) */
-        int nul = 0;
-        for (uint32_t i = 0; i < req; i++) {
-            uint8_t b = in[ip + i];
-            if (b == '\t') tabs++;
-            if (b == 0) nul = 1;
-            if (!nul) DEMIT(b);
-        }
-        ip += req;
-        if (tabs != 9 && !(tabs == 8 && sample_count == 0)) FAIL();
-        uint64_t got = 0;
-        while (got < sample_count) {
-            if (ip >= n) FAIL();
-            uint8_t b = in[ip++];
-            if ((b & 0x80) == 0) {
-                uint32_t cnt = b & 0x7F;
-                for (uint32_t k = 0; k < cnt; k++) { DEMIT('0'); DEMIT('|'); DEMIT('0'); DEMIT('\t'); }
-                got += cnt;
-                if (got >= sample_count) o--;     /* pop_back the trailing tab (:864-867) */
-            } else if ((b & 0xE0) == 0xE0) {
-                uint32_t ucount = b & 0x1F, u = 0;
-                while (u < ucount) {
-                    if (ip >= n) FAIL();
-                    uint8_t x = in[ip++];
-                    if (x == '\n') {
-                        u++; got++;
-                        if (u != ucount) FAIL();
-                        ip--;                     /* fseek(-1): re-read as the line end */
-                    } else if (x == '\t') {
-                        u++; got++;
-                        if (got < sample_count) DEMIT('\t');
-                    } else {
-                        DEMIT(x);
-                    }
-                }
-            } else {
-                uint32_t m = b & 0xE0, cnt = b & 0x1F;
-                int c = m == M_01 ? 1 : m == M_10 ? 2 : 3;
-                while (cnt--) {
-                    DEMIT(GTS[c][0]); DEMIT(GTS[c][1]); DEMIT(GTS[c][2]);
-                    got++;
+    *o_io = o;
+    *data = ip;
+    *samples = sample_count;
+    return VCFO_OK;
+}
+
+/* decompress2_data_line (:741-986) for the record at *ip_io; appends the
+ * line at out[*o_io].  VCFO_OK (line done), 1 (fewer than 8 bytes left:
+ * the caller's loop ends, :768-774) or VCFO_E_FORMAT / VCFO_E_NOSPACE. */
+static int dec_line(const uint8_t *in, size_t n, size_t *ip_io, uint64_t sample_count,
+                    uint8_t *out, size_t cap, size_t *o_io) {
+    size_t ip = *ip_io, o = *o_io;
+    if (n - ip < 8) return 1;
+    const uint8_t *h = in + ip;
+    if ((h[0] >> 6) != 3 || (h[4] >> 6) != 3) return VCFO_E_FORMAT; /* utils.hpp:200-206 */
+    uint32_t req = ((uint32_t)(h[4] & 0x3F) << 24) | ((uint32_t)h[5] << 16) | ((uint32_t)h[6] << 8) | h[7];
+    ip += 8;
+    if (req == 0 || n - ip < req) return VCFO_E_FORMAT;
+    size_t tabs = 0;
+    /* linebuf.append(buf): C string, stops at the first NUL (:798) */
+    int nul = 0;
+    for (uint32_t i = 0; i < req; i++) {
+        uint8_t b = in[ip + i];
+        if (b == '\t') tabs++;
+        if (b == 0) nul = 1;
+        if (!nul) DEMIT(b);
+    }
+    ip += req;
+    if (tabs != 9 && !(tabs == 8 && sample_count == 0)) return VCFO_E_FORMAT;
+    uint64_t got = 0;
+    while (got < sample_count) {
+        if (ip >= n) return VCFO_E_FORMAT;
+        uint8_t b = in[ip++];
+        if ((b & 0x80) == 0) {
+            uint32_t cnt = b & 0x7F;
+            for (uint32_t k = 0; k < cnt; k++) { DEMIT('0'); DEMIT('|'); DEMIT('0'); DEMIT('\t'); }
+            got += cnt;
+            if (got >= sample_count) o--;     /* pop_back the trailing tab (:864-867) */
+        } else if ((b & 0xE0) == 0xE0) {
+            uint32_t ucount = b & 0x1F, u = 0;
+            while (u < ucount) {
+                if (ip >= n) return VCFO_E_FORMAT;
+                uint8_t x = in[ip++];
+                if (x == '\n') {
+                    u++; got++;
+                    if (u != ucount) return VCFO_E_FORMAT;
+                    ip--;                     /* fseek(-1): re-read as the line end */
+                } else if (x == '\t') {
+                    u++; got++;
                     if (got < sample_count) DEMIT('\t');
+                } else {
+                    DEMIT(x);
                 }
             }
+        } else {
+            uint32_t m = b & 0xE0, cnt = b & 0x1F;
+            int c = m == M_01 ? 1 : m == M_10 ? 2 : 3;
+            while (cnt--) {
+                DEMIT(GTS[c][0]); DEMIT(GTS[c][1]); DEMIT(GTS[c][2]);
+                got++;
+                if (got < sample_count) DEMIT('\t');
+            }
         }
-        if (ip >= n) FAIL();
-        if (in[ip++] != '\n') FAIL();
-        DEMIT('\n');
-        committed = o;
     }
-#undef FAIL
+    if (ip >= n) return VCFO_E_FORMAT;
+    if (in[ip++] != '\n') return VCFO_E_FORMAT;
+    DEMIT('\n');
+    *ip_io = ip;
+    *o_io = o;
+    return VCFO_OK;
+}
+
+int vcfo_decompress(const uint8_t *in, size_t n, uint8_t *out, size_t cap, size_t *out_len) {
+    size_t ip = 0, o = 0;
+    uint64_t sample_count = 0;
+    *out_len = 0;
+    int st = parse_headers(in, n, out, cap, &o, &ip, &sample_count);
+    if (st) return st;
+    /* decompress2_fd writes the header lines once they all parse, then each
+     * line as it completes (:1222-1250): on an error the output holds exactly
+     * those bytes. */
+    for (;;) {
+        st = dec_line(in, n, &ip, sample_count, out, cap, &o);
+        if (st == 1) break;
+        if (st) { *out_len = o; return st; }
+    }
+    *out_len = o;
+    return VCFO_OK;
+}
+
+/* str_to_uint64 (src/utils.cpp:152-165): strtoul(s.c_str(), &end, 10) and
+ * success iff end == s.c_str() + s.size().  An empty string converts to 0
+ * (no digits: end == start == the end); a NUL inside stops strtoul early. */
+static int str_to_uint64(const uint8_t *s, size_t n, uint64_t *out) {
+    if (n == 0) { *out = 0; return 1; }
+    return vcfo_strtoul_whole(s, n, out);
+}
+
+/* parse_coordinate_string (src/main.cpp:3993-4026): "<ref>" alone, or
+ * "<ref>:<start>-<end>" (ref = text before the first ':', start/end split at
+ * the first '-' after it, each through str_to_uint64).  Returns 0 and fills
+ * the query, or -1 (the reference prints a message and exits 1). */
+int vcfo_parse_query(const uint8_t *q, size_t n, size_t *ref_len, int *has_range, uint64_t *start, uint64_t *end) {
+    const uint8_t *colon = memchr(q, ':', n);
+    if (!colon) { *ref_len = n; *has_range = 0; *start = *end = 0; return 0; }
+    size_t ci = (size_t)(colon - q);
+    const uint8_t *dash = memchr(q + ci + 1, '-', n - ci - 1);
+    if (!dash) return -1;
+    size_t di = (size_t)(dash - q);
+    if (!str_to_uint64(q + ci + 1, di - ci - 1, start)) return -1;
+    if (!str_to_uint64(q + di + 1, n - di - 1, end)) return -1;
+    *ref_len = ci;
+    *has_range = 1;
+    return 0;
+}
+
+/* query_compressed_file (src/main.cpp:3777-3929) with the query of
+ * parse_coordinate_string (:3993-4026) and VcfCoordinateQuery::matches
+ * (:75-86): matching lines (no header) are the output (the reference writes
+ * them to stdout as it goes).  has_range = 0: reference name only. */
+int vcfo_query(const uint8_t *in, size_t n, const uint8_t *qref, size_t qref_len, int has_range,
+               uint64_t qstart, uint64_t qend, uint8_t *out, size_t cap, size_t *out_len) {
+    size_t ip = 0, o = 0;
+    uint64_t sample_count = 0;
+    *out_len = 0;
+    int st = parse_headers(in, n, NULL, 0, &o, &ip, &sample_count);
+    if (st) return st;
+    o = 0;
+    for (;;) {
+        if (ip >= n) break;                              /* read() == 0: done */
+        if (n - ip < 8) { *out_len = o; return VCFO_E_FORMAT; }   /* "Only read %d bytes, expected 4" */
+        const size_t rec = ip;
+        const uint8_t *lenb = in + ip;
+        ip += 8;
+        size_t read_bytes = 8;
+        size_t r0 = ip, rl = 0, p0, pl = 0;
+        for (;;) {
+            if (ip >= n) { *out_len = o; return VCFO_E_FORMAT; }   /* EOF reading the reference name */
+            uint8_t c = in[ip++];
+            read_bytes++;
+            if (c == '\t') break;
+            rl++;
+        }
+        p0 = ip;
+        for (;;) {
+            if (ip >= n) { *out_len = o; return VCFO_E_FORMAT; }   /* EOF reading the position */
+            uint8_t c = in[ip++];
+            read_bytes++;
+            if (c == '\t') break;
+            pl++;
+        }
+        uint64_t pos = 0;
+        if (!str_to_uint64(in + p0, pl, &pos)) { *out_len = o; return VCFO_E_FORMAT; }
+        int match = 1;
+        if (qref_len > 0 && (qref_len != rl || memcmp(qref, in + r0, rl) != 0)) match = 0;
+        if (has_range && (pos < qstart || pos > qend)) match = 0;
+        if (match) {
+            size_t lp = rec;
+            st = dec_line(in, n, &lp, sample_count, out, cap, &o);
+            if (st == 1) { *out_len = o; return VCFO_E_FORMAT; }   /* "Unexpected EOF" */
+            if (st) { *out_len = o; return st; }
+            ip = lp;
+        } else {
+            if ((lenb[0] >> 6) != 3) { *out_len = o; return VCFO_E_FORMAT; }   /* deserialize: extension count */
+            uint32_t L = ((uint32_t)(lenb[0] & 0x3F) << 24) | ((uint32_t)lenb[1] << 16) | ((uint32_t)lenb[2] << 8) | lenb[3];
+            uint32_t skip = L - (uint32_t)(read_bytes - 4);     /* uint32 arithmetic, as the reference */
+            if ((size_t)skip > n - ip) break;                   /* lseek past EOF: the next read returns 0 */
+            ip += skip;
+        }
+    }
     *out_len = o;
     return VCFO_OK;
 }

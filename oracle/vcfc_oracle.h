@@ -22,6 +22,9 @@ size_t vcfo_encode_bound(size_t line_len);
 int vcfo_compress(const uint8_t *in, size_t n, uint8_t *out, size_t cap,
                   size_t *out_len, int64_t *err_line);
 int vcfo_decompress(const uint8_t *in, size_t n, uint8_t *out, size_t cap, size_t *out_len);
+int vcfo_parse_query(const uint8_t *q, size_t n, size_t *ref_len, int *has_range, uint64_t *start, uint64_t *end);
+int vcfo_query(const uint8_t *in, size_t n, const uint8_t *qref, size_t qref_len, int has_range,
+               uint64_t qstart, uint64_t qend, uint8_t *out, size_t cap, size_t *out_len);
 uint64_t vcfo_sparse_offset(uint64_t pos);
 int vcfo_sparsify(const uint8_t *in, size_t n, const char *out_path);
 int vcfo_strtoul_whole(const uint8_t *s, size_t n, uint64_t *out);

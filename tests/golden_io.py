@@ -42,6 +42,11 @@ def oracle():
         lib.vcfo_compress.argtypes = [u8p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, szp,
                                       ctypes.POINTER(ctypes.c_int64)]
         lib.vcfo_decompress.argtypes = [u8p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, szp]
+        u64 = ctypes.c_uint64
+        lib.vcfo_parse_query.argtypes = [u8p, ctypes.c_size_t, szp, ctypes.POINTER(ctypes.c_int),
+                                         ctypes.POINTER(u64), ctypes.POINTER(u64)]
+        lib.vcfo_query.argtypes = [u8p, ctypes.c_size_t, u8p, ctypes.c_size_t, ctypes.c_int, u64, u64,
+                                   ctypes.c_void_p, ctypes.c_size_t, szp]
         lib.vcfo_sparsify.argtypes = [u8p, ctypes.c_size_t, ctypes.c_char_p]
         lib.vcfo_sparse_offset.restype = ctypes.c_uint64
         lib.vcfo_sparse_offset.argtypes = [ctypes.c_uint64]
@@ -77,3 +82,38 @@ def oracle_decompress(data, cap=None):
     n = ctypes.c_size_t(0)
     st = lib.vcfo_decompress(data, len(data), buf, cap, ctypes.byref(n))
     return st, buf.raw[:n.value]
+
+
+def oracle_parse_query(q):
+    """parse_coordinate_string: None on failure, else (ref, has_range, start, end)."""
+    lib = oracle()
+    rl, hr = ctypes.c_size_t(0), ctypes.c_int(0)
+    a, b = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    if lib.vcfo_parse_query(q, len(q), ctypes.byref(rl), ctypes.byref(hr), ctypes.byref(a), ctypes.byref(b)) != 0:
+        return None
+    return q[:rl.value], bool(hr.value), a.value, b.value
+
+
+def oracle_query(data, q, cap=None):
+    """query_compressed_file over bytes: (status, matching lines)."""
+    lib = oracle()
+    pq = oracle_parse_query(q)
+    assert pq is not None
+    ref, hr, a, b = pq
+    cap = cap or len(data) * 600 + 4096
+    buf = ctypes.create_string_buffer(cap)
+    n = ctypes.c_size_t(0)
+    st = lib.vcfo_query(data, len(data), ref, len(ref), int(hr), a, b, buf, cap, ctypes.byref(n))
+    return st, buf.raw[:n.value]
+
+
+def query_cases():
+    """(case dict, file bytes) for tests/golden/query_cases.json."""
+    d = json.load(open(os.path.join(GOLDEN, "query_cases.json")))
+    files = {k: bytes.fromhex(v) for k, v in d["inline_files"].items()}
+    for k, (src, frac) in d["truncated_from"].items():
+        full = gz(src)
+        files[k] = full[:len(full) * 2 // 3]
+    for c in d["cases"]:
+        f = c["file"]
+        yield c, files[f] if f in files else gz(f)
