@@ -45,8 +45,9 @@ def parse():
     ap.add_argument("--cpu-rows", type=int, default=120_000, help="rows in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify-rows", type=int, default=64, help="rows checked against the CPU path")
-    ap.add_argument("--mode", choices=["encode", "decode"], default="encode",
-                    help="encode = the headline (BASELINE metric); decode = row f1 (config 5 building block)")
+    ap.add_argument("--mode", choices=["encode", "decode", "query"], default="encode",
+                    help="encode = the headline (BASELINE metric); decode = row f1; query = row f2")
+    ap.add_argument("--query-frac", type=float, default=0.125, help="rows selected by the --mode query range")
     return ap.parse_args()
 
 
@@ -101,13 +102,13 @@ def load_pmc(workload_key):
     return None
 
 
-def bench_decode(args, torch, vcfc, workload):
-    """Row f1: decode the same synthetic batch (device-resident records made
-    by the GPU encoder) back to VCF lines; every output byte is checked
-    against the original rows on the GPU.  One GPU (replicas only)."""
-    import numpy as np
-    dev = torch.device("cuda:0")
-    torch.cuda.set_device(dev)
+def sample_header(S):
+    return ("##fileformat=VCFv4.2\n##source=vcfc-mi355x bench\n#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT"
+            + "".join("\tS%d" % i for i in range(S)) + "\n").encode()
+
+
+def encoded_shard(args, torch, vcfc, workload, dev):
+    """The synthetic batch and its records, both resident in HBM (GPU encoder)."""
     n, S = args.rows, args.samples
     rows = workload.DeviceRows(torch, vcfc, n, S, args.law, seed=1000, device=dev)
     ws_bytes = vcfc.workspace_size(n, rows.line_bytes)
@@ -116,23 +117,48 @@ def bench_decode(args, torch, vcfc, workload):
     recs = torch.empty(cap, dtype=torch.uint8, device=dev)
     rec = torch.empty(n + 1, dtype=torch.int64, device=dev)
     err = torch.empty(1, dtype=torch.int64, device=dev)
-    stream = torch.cuda.current_stream(dev).cuda_stream
     vcfc.encode_rows_device(rows.buf.data_ptr(), rows.line_off.data_ptr(), rows.line_len.data_ptr(), n,
                             rows.line_bytes, recs.data_ptr(), cap, rec.data_ptr(), ws.data_ptr(), ws_bytes,
-                            err.data_ptr(), stream)
+                            err.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
     torch.cuda.synchronize(dev)
-    rec_bytes = int(rec[n].item())
     del ws
-    dws_bytes = vcfc.decode_workspace_size(n)
-    dws = torch.empty(dws_bytes, dtype=torch.uint8, device=dev)
-    out_cap = rows.total_bytes + 64
-    out = torch.empty(out_cap, dtype=torch.uint8, device=dev)
-    loff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    return rows, recs, rec, int(rec[n].item())
 
-    def step():
-        vcfc.decode_records_device(recs.data_ptr(), rec_bytes, rec.data_ptr(), n, S, out.data_ptr(), out_cap,
-                                   loff.data_ptr(), dws.data_ptr(), dws_bytes, err.data_ptr(), stream)
 
+def cpu_reference_run(rows, recs, rec, args, verb_args):
+    """Time the reference CLI (oracle/_ref/main; else the C restatement) on
+    a .vcfc of the first --cpu-rows rows of the batch.  verb_args(path) ->
+    argv tail, e.g. ["decompress", path, out].  Returns (seconds, rows, kind)."""
+    k = min(args.cpu_rows, rows.n)
+    body = recs[:int(rec[k].item())].cpu().numpy().tobytes()
+    data = sample_header(rows.samples) + body
+    ref = os.path.join(REPO, "oracle", "_ref", "main")
+    with tempfile.TemporaryDirectory(dir="/tmp") as d:
+        path = os.path.join(d, "s.vcfc")
+        with open(path, "wb") as f:
+            f.write(data)
+        argv = verb_args(path)
+        if os.path.exists(ref):
+            with open(os.path.join(d, "stdout"), "wb") as so:
+                t0 = time.perf_counter()
+                r = subprocess.run([ref] + argv, stdout=so, stderr=subprocess.PIPE)
+                dt = time.perf_counter() - t0
+            if r.returncode != 0:
+                raise RuntimeError("reference %s failed: %s" % (argv[0], r.stderr[-400:]))
+            return dt, k, "reference"
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        import golden_io as G
+        t0 = time.perf_counter()
+        if argv[0] == "decompress":
+            st, _ = G.oracle_decompress(data, cap=len(data) * 8 + (1 << 20))
+        else:
+            st, _ = G.oracle_query(data, argv[2].encode(), cap=len(data) * 8 + (1 << 20))
+        dt = time.perf_counter() - t0
+        assert st == 0
+        return dt, k, "port"
+
+
+def timed(torch, dev, args, step):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -143,8 +169,31 @@ def bench_decode(args, torch, vcfc, workload):
         step()
     e1.record()
     torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    ev_ms = e0.elapsed_time(e1) / args.steps
+    return time.perf_counter() - t0, e0.elapsed_time(e1) / args.steps
+
+
+def bench_decode(args, torch, vcfc, workload):
+    """Row f1: decode the same synthetic batch (device-resident records made
+    by the GPU encoder) back to VCF lines; every output byte is checked
+    against the original rows on the GPU.  One GPU (replicas only)."""
+    import numpy as np
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    n, S = args.rows, args.samples
+    rows, recs, rec, rec_bytes = encoded_shard(args, torch, vcfc, workload, dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    err = torch.empty(1, dtype=torch.int64, device=dev)
+    dws_bytes = vcfc.decode_workspace_size(n)
+    dws = torch.empty(dws_bytes, dtype=torch.uint8, device=dev)
+    out_cap = rows.total_bytes + 64
+    out = torch.empty(out_cap, dtype=torch.uint8, device=dev)
+    loff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+
+    def step():
+        vcfc.decode_records_device(recs.data_ptr(), rec_bytes, rec.data_ptr(), n, S, out.data_ptr(), out_cap,
+                                   loff.data_ptr(), dws.data_ptr(), dws_bytes, err.data_ptr(), stream)
+
+    elapsed, ev_ms = timed(torch, dev, args, step)
     e = int(err.cpu().numpy().view(np.uint64)[0])
     total = int(loff[n].item())
     # (light plan: a code-4 report would mean "rerun exact"; it is counted as a failure here)
@@ -163,16 +212,96 @@ def bench_decode(args, torch, vcfc, workload):
                         "frac": round(alg / (ev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
                         "algorithmic_bytes_per_launch": alg, "avg_launch_ms": round(ev_ms, 4)},
            "output_identical_to_input_rows": identical}
+    if not args.no_cpu_baseline:
+        dt, k, kind = cpu_reference_run(rows, recs, rec, args, lambda p: ["decompress", p, p + ".vcf"])
+        res["cpu_baseline"] = {"value": round(4 * S * k / dt / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": kind,
+                               "sample": "`main decompress` of the first %d records (%d GT bytes), wall time %.2f s"
+                                         % (k, 4 * S * k, dt)}
+    print(json.dumps(res), flush=True)
+
+
+def bench_query(args, torch, vcfc, workload):
+    """Row f2: range query over the same device-resident .vcfc records: match
+    every record's CHROM/POS (k_query_match), then decode the selected ones
+    (k_dec_plan + k_dec_write with the match flags).  The query selects
+    --query-frac of the rows (a POS window in the middle of the batch); the
+    output is checked byte-exact against those rows on the GPU."""
+    import numpy as np
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    n, S = args.rows, args.samples
+    rows, recs, rec, rec_bytes = encoded_shard(args, torch, vcfc, workload, dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    a = int(n * (0.5 - args.query_frac / 2))
+    b = min(n - 1, a + max(1, int(n * args.query_frac)) - 1)
+    qs, qe = int(rows.pos[a]), int(rows.pos[b])
+    ref = rows.chrom.encode()
+    d_ref = torch.tensor(list(ref), dtype=torch.uint8, device=dev)
+    flag = torch.empty(n + 64, dtype=torch.uint8, device=dev)
+    merr = torch.empty(1, dtype=torch.int64, device=dev)
+    derr = torch.empty(1, dtype=torch.int64, device=dev)
+    dws_bytes = vcfc.decode_workspace_size(n)
+    dws = torch.empty(dws_bytes, dtype=torch.uint8, device=dev)
+    lo = rows.line_off.cpu().numpy()
+    sel_lines = int(lo[b + 1] if b + 1 < n else rows.total_bytes) - int(lo[a])
+    out_cap = sel_lines + 64
+    out = torch.empty(out_cap, dtype=torch.uint8, device=dev)
+    loff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+
+    def step():
+        st = vcfc.query_match_device(recs.data_ptr(), rec.data_ptr(), n, d_ref.data_ptr(), len(ref), True, qs, qe,
+                                     flag.data_ptr(), merr.data_ptr(), stream)
+        vcfc.raise_for(st)
+        vcfc.decode_selected_device(recs.data_ptr(), rec_bytes, rec.data_ptr(), flag.data_ptr(), n, S, out.data_ptr(),
+                                    out_cap, loff.data_ptr(), dws.data_ptr(), dws_bytes, derr.data_ptr(), stream)
+
+    elapsed, ev_ms = timed(torch, dev, args, step)
+    e1 = int(merr.cpu().numpy().view(np.uint64)[0])
+    e2 = int(derr.cpu().numpy().view(np.uint64)[0])
+    total = int(loff[n].item())
+    want = rows.buf[int(lo[a]):int(lo[a]) + sel_lines]
+    identical = (e1 == vcfc.NO_ERROR and e2 == vcfc.NO_ERROR and total == sel_lines
+                 and int(flag[:n].sum().item()) == b - a + 1 and bool(torch.equal(out[:total], want)))
+    sel_rec = int(rec[b + 1].item()) - int(rec[a].item())
+    # algorithmic bytes: per record its offset (8), LEN/REQ + CHROM\tPOS\t (read), its flag (write); the
+    # selected records once more in full, their lines written, plus the line offsets
+    fields = 8 + len(ref) + 1 + float(np.mean([len(str(p)) for p in rows.pos[:1000]])) + 1
+    alg = int(n * (8 + fields + 1 + 8) + sel_rec + sel_lines)
+    q = "%s:%d-%d" % (rows.chrom, qs, qe)
+    res = {"metric": "queried .vcfc bytes/sec, range query over a 2504-sample x 1M-variant .vcfc (row f2)",
+           "value": round(rec_bytes * args.steps / elapsed / 1e9, 2), "unit": "GB/s", "n_gpus": 1,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+           "higher_is_better": True, "scaling": "replicas", "vs_baseline": None, "dtype": "u8",
+           "data": "synthetic (generated and encoded in HBM)",
+           "config": {"workload": "%s %d samples x %d variants, query %s (%d rows, %.1f%%)"
+                                  % ("chr22-shaped" if args.law == 1 else "random_vcf-law", S, n, q, b - a + 1,
+                                     100.0 * (b - a + 1) / n),
+                      "record_bytes": rec_bytes, "selected_record_bytes": sel_rec, "line_bytes": total},
+           "roofline": {"kernel": "k_query_match + k_dec_plan + k_dec_write", "bound": "hbm",
+                        "achieved": round(alg / (ev_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(alg / (ev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                        "algorithmic_bytes_per_launch": alg, "avg_launch_ms": round(ev_ms, 4)},
+           "output_identical_to_selected_rows": identical}
+    if not args.no_cpu_baseline:
+        k = min(args.cpu_rows, n)
+        ka = int(k * (0.5 - args.query_frac / 2))
+        kb = min(k - 1, ka + max(1, int(k * args.query_frac)) - 1)
+        kq = "%s:%d-%d" % (rows.chrom, int(rows.pos[ka]), int(rows.pos[kb]))
+        dt, k, kind = cpu_reference_run(rows, recs, rec, args, lambda p: ["query", p, kq])
+        kbytes = int(rec[k].item())
+        res["cpu_baseline"] = {"value": round(kbytes / dt / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": kind,
+                               "sample": "`main query %s` over the first %d records (%d .vcfc bytes), wall time %.2f s"
+                                         % (kq, k, kbytes, dt)}
     print(json.dumps(res), flush=True)
 
 
 def main():
     args = parse()
-    if args.mode == "decode":
+    if args.mode in ("decode", "query"):
         import torch
         import vcfc
         import workload
-        return bench_decode(args, torch, vcfc, workload)
+        return (bench_decode if args.mode == "decode" else bench_query)(args, torch, vcfc, workload)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -146,6 +146,43 @@ uint64_t vcfc_decode_workspace_size(uint64_t n_records);
 int vcfc_decode_records_device(const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_rec_start, uint64_t n,
                                uint64_t samples, uint8_t *d_out, uint64_t out_cap, uint64_t *d_line_off,
                                void *d_ws, uint64_t ws_bytes, uint64_t *d_err, int exact, void *stream);
+/* As vcfc_decode_records_device, for the records with d_select[i] != 0 only
+ * (the others get no line: d_line_off[i + 1] == d_line_off[i]); d_select =
+ * the range query's match flags (vcfc_query_match_device). */
+int vcfc_decode_selected_device(const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_rec_start,
+                                const uint8_t *d_select, uint64_t n, uint64_t samples, uint8_t *d_out,
+                                uint64_t out_cap, uint64_t *d_line_off, void *d_ws, uint64_t ws_bytes,
+                                uint64_t *d_err, int exact, void *stream);
+
+/* ---- range query: query_compressed_file (reference src/main.cpp:3777-3929)
+ * Lines (no header) of the records whose CHROM equals `ref` (ref_len == 0:
+ * any name) and, when has_range, whose POS lies in [start, end]
+ * (VcfCoordinateQuery::matches, src/main.cpp:75-86), byte-identical to the
+ * reference's stdout.  On VCFC_E_FORMAT (where the reference throws) the
+ * output holds every line the reference writes before throwing.
+ * vcfc_parse_query restates parse_coordinate_string (src/main.cpp:3993-4026):
+ * "<ref>" or "<ref>:<start>-<end>"; returns 0, or 1 (no '-' after the ':'),
+ * 2 (start does not parse), 3 (end does not parse) where the reference
+ * prints its message and exits 1; *ref_len = bytes of q holding the name.
+ * vcfc_query_buffer: VCFC_E_NOSPACE if out_cap is short (*out_len = size
+ * needed); vcfc_query_file writes to out_fd as lines are decoded. */
+int vcfc_parse_query(const char *q, uint64_t q_len, uint64_t *ref_len, int *has_range, uint64_t *start,
+                     uint64_t *end);
+int vcfc_query_buffer(vcfc_ctx *ctx, const uint8_t *in, uint64_t in_bytes, const char *ref, uint64_t ref_len,
+                      int has_range, uint64_t start, uint64_t end, uint8_t *out, uint64_t out_cap,
+                      uint64_t *out_len);
+int vcfc_query_file(vcfc_ctx *ctx, const char *in_vcfc, const char *ref, uint64_t ref_len, int has_range,
+                    uint64_t start, uint64_t end, int out_fd);
+/* Device-resident match step: d_flag[i] = 1 where record
+ * d_in[d_rec_start[i], d_rec_start[i+1]) matches; *d_err = ~0 or min over
+ * records of (i << 8 | 2) where its POS does not parse (the reference
+ * throws) or (i << 8 | 3) where CHROM/POS runs past the record (the
+ * reference's walk leaves the LEN hops there).  d_ref is device memory.
+ * Enqueued on `stream`; decode the flagged records with
+ * vcfc_decode_selected_device. */
+int vcfc_query_match_device(const uint8_t *d_in, const uint64_t *d_rec_start, uint64_t n, const uint8_t *d_ref,
+                            uint64_t ref_len, int has_range, uint64_t start, uint64_t end, uint8_t *d_flag,
+                            uint64_t *d_err, void *stream);
 
 /* ---- sparse layout: sparsify_file (reference src/sparse.cpp:290-580) -------
  * Record i of the .vcfc goes to data_start + (300e6 + POS_i) * 16384

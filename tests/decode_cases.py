@@ -107,3 +107,59 @@ def mutated_files(seed):
     out.append(("req_9tabs_missing", hd + rec(req[:-1], b"\x04")))
     out.append(("S0_row", header(0) + rec(req[:-1].rsplit(b"\t", 1)[0], b"")))
     return out
+
+
+def query_files(seed):
+    """(name, bytes, queries) for the range query (query_compressed_file,
+    reference src/main.cpp:3777-3929): valid files with several CHROMs and
+    odd POS fields, and mutations that make the reference's walk leave the
+    LEN hops (CHROM or POS running past its record, a matched record whose
+    parse ends off its hop) or throw (POS that does not parse)."""
+    rnd = random.Random(seed)
+    S = 40
+    lines = []
+    for i in range(60):
+        chrom = rnd.choice([b"1", b"1", b"2", b"chrX"])   # (the encoder drops empty fields)
+        pos = rnd.choice([b"%d" % (100 + 10 * i), b" %d" % (100 + 10 * i), b"+%d" % i, b"0%d" % i])
+        toks = [CLASSES[rnd.randrange(4) if rnd.random() < 0.3 else 0] for _ in range(S)]
+        lines.append(chrom + b"\t" + pos + b"\trs\tA\tG\t1\tPASS\t.\tGT\t" + b"\t".join(toks))
+    enc = encode_file(S, lines)
+    h = len(header(S))
+    queries = [b"1", b"2:100-400", b"1:0-18446744073709551615", b":150-500", b"chrX:0-0", b"", b"1:300-200"]
+    out = [("mixed", enc, queries)]
+    # locate the records (LEN hops) to aim the mutations
+    recs, p = [], h
+    while p + 8 <= len(enc):
+        L = ((enc[p] & 0x3F) << 24) | (enc[p + 1] << 16) | (enc[p + 2] << 8) | enc[p + 3]
+        recs.append(p)
+        p += 4 + L
+    def mut(name, k, f):
+        b = bytearray(enc)
+        f(b, recs[k])
+        out.append((name, bytes(b), queries[:4]))
+    def retab(b, r, keep):   # TABs of record r past the first `keep` become 'z'
+        end = recs[recs.index(r) + 1] if r != recs[-1] else len(b)
+        seen = 0
+        for j in range(r + 8, end):
+            if b[j] == 9:
+                seen += 1
+                if seen > keep:
+                    b[j] = ord("z")
+    for k in (0, 17, 59):
+        mut("chrom_past%d" % k, k, lambda b, r: retab(b, r, 0))   # CHROM runs into the next record / EOF
+        mut("pos_past%d" % k, k, lambda b, r: retab(b, r, 1))     # POS does
+        mut("pos_bad%d" % k, k, lambda b, r: b.__setitem__(b.index(b"\t", r + 8) + 1, ord("q")))
+    # token counts off the header: matched records whose parse ends off
+    # their hop or throws
+    for k, extra in ((12, -1), (12, 1), (30, -3)):
+        ls = list(lines)
+        ls[k] = b"1" + ls[k][ls[k].index(b"\t"):] + (b"\t0|0" * extra if extra > 0 else b"")
+        if extra < 0:
+            ls[k] = ls[k][:ls[k].rindex(b"\t")] if extra == -1 else b"\t".join(ls[k].split(b"\t")[:extra])
+        out.append(("row%d_tokens%+d" % (k, extra), encode_file(S, ls), queries[:4]))
+    body = enc[h:]
+    for dS in (-1, 2):
+        out.append(("hdr_samples%+d" % dS, header(S + dS) + body, queries[:3]))
+    for cut in (1, 9, 30):
+        out.append(("truncate%d" % cut, enc[:-cut], queries[:3]))
+    return out

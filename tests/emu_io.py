@@ -23,6 +23,9 @@ def lib():
         L.emu_sparse_plan.argtypes = [vp, vp, ctypes.c_uint64, ctypes.c_uint64, vp, vp, vp]
         L.emu_decompress.argtypes = [ctypes.c_char_p, ctypes.c_uint64, vp, ctypes.c_uint64,
                                      ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint64]
+        u64 = ctypes.c_uint64
+        L.emu_query.argtypes = [ctypes.c_char_p, u64, ctypes.c_char_p, u64, ctypes.c_int, u64, u64, vp, u64,
+                                ctypes.POINTER(u64), u64]
         _lib = L
     return _lib
 
@@ -87,4 +90,14 @@ def emu_decompress(data, out_batch=1 << 16, cap=None):
     out = np.zeros(cap, dtype=np.uint8)
     n = ctypes.c_uint64(0)
     st = lib().emu_decompress(data, len(data), out.ctypes.data, cap, ctypes.byref(n), out_batch)
+    return st, out[:n.value].tobytes()
+
+
+def emu_query(data, ref, has_range, start, end, out_batch=1 << 16, cap=None):
+    """Run the product query driver + kernels on the emulator: (status, bytes)."""
+    cap = cap or len(data) * 600 + 4096
+    out = np.zeros(cap, dtype=np.uint8)
+    n = ctypes.c_uint64(0)
+    st = lib().emu_query(data, len(data), ref, len(ref), int(has_range), start, end, out.ctypes.data, cap,
+                         ctypes.byref(n), out_batch)
     return st, out[:n.value].tobytes()

@@ -77,3 +77,25 @@ extern "C" int emu_decompress(const uint8_t *in, uint64_t n, uint8_t *out, uint6
     *out_len = o;
     return st;
 }
+
+// Range query through the product driver (vcfc_dec::query_section).
+extern "C" int emu_query(const uint8_t *in, uint64_t n, const uint8_t *ref, uint64_t ref_len, int has_range,
+                         uint64_t qstart, uint64_t qend, uint8_t *out, uint64_t cap, uint64_t *out_len,
+                         uint64_t out_batch) {
+    uint64_t data_off = 0, S = 0;
+    *out_len = 0;
+    int st = vcfc_dec::parse_header(in, n, &data_off, &S);
+    if (st) return st;
+    uint64_t o = 0;
+    auto sink = [&](const uint8_t *p, uint64_t k) {
+        if (o + k > cap) return false;
+        memcpy(out + o, p, k);
+        o += k;
+        return true;
+    };
+    HostBuffers B;
+    st = vcfc_dec::query_section(in + data_off, n - data_off, S, ref, ref_len, has_range, qstart, qend, B, nullptr,
+                                 sink, out_batch);
+    *out_len = o;
+    return st;
+}

@@ -19,10 +19,13 @@ for s in $STEPS; do
     bench) timeout -k 10 600 python bench.py > "$O/bench.json" 2> "$O/bench.err" || { echo "bench failed rc=$?"; tail -30 "$O/bench.err"; exit 1; } ; cat "$O/bench.json" ;;
     bench0) timeout -k 10 600 python bench.py --law 0 --no-cpu-baseline > "$O/bench_law0.json" 2> "$O/bench_law0.err" || { echo "bench0 failed"; tail -30 "$O/bench_law0.err"; exit 1; } ; cat "$O/bench_law0.json" ;;
     benchdec) timeout -k 10 600 python bench.py --mode decode > "$O/bench_decode.json" 2> "$O/bench_decode.err" || { echo "benchdec failed"; tail -30 "$O/bench_decode.err"; exit 1; } ; cat "$O/bench_decode.json" ;;
-    profdec) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/profdec" -o run -- python3 "$R/bench.py" --mode decode --steps 10 --warmup 2 > "$O/profdec.log" 2>&1) || { echo "profdec failed rc=$?"; tail -30 "$O/profdec.log"; exit 1; } ;;
+    benchq) timeout -k 10 600 python bench.py --mode query > "$O/bench_query.json" 2> "$O/bench_query.err" || { echo "benchq failed"; tail -30 "$O/bench_query.err"; exit 1; } ; cat "$O/bench_query.json" ;;
+    profq) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/profq" -o run -- python3 "$R/bench.py" --mode query --steps 10 --warmup 2 --no-cpu-baseline > "$O/profq.log" 2>&1) || { echo "profq failed rc=$?"; tail -30 "$O/profq.log"; exit 1; } ;;
+    qtests) timeout -k 10 900 python -m pytest tests/test_gpu_query.py tests/test_gpu_decode.py -x -q -p no:cacheprovider > "$O/pytest_q.log" 2>&1 || { echo "qtests failed rc=$?"; tail -40 "$O/pytest_q.log"; exit 1; } ;;
+    profdec) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/profdec" -o run -- python3 "$R/bench.py" --mode decode --steps 10 --warmup 2 --no-cpu-baseline > "$O/profdec.log" 2>&1) || { echo "profdec failed rc=$?"; tail -30 "$O/profdec.log"; exit 1; } ;;
     pmcdec) for P in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" "FETCH_SIZE" "WRITE_SIZE" "GRBM_GUI_ACTIVE SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR"; do
            n=$(echo $P | cut -d' ' -f1)
-           (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --pmc $P --kernel-trace --output-format csv -d "$O/pmcdec_$n" -o run -- python3 "$R/bench.py" --mode decode --steps 3 --warmup 1 > "$O/pmcdec_$n.log" 2>&1) || { echo "pmcdec $n failed rc=$?"; tail -30 "$O/pmcdec_$n.log"; exit 1; }
+           (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --pmc $P --kernel-trace --output-format csv -d "$O/pmcdec_$n" -o run -- python3 "$R/bench.py" --mode decode --steps 3 --warmup 1 --no-cpu-baseline > "$O/pmcdec_$n.log" 2>&1) || { echo "pmcdec $n failed rc=$?"; tail -30 "$O/pmcdec_$n.log"; exit 1; }
          done ;;
     prof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof" -o run -- python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu-baseline > "$O/prof.log" 2>&1) || { echo "prof failed rc=$?"; tail -30 "$O/prof.log"; exit 1; } ;;
     pmc) for P in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" "FETCH_SIZE" "WRITE_SIZE" "GRBM_GUI_ACTIVE SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR"; do

@@ -1,5 +1,6 @@
 // main.cpp -- CLI with the reference's argv contract (src/main.cpp:4028-4185)
-// for the codec path: `main compress|decompress|sparsify <in> <out>`.  Data lines are
+// for the codec path: `main compress|decompress|sparsify <in> <out>` and
+// `main query <in> <query>`.  Data lines are
 // encoded on the GPU through libvcfc.so.  Error messages mirror the
 // reference's exceptions (which terminate the reference process).
 #include <cstdio>
@@ -10,7 +11,8 @@
 #include "vcfc.h"
 
 static int usage() {
-    fprintf(stderr, "./main [compress|decompress|sparsify] <input_file> <output_file>\n");
+    fprintf(stderr, "./main [compress|decompress|sparsify] <input_file> <output_file>\n"
+                    "./main query <input_file> <ref>[:<start>-<end>]\n");
     return 1;
 }
 
@@ -99,6 +101,39 @@ int main(int argc, char **argv) {
             return 1;
         }
         st = vcfc_sparsify_file(ctx, argv[2], argv[3]);
+        vcfc_ctx_destroy(ctx);
+        if (st != VCFC_OK) {
+            fprintf(stderr, "terminate called after throwing an instance of 'VcfValidationError'\n"
+                            "  what():  %s\n", vcfc_strerror(st));
+            return 134;
+        }
+        return 0;
+    }
+    if (action == "query") {
+        // src/main.cpp:4057-4069 -> parse_coordinate_string (:3993-4026),
+        // query_compressed_file (:3777-3929); matching lines go to stdout
+        if (argc < 4) return usage();
+        if (!file_exists(argv[2])) printf("Input file does not exist: %s\n", argv[2]);
+        const std::string q(argv[3]);
+        uint64_t ref_len = 0, start = 0, end = 0;
+        int has_range = 0;
+        const int pq = vcfc_parse_query(q.data(), q.size(), &ref_len, &has_range, &start, &end);
+        if (pq != 0) {
+            const size_t colon = q.find(':'), dash = q.find('-', colon + 1);
+            if (pq == 1) printf("Query must contain a dash character: <ref>:<start>-<end>\n");
+            else if (pq == 2) printf("Failed to parse int from start position: %s\n", q.substr(colon + 1, dash - colon - 1).c_str());
+            else printf("Failed to parse int from end position: %s\n", q.substr(dash + 1).c_str());
+            printf("Failed to parse query string: %s\n", q.c_str());
+            return 1;
+        }
+        vcfc_ctx *ctx = nullptr;
+        int st = vcfc_ctx_create(0, &ctx);
+        if (st != VCFC_OK) {
+            fprintf(stderr, "vcfc: %s\n", vcfc_strerror(st));
+            return 1;
+        }
+        fflush(stdout);
+        st = vcfc_query_file(ctx, argv[2], q.data(), ref_len, has_range, start, end, 1);
         vcfc_ctx_destroy(ctx);
         if (st != VCFC_OK) {
             fprintf(stderr, "terminate called after throwing an instance of 'VcfValidationError'\n"

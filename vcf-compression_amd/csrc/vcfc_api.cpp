@@ -63,7 +63,7 @@ struct vcfc_timer {
 struct vcfc_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    DevBuf in, off, len, out, rec, ws, err, aux;
+    DevBuf in, off, len, out, rec, ws, err, aux, flag, qref;
 };
 
 namespace {
@@ -136,7 +136,8 @@ struct CtxDecodeBuffers : vcfc_dec::Buffers {
     explicit CtxDecodeBuffers(vcfc_ctx *cc) : c(cc) {}
     void *get(int slot, uint64_t bytes) override {
         DevBuf *b = slot == IN ? &c->in : slot == REC ? &c->rec : slot == WS ? &c->ws : slot == OUT ? &c->out
-                  : slot == LINE_OFF ? &c->off : &c->err;
+                  : slot == LINE_OFF ? &c->off : slot == FLAG ? &c->flag
+                  : slot == QREF ? &c->qref : &c->err;
         return b->ensure(bytes) == hipSuccess ? b->p : nullptr;
     }
 };
@@ -182,7 +183,8 @@ void vcfc_ctx_destroy(vcfc_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     c->in.release(); c->off.release(); c->len.release(); c->out.release();
-    c->rec.release(); c->ws.release(); c->err.release();
+    c->rec.release(); c->ws.release(); c->err.release(); c->aux.release();
+    c->flag.release(); c->qref.release();
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -635,18 +637,120 @@ int vcfc_decompress_file(vcfc_ctx *c, const char *in_path, const char *out_path)
     return st;
 }
 
+// ---- range query: query_compressed_file, reference
+// src/main.cpp:3777-3929 ----------------------------------------------------
+
+// parse_coordinate_string (src/main.cpp:3993-4026) with str_to_uint64
+// (src/utils.cpp:152-165: strtoul over the whole string; "" parses as 0)
+static bool str_to_u64(const char *s, uint64_t n, uint64_t *out) {
+    if (n == 0) { *out = 0; return true; }
+    uint64_t i = 0;
+    while (i < n && (s[i] == ' ' || (s[i] >= '\t' && s[i] <= '\r'))) i++;
+    bool neg = false;
+    if (i < n && (s[i] == '+' || s[i] == '-')) { neg = s[i] == '-'; i++; }
+    if (i >= n || s[i] < '0' || s[i] > '9') return false;
+    uint64_t v = 0;
+    bool ovf = false;
+    for (; i < n && s[i] >= '0' && s[i] <= '9'; i++) {
+        const uint64_t d = (uint64_t)(s[i] - '0');
+        ovf = ovf || v > (UINT64_MAX - d) / 10;
+        v = v * 10 + d;
+    }
+    if (i != n) return false;
+    *out = ovf ? UINT64_MAX : (neg ? 0 - v : v);
+    return true;
+}
+
+int vcfc_parse_query(const char *q, uint64_t q_len, uint64_t *ref_len, int *has_range, uint64_t *start,
+                     uint64_t *end) {
+    if ((!q && q_len) || !ref_len || !has_range || !start || !end) return VCFC_E_ARG;
+    const char *colon = q_len ? static_cast<const char *>(memchr(q, ':', q_len)) : nullptr;
+    if (!colon) {
+        *ref_len = q_len; *has_range = 0; *start = *end = 0;
+        return 0;
+    }
+    const uint64_t ci = (uint64_t)(colon - q);
+    const char *dash = static_cast<const char *>(memchr(q + ci + 1, '-', q_len - ci - 1));
+    if (!dash) return 1;
+    const uint64_t di = (uint64_t)(dash - q);
+    if (!str_to_u64(q + ci + 1, di - ci - 1, start)) return 2;
+    if (!str_to_u64(q + di + 1, q_len - di - 1, end)) return 3;
+    *ref_len = ci;
+    *has_range = 1;
+    return 0;
+}
+
+int vcfc_query_buffer(vcfc_ctx *c, const uint8_t *in, uint64_t n, const char *ref, uint64_t ref_len, int has_range,
+                      uint64_t start, uint64_t end, uint8_t *out, uint64_t out_cap, uint64_t *out_len) {
+    if (!c || (!in && n) || (!ref && ref_len) || (!out && out_cap) || !out_len) return VCFC_E_ARG;
+    *out_len = 0;
+    if (hipSetDevice(c->device) != hipSuccess) return VCFC_E_HIP;
+    uint64_t data_off = 0, S = 0;
+    int st = parse_vcfc_header(in, n, &data_off, &S);
+    if (st) return st;
+    uint64_t o = 0;
+    bool fits = true;
+    auto sink = [&](const uint8_t *p, uint64_t k) {
+        if (fits && o + k <= out_cap) memcpy(out + o, p, k);
+        else fits = false;
+        o += k;
+        return true;
+    };
+    CtxDecodeBuffers B(c);
+    st = vcfc_dec::query_section(in + data_off, n - data_off, S, reinterpret_cast<const uint8_t *>(ref), ref_len,
+                                 has_range, start, end, B, c->stream, sink);
+    *out_len = o;
+    if (!fits) return VCFC_E_NOSPACE;
+    return st;
+}
+
+int vcfc_query_file(vcfc_ctx *c, const char *in_path, const char *ref, uint64_t ref_len, int has_range,
+                    uint64_t start, uint64_t end, int out_fd) {
+    if (!c || !in_path || (!ref && ref_len) || out_fd < 0) return VCFC_E_ARG;
+    if (hipSetDevice(c->device) != hipSuccess) return VCFC_E_HIP;
+    MappedFile f;
+    int st = f.open_ro(in_path);
+    if (st) return st;
+    uint64_t data_off = 0, S = 0;
+    if ((st = parse_vcfc_header(f.p, f.n, &data_off, &S))) return st;
+    auto sink = [&](const uint8_t *p, uint64_t k) {
+        while (k) {
+            const ssize_t w = write(out_fd, p, std::min<uint64_t>(k, 1ull << 30));
+            if (w <= 0) return false;
+            p += w;
+            k -= (uint64_t)w;
+        }
+        return true;
+    };
+    CtxDecodeBuffers B(c);
+    return vcfc_dec::query_section(f.p + data_off, f.n - data_off, S, reinterpret_cast<const uint8_t *>(ref), ref_len,
+                                   has_range, start, end, B, c->stream, sink);
+}
+
+int vcfc_query_match_device(const uint8_t *d_in, const uint64_t *d_rec_start, uint64_t n, const uint8_t *d_ref,
+                            uint64_t ref_len, int has_range, uint64_t start, uint64_t end, uint8_t *d_flag,
+                            uint64_t *d_err, void *stream) {
+    if ((n && (!d_in || !d_rec_start || !d_flag)) || (!d_ref && ref_len) || ref_len > 0xFFFFFFFFull || !d_err)
+        return VCFC_E_ARG;
+    VcfcQuery q;
+    q.ref = d_ref; q.ref_len = (uint32_t)ref_len; q.has_range = has_range ? 1u : 0u; q.start = start; q.end = end;
+    return vcfc_query_match(d_in, d_rec_start, n, q, d_flag, d_err, static_cast<hipStream_t>(stream)) == hipSuccess
+               ? VCFC_OK : VCFC_E_HIP;
+}
+
 uint64_t vcfc_decode_workspace_size(uint64_t n_records) { return vcfc_decode_workspace_layout(n_records).total; }
 
-int vcfc_decode_records_device(const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_rec_start, uint64_t n,
-                               uint64_t samples, uint8_t *d_out, uint64_t out_cap, uint64_t *d_line_off, void *d_ws,
-                               uint64_t ws_bytes, uint64_t *d_err, int exact, void *stream) {
+int vcfc_decode_selected_device(const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_rec_start,
+                                const uint8_t *d_select, uint64_t n, uint64_t samples, uint8_t *d_out, uint64_t out_cap,
+                                uint64_t *d_line_off, void *d_ws, uint64_t ws_bytes, uint64_t *d_err, int exact,
+                                void *stream) {
     if ((n && (!d_in || !d_rec_start || !d_out || !d_ws)) || !d_line_off || !d_err) return VCFC_E_ARG;
     const VcfcDecodeLayout L = vcfc_decode_workspace_layout(n);
     if (ws_bytes < L.total) return VCFC_E_NOSPACE;
     uint8_t *ws = static_cast<uint8_t *>(d_ws);
     hipStream_t s = static_cast<hipStream_t>(stream);
     VcfcDecodeArgs a;
-    a.in = d_in; a.n_bytes = in_bytes; a.rec_start = d_rec_start; a.n = n; a.S = samples;
+    a.in = d_in; a.n_bytes = in_bytes; a.rec_start = d_rec_start; a.select = d_select; a.n = n; a.S = samples;
     a.out = d_out; a.out_cap = out_cap; a.line_off = d_line_off;
     a.st = reinterpret_cast<uint32_t *>(ws + L.st);
     a.line_size = reinterpret_cast<uint32_t *>(ws + L.line_size);
@@ -657,6 +761,13 @@ int vcfc_decode_records_device(const uint8_t *d_in, uint64_t in_bytes, const uin
     a.partials = reinterpret_cast<uint64_t *>(ws + L.partials);
     if (vcfc_decode_plan(a, exact != 0, s) != hipSuccess) return VCFC_E_HIP;
     return vcfc_decode_write(a, 0, n, s) == hipSuccess ? VCFC_OK : VCFC_E_HIP;
+}
+
+int vcfc_decode_records_device(const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_rec_start, uint64_t n,
+                               uint64_t samples, uint8_t *d_out, uint64_t out_cap, uint64_t *d_line_off, void *d_ws,
+                               uint64_t ws_bytes, uint64_t *d_err, int exact, void *stream) {
+    return vcfc_decode_selected_device(d_in, in_bytes, d_rec_start, nullptr, n, samples, d_out, out_cap, d_line_off,
+                                       d_ws, ws_bytes, d_err, exact, stream);
 }
 
 }  // extern "C"

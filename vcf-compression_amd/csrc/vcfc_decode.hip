@@ -44,6 +44,7 @@ constexpr uint32_t DS_SIMPLE = 0;   // line = REQ' + 4S bytes, item fill
 constexpr uint32_t DS_SEQ = 1;      // byte-serial path, consistent end
 constexpr uint32_t DS_INCONS = 2;   // byte-serial parse ends off the LEN hop
 constexpr uint32_t DS_ERR = 3;      // the reference throws at this record
+constexpr uint32_t DS_SKIP = 5;     // not selected: no line
 
 // result of dec_line_seq
 constexpr int DL_OK = 0, DL_END = 1, DL_ERR = 2;
@@ -276,6 +277,10 @@ __global__ __launch_bounds__(256) void k_dec_plan(VcfcDecodeArgs a) {
     const uint64_t i = (uint64_t)blockIdx.x * DEC_WAVES + wave;
     if (i >= a.n) return;
     const uint32_t l = vw::lane_id();
+    if (a.select && !a.select[i]) {
+        if (l == 0) { a.st[i] = DS_SKIP; a.line_size[i] = 0; }
+        return;
+    }
     const uint64_t rs_abs = a.rec_start[i], re_abs = a.rec_start[i + 1];
     bool simple = false;
     uint64_t size = 0;
@@ -349,7 +354,7 @@ __global__ __launch_bounds__(256) void k_dec_write(VcfcDecodeArgs a, uint64_t fi
         return;
     }
     uint8_t *line = a.out + L0;
-    if (a.st[i] == DS_ERR) return;   // no line (size 0); the reference throws here
+    if (a.st[i] == DS_ERR || a.st[i] == DS_SKIP) return;   // no line (size 0)
     if (a.st[i] != DS_SIMPLE) {
         if (l == 0) {
             uint64_t size, end;
@@ -465,6 +470,106 @@ __global__ void k_dec_stream(const uint8_t *in, uint64_t n, uint64_t p, uint64_t
     st[2] = lines;
 }
 
+
+// ---------------------------------------------------------------------------
+// Range query: query_compressed_file (reference src/main.cpp:3777-3929).
+// Per record the reference reads LEN and REQ (8 bytes), then CHROM and POS
+// byte by byte up to a TAB each; POS goes through str_to_uint64
+// (src/utils.cpp:152-165: strtoul over the whole field, "" is 0) and throws
+// when that fails.  A match (VcfCoordinateQuery::matches, :75-86) decodes the
+// line from the record start and goes on where the decode ends; otherwise the
+// walk seeks LEN - (bytes read - 4) further, which is the next LEN hop
+// whenever CHROM and POS lie inside the record.
+
+// strtoul(s, &end, 10) with end == s + n required; n == 0 parses as 0
+__device__ bool pos_parse(const uint8_t *s, uint64_t n, uint64_t *out) {
+    if (n == 0) { *out = 0; return true; }
+    uint64_t i = 0;
+    while (i < n && (s[i] == ' ' || (s[i] >= '\t' && s[i] <= '\r'))) i++;
+    bool neg = false;
+    if (i < n && (s[i] == '+' || s[i] == '-')) { neg = s[i] == '-'; i++; }
+    if (i >= n || s[i] < '0' || s[i] > '9') return false;
+    uint64_t v = 0;
+    bool ovf = false;
+    for (; i < n && s[i] >= '0' && s[i] <= '9'; i++) {
+        const uint64_t d = (uint64_t)(s[i] - '0');
+        ovf = ovf || v > (~0ull - d) / 10;
+        v = v * 10 + d;
+    }
+    if (i != n) return false;
+    *out = ovf ? ~0ull : (neg ? 0ull - v : v);
+    return true;
+}
+
+__device__ __forceinline__ bool query_matches(const VcfcQuery &q, const uint8_t *name, uint64_t name_len, uint64_t pos) {
+    if (q.ref_len) {
+        if (name_len != q.ref_len) return false;
+        for (uint32_t k = 0; k < q.ref_len; k++)
+            if (name[k] != q.ref[k]) return false;
+    }
+    return !q.has_range || (pos >= q.start && pos <= q.end);
+}
+
+// CHROM and POS of the record at p: *f0 = CHROM start, *f1 = POS start,
+// *f2 = the TAB after POS (all searched below lim)
+__device__ __forceinline__ bool query_fields(const uint8_t *in, uint64_t p, uint64_t lim, uint64_t *f1, uint64_t *f2) {
+    uint64_t k = p + 8;
+    while (k < lim && in[k] != '\t') k++;
+    if (k >= lim) return false;
+    *f1 = ++k;
+    while (k < lim && in[k] != '\t') k++;
+    if (k >= lim) return false;
+    *f2 = k;
+    return true;
+}
+
+__global__ __launch_bounds__(256) void k_query_match(const uint8_t *in, const uint64_t *rec, uint64_t n, VcfcQuery q,
+                                                     uint8_t *flag, uint64_t *err) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t rs = rec[i], re = rec[i + 1];
+    uint64_t f1 = 0, f2 = 0, pos = 0;
+    uint32_t code = 0;
+    bool m = false;
+    if (!query_fields(in, rs, re, &f1, &f2)) code = 3;
+    else if (!pos_parse(in + f1, f2 - f1, &pos)) code = 2;
+    else m = query_matches(q, in + rs + 8, f1 - 1 - (rs + 8), pos);
+    flag[i] = m ? 1 : 0;
+    if (code) atomicMin((unsigned long long *)err, (unsigned long long)((i << 8) | code));
+}
+
+// One lane: the reference's walk over in[p, n); out == nullptr counts.
+// st[0] = 0 (clean end) or DL_ERR (the reference throws), st[1] = bytes,
+// st[2] = lines.
+__global__ void k_query_stream(const uint8_t *in, uint64_t n, uint64_t p, uint64_t S, VcfcQuery q, uint8_t *out,
+                               uint64_t *st) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    uint64_t o = 0, lines = 0;
+    int r = 0;
+    while (p < n) {
+        if (n - p < 8) { r = DL_ERR; break; }   // "Only read %d bytes, expected 4"
+        uint64_t f1, f2, pos = 0;
+        if (!query_fields(in, p, n, &f1, &f2)) { r = DL_ERR; break; }   // EOF inside CHROM / POS
+        if (!pos_parse(in + f1, f2 - f1, &pos)) { r = DL_ERR; break; }
+        if (query_matches(q, in + p + 8, f1 - 1 - (p + 8), pos)) {
+            uint64_t size = 0, end = 0;
+            if (dec_line_seq(in, n, p, S, out ? out + o : nullptr, &size, &end) != DL_OK) { r = DL_ERR; break; }
+            o += size;
+            lines++;
+            p = end;
+        } else {
+            if ((in[p] >> 6) != 3u) { r = DL_ERR; break; }   // LEN's extension count
+            const uint32_t skip = be30(in + p) - (uint32_t)(f2 + 1 - p - 4);   // uint32, as the reference
+            const uint64_t at = f2 + 1;
+            if ((uint64_t)skip > n - at) break;          // seek past EOF: the next read returns 0
+            p = at + skip;
+        }
+    }
+    st[0] = (uint64_t)r;
+    st[1] = o;
+    st[2] = lines;
+}
+
 }  // namespace
 
 VcfcDecodeLayout vcfc_decode_workspace_layout(uint64_t n) {
@@ -507,5 +612,19 @@ hipError_t vcfc_decode_write(const VcfcDecodeArgs &a, uint64_t first, uint64_t l
 hipError_t vcfc_decode_stream(const uint8_t *in, uint64_t n, uint64_t p, uint64_t S, uint8_t *out, uint64_t *st,
                               hipStream_t s) {
     hipLaunchKernelGGL(k_dec_stream, dim3(1), dim3(64), 0, s, in, n, p, S, out, st);
+    return hipGetLastError();
+}
+
+hipError_t vcfc_query_match(const uint8_t *in, const uint64_t *rec_start, uint64_t n, const VcfcQuery &q,
+                            uint8_t *flag, uint64_t *err, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(err, 0xFF, 8, s);
+    if (e != hipSuccess || n == 0) return e;
+    hipLaunchKernelGGL(k_query_match, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, in, rec_start, n, q, flag, err);
+    return hipGetLastError();
+}
+
+hipError_t vcfc_query_stream(const uint8_t *in, uint64_t n, uint64_t p, uint64_t S, const VcfcQuery &q, uint8_t *out,
+                             uint64_t *st, hipStream_t s) {
+    hipLaunchKernelGGL(k_query_stream, dim3(1), dim3(64), 0, s, in, n, p, S, q, out, st);
     return hipGetLastError();
 }

@@ -59,6 +59,7 @@ struct VcfcDecodeArgs {
     const uint8_t *in;          // data section bytes (device)
     uint64_t n_bytes;           // bytes available from `in` (the byte-serial parse may read past a record)
     const uint64_t *rec_start;  // n + 1 record offsets into `in` (rec_start[n] = end of the hopped range)
+    const uint8_t *select;      // nullptr, or per record: 0 = skip it (no line; the range query's non-matches)
     uint64_t n;                 // records
     uint64_t S;                 // samples declared by the header line
     uint8_t *out;               // decoded lines, concatenated
@@ -93,3 +94,23 @@ hipError_t vcfc_decode_stream(const uint8_t *in, uint64_t n, uint64_t p, uint64_
                               hipStream_t s);
 // exclusive u32 -> u64 scan with out[n] = total (shared with the encoder)
 hipError_t vcfc_scan_u32(const uint32_t *in, uint64_t n, uint64_t *partials, uint64_t *out, hipStream_t s);
+
+// ---------------------------------------------------------------------------
+// Range query (vcfc_decode.hip; reference query_compressed_file,
+// src/main.cpp:3777-3929).  `ref` is device memory.
+struct VcfcQuery {
+    const uint8_t *ref;   // reference name; ref_len == 0 matches every name
+    uint32_t ref_len;
+    uint32_t has_range;   // 0: name only
+    uint64_t start, end;  // inclusive position range
+};
+// one lane per record [rec_start[i], rec_start[i + 1]): flag[i] = 1 if the
+// record matches; err = min over records of (i << 8 | code), code 2 = its
+// POS does not parse (the reference throws), 3 = its CHROM or POS field runs
+// past the record (the reference's walk leaves the LEN hops: continue with
+// vcfc_query_stream from record i)
+hipError_t vcfc_query_match(const uint8_t *in, const uint64_t *rec_start, uint64_t n, const VcfcQuery &q,
+                            uint8_t *flag, uint64_t *err, hipStream_t s);
+// one-lane byte-serial query of in[p, n) (st as vcfc_decode_stream)
+hipError_t vcfc_query_stream(const uint8_t *in, uint64_t n, uint64_t p, uint64_t S, const VcfcQuery &q, uint8_t *out,
+                             uint64_t *st, hipStream_t s);

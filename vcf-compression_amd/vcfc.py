@@ -4,6 +4,7 @@ Mirrors the reference's operator interface for the encode path:
   compress_data_line(line, add_newline=True)   (reference src/compress.hpp:20-23)
   compress_file(in_path, out_path)             (reference src/compress.cpp:205-257)
   decompress / decompress_file                 (reference src/compress.cpp:1214-1257)
+  parse_coordinate_string, query / query_file  (reference src/main.cpp:3777-4026)
 Errors raise VcfValidationError / RuntimeError like the reference's exceptions
 (src/utils.hpp:117-123, src/compress.cpp:9-11,231-234).
 
@@ -12,6 +13,7 @@ If PyTorch is used in the same process, import torch BEFORE loading this
 module so both share one HIP runtime (libvcfc.so binds to whatever
 libamdhip64.so is already loaded).
 """
+import collections
 import ctypes
 import os
 
@@ -31,7 +33,8 @@ EXPORTS = [
     "vcfc_timer_create", "vcfc_timer_destroy", "vcfc_encode_rows_device_timed", "vcfc_timer_read",
     "vcfc_sparse_offset", "vcfc_sparsify_file", "vcfc_sparse_plan_device",
     "vcfc_decompress_buffer", "vcfc_decompress_file", "vcfc_decode_workspace_size",
-    "vcfc_decode_records_device",
+    "vcfc_decode_records_device", "vcfc_parse_query", "vcfc_query_buffer", "vcfc_query_file",
+    "vcfc_query_match_device", "vcfc_decode_selected_device",
 ]
 
 
@@ -86,6 +89,12 @@ def lib():
     L.vcfc_decode_workspace_size.argtypes = [u64]
     L.vcfc_decode_records_device.argtypes = [vp, u64, vp, u64, u64, vp, u64, vp, vp, u64, vp, ctypes.c_int, vp]
     L.vcfc_synth_rows_device.argtypes = [vp, vp, u64, vp, vp, vp, u32, ctypes.c_int, u64, vp]
+    pu64 = ctypes.POINTER(u64)
+    L.vcfc_parse_query.argtypes = [ctypes.c_char_p, u64, pu64, ctypes.POINTER(ctypes.c_int), pu64, pu64]
+    L.vcfc_query_buffer.argtypes = [vp, vp, u64, ctypes.c_char_p, u64, ctypes.c_int, u64, u64, vp, u64, pu64]
+    L.vcfc_query_file.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, u64, ctypes.c_int, u64, u64, ctypes.c_int]
+    L.vcfc_decode_selected_device.argtypes = [vp, u64, vp, vp, u64, u64, vp, u64, vp, vp, u64, vp, ctypes.c_int, vp]
+    L.vcfc_query_match_device.argtypes = [vp, vp, u64, vp, u64, ctypes.c_int, u64, u64, vp, vp, vp]
     _lib = L
     return L
 
@@ -103,6 +112,29 @@ def raise_for(st, where=""):
     if st == E_8COLS:
         raise LengthError(msg)
     raise RuntimeError(msg)
+
+
+class VcfCoordinateQuery(collections.namedtuple("VcfCoordinateQuery", "reference_name has_range start end")):
+    """VcfCoordinateQuery (reference src/main.cpp:60-90): a reference name
+    (b"" matches any) and, when has_range, an inclusive POS range."""
+
+
+def parse_coordinate_string(q):
+    """parse_coordinate_string (reference src/main.cpp:3993-4026), through
+    the C ABI.  Raises ValueError with the reference's message where it
+    prints one and returns -1."""
+    qb = q.encode() if isinstance(q, str) else bytes(q)
+    ref_len, has_range, start, end = ctypes.c_uint64(), ctypes.c_int(), ctypes.c_uint64(), ctypes.c_uint64()
+    st = lib().vcfc_parse_query(qb, len(qb), ctypes.byref(ref_len), ctypes.byref(has_range), ctypes.byref(start),
+                                ctypes.byref(end))
+    if st != 0:
+        colon = qb.find(b":")
+        dash = qb.find(b"-", colon + 1)
+        msg = {1: "Query must contain a dash character: <ref>:<start>-<end>",
+               2: "Failed to parse int from start position: %s" % qb[colon + 1:dash].decode(errors="replace"),
+               3: "Failed to parse int from end position: %s" % qb[dash + 1:].decode(errors="replace")}.get(st)
+        raise ValueError(msg or strerror(st))
+    return VcfCoordinateQuery(qb[:ref_len.value], bool(has_range.value), start.value, end.value)
 
 
 class Context:
@@ -184,6 +216,41 @@ class Context:
     def decompress_file(self, in_path, out_path):
         raise_for(lib().vcfc_decompress_file(self._h, in_path.encode(), out_path.encode()))
 
+    def query_buffer(self, data, query, cap=None):
+        """query_compressed_file (reference src/main.cpp:3777-3929) over .vcfc
+        bytes: the matching lines (no header).  `query` is a
+        VcfCoordinateQuery or a coordinate string.  Returns (status, bytes):
+        on VCFC_E_FORMAT the bytes are every line the reference writes before
+        it throws."""
+        if not isinstance(query, VcfCoordinateQuery):
+            query = parse_coordinate_string(query)
+        src = np.frombuffer(data, dtype=np.uint8)
+        cap = cap if cap is not None else 16 * len(data) + 4096
+        while True:
+            out = np.empty(max(cap, 1), dtype=np.uint8)
+            n = ctypes.c_uint64(0)
+            st = lib().vcfc_query_buffer(self._h, src.ctypes.data, len(data), query.reference_name,
+                                         len(query.reference_name), int(query.has_range), query.start, query.end,
+                                         out.ctypes.data, cap, ctypes.byref(n))
+            if st == E_NOSPACE and n.value > cap:
+                cap = n.value
+                continue
+            return st, out[:n.value].tobytes()
+
+    def query(self, data, query):
+        """Like query_buffer, raising where the reference throws."""
+        st, out = self.query_buffer(data, query)
+        raise_for(st)
+        return out
+
+    def query_file(self, in_path, query, out_fd=1):
+        """Matching lines of a .vcfc file written to out_fd (stdout by
+        default), as `main query <file> <query>`."""
+        if not isinstance(query, VcfCoordinateQuery):
+            query = parse_coordinate_string(query)
+        raise_for(lib().vcfc_query_file(self._h, in_path.encode(), query.reference_name, len(query.reference_name),
+                                        int(query.has_range), query.start, query.end, out_fd))
+
     def sparsify_file(self, in_path, out_path):
         """sparsify_file (reference src/sparse.cpp:290-580)."""
         raise_for(lib().vcfc_sparsify_file(self._h, in_path.encode(), out_path.encode()))
@@ -254,6 +321,18 @@ def decode_records_device(d_in, in_bytes, d_rec_start, n, samples, d_out, out_ca
                           d_err, stream=0, exact=False):
     raise_for(lib().vcfc_decode_records_device(d_in, in_bytes, d_rec_start, n, samples, d_out, out_cap, d_line_off,
                                                d_ws, ws_bytes, d_err, int(exact), stream))
+
+
+def decode_selected_device(d_in, in_bytes, d_rec_start, d_select, n, samples, d_out, out_cap, d_line_off, d_ws,
+                           ws_bytes, d_err, stream=0, exact=False):
+    raise_for(lib().vcfc_decode_selected_device(d_in, in_bytes, d_rec_start, d_select, n, samples, d_out, out_cap,
+                                                d_line_off, d_ws, ws_bytes, d_err, int(exact), stream))
+
+
+def query_match_device(d_in, d_rec_start, n, d_ref, ref_len, has_range, start, end, d_flag, d_err, stream=0):
+    """Device match step of the range query (see include/vcfc.h)."""
+    return lib().vcfc_query_match_device(d_in, d_rec_start, n, d_ref, ref_len, int(has_range), start, end, d_flag,
+                                         d_err, stream)
 
 
 def synth_rows_device(d_buf, d_line_off, n, d_prefix, d_prefix_off, d_row_af, samples, law, seed, stream=0):

@@ -22,13 +22,14 @@ BASES = np.array(list("ATGC"))
 
 
 def prefixes(n, law, seed, row0=0):
-    """Return (prefix bytes blob, prefix_off[n+1] int64, row_af float32 or None)."""
+    """Return (prefix bytes blob, prefix_off[n+1] int64, row_af float32 or None, POS int64[n])."""
     rng = np.random.default_rng(seed)
     ref = rng.integers(0, 4, n)
     if law == 0:
         alt1 = (ref + rng.integers(1, 4, n)) % 4
         alt2 = (alt1 + 1) % 4
         alt2 = np.where(alt2 == ref, (alt2 + 1) % 4, alt2)
+        pos = 10000 + 2 * (row0 + np.arange(n, dtype=np.int64))
         rows = ["1\t%d\tvar%d\t%s\t%s,%s\t100\tPASS\tINFO\tGT\t" % (10000 + 2 * (row0 + i), row0 + i, BASES[r], BASES[a], BASES[b])
                 for i, (r, a, b) in enumerate(zip(ref.tolist(), alt1.tolist(), alt2.tolist()))]
         af = None
@@ -55,7 +56,7 @@ def prefixes(n, law, seed, row0=0):
     plen = np.fromiter((len(r) for r in rows), dtype=np.int64, count=n)
     poff = np.zeros(n + 1, dtype=np.int64)
     np.cumsum(plen, out=poff[1:])
-    return blob, poff, af
+    return blob, poff, af, np.asarray(pos, dtype=np.int64)
 
 
 def layout(prefix_off, samples):
@@ -72,7 +73,8 @@ class DeviceRows:
     """A synthetic batch resident in HBM (torch tensors)."""
 
     def __init__(self, torch, vcfc, n, samples, law, seed, device, row0=0):
-        blob, poff, af = prefixes(n, law, seed, row0)
+        blob, poff, af, self.pos = prefixes(n, law, seed, row0)
+        self.chrom = "1" if law == 0 else "22"
         line_off, line_len, total = layout(poff, samples)
         dev = torch.device(device)
         self.n, self.samples, self.law = n, samples, law
