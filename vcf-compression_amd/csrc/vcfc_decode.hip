@@ -271,16 +271,8 @@ __device__ __forceinline__ void scan_req(Staged &sg, uint32_t r0, uint32_t req, 
 // header, REQ and final LF look right is assumed simple, and k_dec_write
 // verifies the assumption while it writes (code 4 in err: rerun exactly).
 template <bool FULL>
-__global__ __launch_bounds__(256) void k_dec_plan(VcfcDecodeArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t sbuf[DEC_WAVES * SBUF];
-    const uint32_t wave = vw::readfirst(threadIdx.x >> 6);
-    const uint64_t i = (uint64_t)blockIdx.x * DEC_WAVES + wave;
-    if (i >= a.n) return;
+__device__ __forceinline__ void plan_one(const VcfcDecodeArgs &a, uint64_t i, uint8_t *sb) {
     const uint32_t l = vw::lane_id();
-    if (a.select && !a.select[i]) {
-        if (l == 0) { a.st[i] = DS_SKIP; a.line_size[i] = 0; }
-        return;
-    }
     const uint64_t rs_abs = a.rec_start[i], re_abs = a.rec_start[i + 1];
     bool simple = false;
     uint64_t size = 0;
@@ -288,7 +280,7 @@ __global__ __launch_bounds__(256) void k_dec_plan(VcfcDecodeArgs a) {
         const uint64_t rbase = rs_abs & ~15ull;
         const uint32_t rs = (uint32_t)(rs_abs - rbase), re = (uint32_t)(re_abs - rbase);
         Staged sg;
-        sg.init(sbuf + wave * SBUF, a.in + rbase, re);
+        sg.init(sb, a.in + rbase, re);
         sg.load(rs);
         const uint32_t h0 = sg.at(rs), h4 = sg.at(rs + 4);
         const uint32_t req = ((h4 & 0x3Fu) << 24) | (sg.at(rs + 5) << 16) | (sg.at(rs + 6) << 8) | sg.at(rs + 7);
@@ -322,6 +314,33 @@ __global__ __launch_bounds__(256) void k_dec_plan(VcfcDecodeArgs a) {
     }
 }
 
+// Selected decodes (a.select set, the range query): a grid of n / SEL_R
+// waves; wave g takes records g, g + G, g + 2G, ... (G = waves in the grid)
+// and plans / writes the selected ones, so an unselected record costs a flag
+// read instead of a wave launch, and a contiguous selected range (a POS
+// window) spreads over all waves.
+constexpr uint32_t SEL_R = 8;
+
+template <bool FULL, bool SEL>
+__global__ __launch_bounds__(256) void k_dec_plan(VcfcDecodeArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t sbuf[DEC_WAVES * SBUF];
+    const uint32_t wave = vw::readfirst(threadIdx.x >> 6);
+    uint8_t *sb = sbuf + wave * SBUF;
+    const uint64_t g = (uint64_t)blockIdx.x * DEC_WAVES + wave;
+    if (!SEL) {
+        if (g < a.n) plan_one<FULL>(a, g, sb);
+        return;
+    }
+    const uint64_t G = (uint64_t)gridDim.x * DEC_WAVES;
+    const uint32_t l = vw::lane_id();
+    const uint64_t il = g + (uint64_t)l * G;   // lane l < SEL_R: the wave's l-th record
+    const bool mine = l < SEL_R && il < a.n;
+    const bool on = mine && a.select[il];
+    if (mine && !on) { a.st[il] = DS_SKIP; a.line_size[il] = 0; }
+    for (uint64_t m = vw::ballot(on); m; m &= m - 1)
+        plan_one<FULL>(a, g + (uint64_t)__builtin_ctzll(m) * G, sb);
+}
+
 // Queued records, one lane each (grid-stride).
 __global__ __launch_bounds__(256) void k_dec_seq(VcfcDecodeArgs a) {
     const uint32_t cnt = *a.seq_count;
@@ -340,12 +359,7 @@ __global__ __launch_bounds__(256) void k_dec_seq(VcfcDecodeArgs a) {
     }
 }
 
-__global__ __launch_bounds__(256) void k_dec_write(VcfcDecodeArgs a, uint64_t first, uint64_t last) {
-    __shared__ __attribute__((aligned(16))) uint8_t sbuf[DEC_WAVES * SBUF];
-    __shared__ __attribute__((aligned(16))) uint32_t tbuf[DEC_WAVES * TB];
-    const uint32_t wave = vw::readfirst(threadIdx.x >> 6);
-    const uint64_t i = first + (uint64_t)blockIdx.x * DEC_WAVES + wave;
-    if (i >= last) return;
+__device__ __forceinline__ void write_one(const VcfcDecodeArgs &a, uint64_t i, uint8_t *sb, uint32_t *W) {
     const uint32_t l = vw::lane_id();
     const uint64_t rs_abs = a.rec_start[i];
     const uint64_t L0 = a.line_off[i];
@@ -366,7 +380,7 @@ __global__ __launch_bounds__(256) void k_dec_write(VcfcDecodeArgs a, uint64_t fi
     const uint32_t rs = (uint32_t)(rs_abs - rbase), re = (uint32_t)(a.rec_start[i + 1] - rbase);
     const uint32_t S = (uint32_t)a.S;
     Staged sg;
-    sg.init(sbuf + wave * SBUF, a.in + rbase, re);
+    sg.init(sb, a.in + rbase, re);
     sg.load(rs);
     const uint32_t req = ((sg.at(rs + 4) & 0x3Fu) << 24) | (sg.at(rs + 5) << 16) | (sg.at(rs + 6) << 8) | sg.at(rs + 7);
     const uint32_t slen = (uint32_t)(a.line_off[i + 1] - L0 - 4ull * S);   // REQ' = line - 4S
@@ -381,7 +395,6 @@ __global__ __launch_bounds__(256) void k_dec_write(VcfcDecodeArgs a, uint64_t fi
     // in-lane, then across lanes by a max-scan of lane indices and one
     // ds_bpermute) and goes out as contiguous 16-byte stores.  Work per tile
     // does not depend on run lengths.
-    uint32_t *W = tbuf + wave * TB;
     constexpr uint32_t PL = TB / 64;   // slots per lane
     for (uint32_t q = 0; q < PL; q += 4) *reinterpret_cast<uint4 *>(W + PL * l + q) = make_uint4(0, 0, 0, 0);
     uint32_t j0 = 0, carry = 0;   // tile start; word of the item holding token j0
@@ -449,6 +462,25 @@ __global__ __launch_bounds__(256) void k_dec_write(VcfcDecodeArgs a, uint64_t fi
         atomicMin((unsigned long long *)a.err, (unsigned long long)((i << 8) | 4u));
 }
 
+template <bool SEL>
+__global__ __launch_bounds__(256) void k_dec_write(VcfcDecodeArgs a, uint64_t first, uint64_t last) {
+    __shared__ __attribute__((aligned(16))) uint8_t sbuf[DEC_WAVES * SBUF];
+    __shared__ __attribute__((aligned(16))) uint32_t tbuf[DEC_WAVES * TB];
+    const uint32_t wave = vw::readfirst(threadIdx.x >> 6);
+    uint8_t *sb = sbuf + wave * SBUF;
+    uint32_t *W = tbuf + wave * TB;
+    const uint64_t g = (uint64_t)blockIdx.x * DEC_WAVES + wave;
+    if (!SEL) {
+        if (first + g < last) write_one(a, first + g, sb, W);
+        return;
+    }
+    const uint64_t G = (uint64_t)gridDim.x * DEC_WAVES;
+    const uint32_t l = vw::lane_id();
+    const uint64_t il = first + g + (uint64_t)l * G;
+    for (uint64_t m = vw::ballot(l < SEL_R && il < last && a.select[il]); m; m &= m - 1)
+        write_one(a, first + g + (uint64_t)__builtin_ctzll(m) * G, sb, W);
+}
+
 // Byte-serial decode of [p, n): mode 0 counts (lines, bytes, end state),
 // mode 1 writes.  One lane.  st[0] = DL_END (clean end) or DL_ERR; st[1] =
 // bytes; st[2] = lines.
@@ -482,7 +514,7 @@ __global__ void k_dec_stream(const uint8_t *in, uint64_t n, uint64_t p, uint64_t
 // whenever CHROM and POS lie inside the record.
 
 // strtoul(s, &end, 10) with end == s + n required; n == 0 parses as 0
-__device__ bool pos_parse(const uint8_t *s, uint64_t n, uint64_t *out) {
+__device__ __forceinline__ bool pos_parse(const uint8_t *s, uint64_t n, uint64_t *out) {
     if (n == 0) { *out = 0; return true; }
     uint64_t i = 0;
     while (i < n && (s[i] == ' ' || (s[i] >= '\t' && s[i] <= '\r'))) i++;
@@ -510,8 +542,8 @@ __device__ __forceinline__ bool query_matches(const VcfcQuery &q, const uint8_t 
     return !q.has_range || (pos >= q.start && pos <= q.end);
 }
 
-// CHROM and POS of the record at p: *f0 = CHROM start, *f1 = POS start,
-// *f2 = the TAB after POS (all searched below lim)
+// CHROM and POS of the record at p (CHROM starts at p + 8): *f1 = POS start,
+// *f2 = the TAB after POS (both TABs searched below lim)
 __device__ __forceinline__ bool query_fields(const uint8_t *in, uint64_t p, uint64_t lim, uint64_t *f1, uint64_t *f2) {
     uint64_t k = p + 8;
     while (k < lim && in[k] != '\t') k++;
@@ -523,17 +555,56 @@ __device__ __forceinline__ bool query_fields(const uint8_t *in, uint64_t p, uint
     return true;
 }
 
+// bit j of the result: byte j of x is a TAB (exact per byte)
+__device__ __forceinline__ uint32_t tab_bits(uint32_t x) {
+    const uint32_t t = x ^ 0x09090909u;
+    const uint32_t z = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t | 0x7F7F7F7Fu);   // 0x80 in each zero byte
+    return ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
+}
+
+// One lane per record.  Fast path: the 48 bytes from the 16-byte block
+// holding the CHROM start lie inside the record; three 16-byte loads, TABs
+// found by SWAR in registers, the fields parsed from an LDS copy.  Otherwise
+// byte by byte.
+constexpr uint32_t QM_WIN = 48;
 __global__ __launch_bounds__(256) void k_query_match(const uint8_t *in, const uint64_t *rec, uint64_t n, VcfcQuery q,
                                                      uint8_t *flag, uint64_t *err) {
+    __shared__ __attribute__((aligned(16))) uint8_t win[256 * QM_WIN];
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint64_t rs = rec[i], re = rec[i + 1];
+    const uint8_t *p = in + rs + 8;
+    const uint8_t *a = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(p) & ~(uintptr_t)15);
     uint64_t f1 = 0, f2 = 0, pos = 0;
     uint32_t code = 0;
-    bool m = false;
-    if (!query_fields(in, rs, re, &f1, &f2)) code = 3;
-    else if (!pos_parse(in + f1, f2 - f1, &pos)) code = 2;
-    else m = query_matches(q, in + rs + 8, f1 - 1 - (rs + 8), pos);
+    bool m = false, done = false;
+    if (a + QM_WIN <= in + re) {
+        const uint4 *g = reinterpret_cast<const uint4 *>(a);
+        const uint4 v0 = g[0], v1 = g[1], v2 = g[2];
+        uint4 *w = reinterpret_cast<uint4 *>(win + threadIdx.x * QM_WIN);
+        w[0] = v0; w[1] = v1; w[2] = v2;
+        const uint64_t tabs = (uint64_t)tab_bits(v0.x) | (uint64_t)tab_bits(v0.y) << 4 | (uint64_t)tab_bits(v0.z) << 8 |
+                              (uint64_t)tab_bits(v0.w) << 12 | (uint64_t)tab_bits(v1.x) << 16 |
+                              (uint64_t)tab_bits(v1.y) << 20 | (uint64_t)tab_bits(v1.z) << 24 |
+                              (uint64_t)tab_bits(v1.w) << 28 | (uint64_t)tab_bits(v2.x) << 32 |
+                              (uint64_t)tab_bits(v2.y) << 36 | (uint64_t)tab_bits(v2.z) << 40 |
+                              (uint64_t)tab_bits(v2.w) << 44;
+        const uint32_t sh = (uint32_t)(p - a);
+        const uint64_t t = tabs >> sh;
+        const uint64_t t2 = t & (t - 1);
+        if (t2) {   // both TABs inside the window
+            const uint32_t c = (uint32_t)__builtin_ctzll(t), d = (uint32_t)__builtin_ctzll(t2);
+            const uint8_t *f = win + threadIdx.x * QM_WIN + sh;
+            if (!pos_parse(f + c + 1, d - c - 1, &pos)) code = 2;
+            else m = query_matches(q, f, c, pos);
+            done = true;
+        }
+    }
+    if (!done) {
+        if (!query_fields(in, rs, re, &f1, &f2)) code = 3;
+        else if (!pos_parse(in + f1, f2 - f1, &pos)) code = 2;
+        else m = query_matches(q, in + rs + 8, f1 - 1 - (rs + 8), pos);
+    }
     flag[i] = m ? 1 : 0;
     if (code) atomicMin((unsigned long long *)err, (unsigned long long)((i << 8) | code));
 }
@@ -592,9 +663,15 @@ hipError_t vcfc_decode_plan(const VcfcDecodeArgs &a, bool exact, hipStream_t s) 
     if (e != hipSuccess) return e;
     if ((e = hipMemsetAsync(a.seq_count, 0, 4, s)) != hipSuccess) return e;
     if (a.n == 0) return hipMemsetAsync(a.line_off, 0, 8, s);
-    const dim3 grid((unsigned)((a.n + DEC_WAVES - 1) / DEC_WAVES)), block(64 * DEC_WAVES);
-    if (exact) hipLaunchKernelGGL(k_dec_plan<true>, grid, block, 0, s, a);
-    else hipLaunchKernelGGL(k_dec_plan<false>, grid, block, 0, s, a);
+    const uint64_t per_wave = a.select ? SEL_R : 1;
+    const dim3 grid((unsigned)((a.n + DEC_WAVES * per_wave - 1) / (DEC_WAVES * per_wave))), block(64 * DEC_WAVES);
+    if (a.select) {
+        if (exact) hipLaunchKernelGGL((k_dec_plan<true, true>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((k_dec_plan<false, true>), grid, block, 0, s, a);
+    } else {
+        if (exact) hipLaunchKernelGGL((k_dec_plan<true, false>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((k_dec_plan<false, false>), grid, block, 0, s, a);
+    }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const uint64_t want = (a.n + 255) / 256;
     hipLaunchKernelGGL(k_dec_seq, dim3((unsigned)(want < 1024 ? want : 1024)), dim3(256), 0, s, a);
@@ -604,8 +681,10 @@ hipError_t vcfc_decode_plan(const VcfcDecodeArgs &a, bool exact, hipStream_t s) 
 
 hipError_t vcfc_decode_write(const VcfcDecodeArgs &a, uint64_t first, uint64_t last, hipStream_t s) {
     if (last <= first) return hipSuccess;
-    hipLaunchKernelGGL(k_dec_write, dim3((unsigned)((last - first + DEC_WAVES - 1) / DEC_WAVES)), dim3(64 * DEC_WAVES), 0,
-                       s, a, first, last);
+    const uint64_t per_block = DEC_WAVES * (a.select ? SEL_R : 1);
+    const dim3 grid((unsigned)((last - first + per_block - 1) / per_block)), block(64 * DEC_WAVES);
+    if (a.select) hipLaunchKernelGGL(k_dec_write<true>, grid, block, 0, s, a, first, last);
+    else hipLaunchKernelGGL(k_dec_write<false>, grid, block, 0, s, a, first, last);
     return hipGetLastError();
 }
 
