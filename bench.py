@@ -45,8 +45,10 @@ def parse():
     ap.add_argument("--cpu-rows", type=int, default=120_000, help="rows in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify-rows", type=int, default=64, help="rows checked against the CPU path")
-    ap.add_argument("--mode", choices=["encode", "decode", "query"], default="encode",
-                    help="encode = the headline (BASELINE metric); decode = row f1; query = row f2")
+    ap.add_argument("--mode", choices=["encode", "decode", "query", "ingest"], default="encode",
+                    help="encode = the headline (BASELINE metric); decode = row f1; query = row f2; "
+                         "ingest = row f4 (end-to-end file compress)")
+    ap.add_argument("--ingest-rows", type=int, default=200_000, help="rows of the --mode ingest file")
     ap.add_argument("--query-frac", type=float, default=0.125, help="rows selected by the --mode query range")
     return ap.parse_args()
 
@@ -295,13 +297,96 @@ def bench_query(args, torch, vcfc, workload):
     print(json.dumps(res), flush=True)
 
 
+def bench_ingest(args, torch, vcfc, workload):
+    """Row f4: end-to-end `compress` of a VCF file on disk to a .vcfc file
+    (vcfc_compress_file: reader threads -> pinned H2D -> GPU line index +
+    encode -> writer thread).  The file holds --ingest-rows synthetic rows
+    (written from HBM, so it sits in the page cache, as in a pipeline that
+    has just produced it); the output is checked byte-for-byte against the
+    GPU encoder's device-resident records."""
+    import numpy as np
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    args.rows = args.ingest_rows
+    n, S = args.rows, args.samples
+    rows, recs, rec, rec_bytes = encoded_shard(args, torch, vcfc, workload, dev)
+    header = sample_header(S)
+    want = header + recs[:rec_bytes].cpu().numpy().tobytes()
+    del recs
+    tmp = tempfile.mkdtemp(dir="/tmp")
+    src, dst = os.path.join(tmp, "in.vcf"), os.path.join(tmp, "out.vcfc")
+    try:
+        with open(src, "wb") as f:
+            f.write(header)
+            step = 1 << 28
+            for a in range(0, rows.total_bytes, step):
+                f.write(rows.buf[a:min(rows.total_bytes, a + step)].cpu().numpy().tobytes())
+        in_bytes = len(header) + rows.total_bytes
+        # pinned H2D peak of this box (the bound of the pipeline's transfer stage)
+        hb = torch.empty(256 << 20, dtype=torch.uint8).pin_memory()
+        db = torch.empty(256 << 20, dtype=torch.uint8, device=dev)
+        db.copy_(hb, non_blocking=True)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(5):
+            db.copy_(hb, non_blocking=True)
+        torch.cuda.synchronize(dev)
+        h2d = 5 * (256 << 20) / (time.perf_counter() - t0) / 1e9
+        del hb, db
+        ctx = vcfc.Context(0)
+        for _ in range(args.warmup):
+            ctx.compress_file(src, dst)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            ctx.compress_file(src, dst)
+        elapsed = time.perf_counter() - t0
+        identical = open(dst, "rb").read() == want
+        ctx.close()
+        res = {"metric": "end-to-end input GT bytes/sec, VCF file -> .vcfc file (row f4)",
+               "value": round(rows.gt_bytes * args.steps / elapsed / 1e9, 3), "unit": "GB/s", "n_gpus": 1,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
+               "higher_is_better": True, "scaling": "replicas", "vs_baseline": None, "dtype": "u8",
+               "data": "synthetic (generated in HBM, written to a file in the page cache)",
+               "config": {"workload": "%s %d samples x %d variants, %.2f GB file"
+                                      % ("chr22-shaped" if args.law == 1 else "random_vcf-law", S, n, in_bytes / 1e9),
+                          "input_bytes": in_bytes, "output_bytes": len(want)},
+               "roofline": {"kernel": "pipeline (file read + H2D + index + encode + D2H + write)", "bound": "pcie",
+                            "achieved": round(in_bytes * args.steps / elapsed / 1e9, 2), "peak": round(h2d, 1),
+                            "unit": "GB/s", "frac": round(in_bytes * args.steps / elapsed / 1e9 / h2d, 4),
+                            "traffic": None, "peak_note": "pinned H2D of this box, measured"},
+               "output_identical_to_gpu_records": identical}
+        if not args.no_cpu_baseline:
+            k = min(args.cpu_rows, n)
+            end = int(rows.line_off[k].item()) if k < n else rows.total_bytes
+            with open(os.path.join(tmp, "s.vcf"), "wb") as f:
+                f.write(header)
+                f.write(rows.buf[:end].cpu().numpy().tobytes())
+            ref = os.path.join(REPO, "oracle", "_ref", "main")
+            if os.path.exists(ref):
+                t0 = time.perf_counter()
+                r = subprocess.run([ref, "compress", os.path.join(tmp, "s.vcf"), os.path.join(tmp, "s.vcfc")],
+                                   capture_output=True)
+                dt = time.perf_counter() - t0
+                if r.returncode == 0:
+                    res["cpu_baseline"] = {"value": round(4 * S * k / dt / 1e9, 4), "unit": "GB/s", "cores": 1,
+                                           "kind": "reference",
+                                           "sample": "`main compress` of the first %d rows (file -> file), %.2f s"
+                                                     % (k, dt)}
+        print(json.dumps(res), flush=True)
+    finally:
+        for f in os.listdir(tmp):
+            os.unlink(os.path.join(tmp, f))
+        os.rmdir(tmp)
+
+
 def main():
     args = parse()
-    if args.mode in ("decode", "query"):
+    if args.mode in ("decode", "query", "ingest"):
         import torch
         import vcfc
         import workload
-        return (bench_decode if args.mode == "decode" else bench_query)(args, torch, vcfc, workload)
+        fn = {"decode": bench_decode, "query": bench_query, "ingest": bench_ingest}[args.mode]
+        return fn(args, torch, vcfc, workload)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

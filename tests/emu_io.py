@@ -26,6 +26,8 @@ def lib():
         u64 = ctypes.c_uint64
         L.emu_query.argtypes = [ctypes.c_char_p, u64, ctypes.c_char_p, u64, ctypes.c_int, u64, u64, vp, u64,
                                 ctypes.POINTER(u64), u64]
+        L.emu_compress.argtypes = [ctypes.c_char_p, u64, vp, u64, ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_int64),
+                                   u64, ctypes.c_int]
         _lib = L
     return _lib
 
@@ -101,3 +103,15 @@ def emu_query(data, ref, has_range, start, end, out_batch=1 << 16, cap=None):
     st = lib().emu_query(data, len(data), ref, len(ref), int(has_range), start, end, out.ctypes.data, cap,
                          ctypes.byref(n), out_batch)
     return st, out[:n.value].tobytes()
+
+
+def emu_compress(vcf, chunk=4096, read_threads=2, cap=None):
+    """compress() through the product ingest pipeline on the emulator:
+    (status, bytes, err_line)."""
+    cap = cap or 2 * len(vcf) + 4096
+    out = np.zeros(cap, dtype=np.uint8)
+    n = ctypes.c_uint64(0)
+    el = ctypes.c_int64(-1)
+    st = lib().emu_compress(vcf, len(vcf), out.ctypes.data, cap, ctypes.byref(n), ctypes.byref(el), chunk,
+                            read_threads)
+    return st, out[:n.value].tobytes(), el.value

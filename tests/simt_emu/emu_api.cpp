@@ -99,3 +99,51 @@ extern "C" int emu_query(const uint8_t *in, uint64_t n, const uint8_t *ref, uint
     *out_len = o;
     return st;
 }
+
+// Pipelined compress() through the product driver (vcfc_ing::compress_stream)
+// with a small chunk size, so carries across chunks and the '#' line
+// interleave are exercised on small inputs.
+#include "vcfc_ingest_driver.h"
+namespace {
+struct HostIngestMemory : vcfc_ing::Memory {
+    std::vector<uint8_t> d[N_DEV], h[N_HOST];
+    void *dev(int slot, uint64_t bytes) override {
+        if (d[slot].size() < bytes + 16) d[slot].assign(bytes + 16, 0xCD);   // poison
+        return d[slot].data();
+    }
+    void *host(int slot, uint64_t bytes) override {
+        if (h[slot].size() < bytes + 16) h[slot].assign(bytes + 16, 0xCD);
+        return h[slot].data();
+    }
+};
+struct BufSource : vcfc_ing::Source {
+    const uint8_t *p;
+    uint64_t n;
+    uint64_t size() const override { return n; }
+    bool read(uint8_t *dst, uint64_t off, uint64_t k) override {
+        memcpy(dst, p + off, k);
+        return true;
+    }
+};
+}  // namespace
+
+extern "C" int emu_compress(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len,
+                            int64_t *err_line, uint64_t chunk, int read_threads) {
+    uint64_t o = 0;
+    auto sink = [&](const uint8_t *p, uint64_t k) {
+        if (o + k > cap) return false;
+        memcpy(out + o, p, k);
+        o += k;
+        return true;
+    };
+    BufSource src;
+    src.p = in;
+    src.n = n;
+    HostIngestMemory M;
+    vcfc_ing::Config cfg;
+    cfg.chunk = chunk;
+    cfg.read_threads = read_threads;
+    int st = vcfc_ing::compress_stream(src, sink, M, nullptr, cfg, err_line);
+    *out_len = o;
+    return st;
+}

@@ -1,0 +1,108 @@
+"""Pipelined ingest on the CPU: the product pipeline
+(csrc/vcfc_ingest_driver.h: reader threads -> line index + encode -> writer)
+and its kernels (csrc/vcfc_ingest.hip, csrc/vcfc_encode.hip) compiled against
+the fiber SIMT emulator, with chunks of a few KiB so that lines straddle
+chunk boundaries.  Checked byte-exact against the reference's own compress
+outputs (tests/golden) and against the oracle (statuses, error lines, the
+output written before an error)."""
+import random
+
+import pytest
+
+import decode_cases as D
+import emu_io as E
+import golden_io as G
+
+OK, E_LT8COLS, E_8COLS, E_HEADER, E_ARG = 0, 1, 2, 3, 5
+
+
+def check(vcf, chunk, name=""):
+    st_o, want, el_o = G.oracle_compress(vcf)
+    st, got, el = E.emu_compress(vcf, chunk=chunk)
+    assert st == st_o, (name, chunk, st, st_o)
+    assert got == want, (name, chunk, len(got), len(want))
+    if st_o != OK:
+        assert el == el_o, (name, chunk, el, el_o)
+
+
+@pytest.mark.parametrize("chunk", [4096, 65536, 1 << 20])
+def test_reference_config1(chunk):
+    st, out, _ = E.emu_compress(G.gz("random_100x10000.vcf.gz"), chunk=chunk)
+    assert st == OK and out == G.gz("random_100x10000.vcfc.gz")
+
+
+def test_reference_edge_file_and_bad_header():
+    ec = G.edge_cases()
+    st, out, _ = E.emu_compress(bytes.fromhex(ec["file"]["input"]), chunk=4096)
+    assert st == OK and out.hex() == ec["file"]["output"]
+    check(bytes.fromhex(ec["bad_header_file"]["input"]), 4096, "bad_header_file")
+
+
+def mixed_file(rnd, n_rows, samples):
+    """Header, data rows, and the lines compress() treats specially: empty
+    lines, '##'/'#' lines between data rows, a final line without '\\n'."""
+    lines = [D.header(samples).rstrip(b"\n").split(b"\n")[0], D.header(samples).rstrip(b"\n").split(b"\n")[1]]
+    for r in D.rows(rnd, n_rows, samples, escapes=0.03):
+        lines.append(r)
+        x = rnd.random()
+        if x < 0.05:
+            lines.append(b"")
+        elif x < 0.08:
+            lines.append(b"##note=%d" % rnd.randrange(1000))
+        elif x < 0.10:
+            lines.append(b"#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\tS0")
+    return b"\n".join(lines) + (b"\n" if rnd.random() < 0.5 else b"")
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_mixed_files_match_oracle(seed):
+    rnd = random.Random(seed)
+    for samples in (1, 40, 300):
+        vcf = mixed_file(rnd, 60, samples)
+        for chunk in (1 << 12, 1 << 14, 1 << 20):
+            check(vcf, chunk, "mixed S=%d" % samples)
+
+
+@pytest.mark.parametrize("seed", [4, 5])
+def test_errors_match_oracle(seed):
+    """A failing line (data line with < 8 or exactly 8 columns, a '#' header
+    line with < 8 terms) in various chunks: output up to that line, its
+    status and line number."""
+    rnd = random.Random(seed)
+    base = mixed_file(rnd, 80, 50).split(b"\n")
+    bad = [b"1\t2\t3", b"1\t2\t3\t4\t5\t6\t7\t8", b"#CHROM\tPOS", b"#", b"1\t2\t3\t4\t5\t6\t7\t8\t9"]
+    for b in bad:
+        for at in (2, 5, 40, len(base) - 1):
+            lines = list(base)
+            lines.insert(at, b)
+            vcf = b"\n".join(lines)
+            for chunk in (1 << 12, 1 << 16):
+                check(vcf, chunk, "bad %r at %d" % (b, at))
+        # two failures: the first one wins
+        lines = list(base)
+        lines.insert(30, b"#CHROM")
+        lines.insert(10, b)
+        check(b"\n".join(lines), 1 << 12, "two failures")
+
+
+def test_empty_and_tiny_inputs():
+    for vcf in (b"", b"\n", b"\n\n\n", b"##x", b"##x\n", b"#", b"1\t2\t3\t4\t5\t6\t7\t8\t9",
+                b"1\t2\t3\t4\t5\t6\t7\t8\t9\t0|0\n\n", b"\r\n"):
+        for chunk in (4096, 1 << 16):
+            check(vcf, chunk, repr(vcf))
+
+
+def test_line_longer_than_chunk():
+    """The driver refuses (E_ARG) a line longer than its chunk; the C ABI then
+    reruns with the whole input as one chunk (vcfc_api.cpp)."""
+    vcf = D.header(2000) + b"\t".join([b"1", b"2", b"a", b"b", b"c", b"d", b"e", b"f", b"GT"] + [b"0|1"] * 2000) + b"\n"
+    st, out, _ = E.emu_compress(vcf, chunk=4096)
+    assert st == E_ARG
+    check(vcf, 1 << 16, "long line, larger chunk")
+
+
+@pytest.mark.parametrize("threads", [1, 3])
+def test_read_threads(threads):
+    vcf = G.gz("random_100x10000.vcf.gz")
+    st, out, _ = E.emu_compress(vcf, chunk=3 << 20, read_threads=threads)
+    assert st == OK and out == G.gz("random_100x10000.vcfc.gz")

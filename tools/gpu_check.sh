@@ -22,6 +22,8 @@ for s in $STEPS; do
     benchq) timeout -k 10 600 python bench.py --mode query > "$O/bench_query.json" 2> "$O/bench_query.err" || { echo "benchq failed"; tail -30 "$O/bench_query.err"; exit 1; } ; cat "$O/bench_query.json" ;;
     profq) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/profq" -o run -- python3 "$R/bench.py" --mode query --steps 10 --warmup 2 --no-cpu-baseline > "$O/profq.log" 2>&1) || { echo "profq failed rc=$?"; tail -30 "$O/profq.log"; exit 1; } ;;
     qtests) timeout -k 10 900 python -m pytest tests/test_gpu_query.py tests/test_gpu_decode.py -x -q -p no:cacheprovider > "$O/pytest_q.log" 2>&1 || { echo "qtests failed rc=$?"; tail -40 "$O/pytest_q.log"; exit 1; } ;;
+    benching) timeout -k 10 900 python bench.py --mode ingest --steps 3 --warmup 1 > "$O/bench_ingest.json" 2> "$O/bench_ingest.err" || { echo "benching failed"; tail -30 "$O/bench_ingest.err"; exit 1; } ; cat "$O/bench_ingest.json" ;;
+    itests) timeout -k 10 900 python -m pytest tests/test_gpu_encode.py -x -q -p no:cacheprovider > "$O/pytest_i.log" 2>&1 || { echo "itests failed rc=$?"; tail -40 "$O/pytest_i.log"; exit 1; } ;;
     profdec) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/profdec" -o run -- python3 "$R/bench.py" --mode decode --steps 10 --warmup 2 --no-cpu-baseline > "$O/profdec.log" 2>&1) || { echo "profdec failed rc=$?"; tail -30 "$O/profdec.log"; exit 1; } ;;
     pmcdec) for P in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" "FETCH_SIZE" "WRITE_SIZE" "GRBM_GUI_ACTIVE SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR"; do
            n=$(echo $P | cut -d' ' -f1)

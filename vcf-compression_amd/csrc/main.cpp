@@ -26,11 +26,17 @@ int main(int argc, char **argv) {
     std::string action(argv[1]);
     if (action == "compress") {
         if (argc < 4) return usage();
-        if (!file_exists(argv[2])) printf("Input file does not exist: %s\n", argv[2]);
+        const bool exists = file_exists(argv[2]);
+        if (!exists) printf("Input file does not exist: %s\n", argv[2]);
         if (std::string(argv[2]) == argv[3]) {
             fprintf(stderr, "terminate called after throwing an instance of 'std::runtime_error'\n"
                             "  what():  input and output file are the same\n");
             return 134;
+        }
+        if (!exists) {   // the reference's ifstream reads nothing: an empty output, exit 0
+            FILE *f = fopen(argv[3], "w");
+            if (f) fclose(f);
+            return 0;
         }
         vcfc_ctx *ctx = nullptr;
         int st = vcfc_ctx_create(0, &ctx);

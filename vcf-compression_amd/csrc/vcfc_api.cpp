@@ -19,6 +19,7 @@
 #include "vcfc.h"
 #include "vcfc_decode_driver.h"
 #include "vcfc_device.h"
+#include "vcfc_ingest_driver.h"
 
 hipError_t vcfc_sparse_plan_launch(const uint8_t *recs, const uint64_t *rec_off, uint64_t n, uint64_t data_start,
                                    uint64_t *file_off, uint8_t *prefix, uint64_t *status, hipStream_t s);
@@ -49,9 +50,25 @@ struct DevBuf {
     }
 };
 
-// Rows per device batch is bounded by bytes so a multi-GB file streams
-// through a fixed device footprint.
-constexpr uint64_t BATCH_BYTES = 1ull << 30;
+// Pinned host memory (the ingest pipeline's staging slots).
+struct HostBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap && p) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        hipError_t e = hipHostMalloc(&p, std::max<size_t>(bytes, 4096), hipHostMallocDefault);
+        if (e == hipSuccess) cap = std::max<size_t>(bytes, 4096);
+        return e;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
 
 }  // namespace
 
@@ -64,6 +81,8 @@ struct vcfc_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     DevBuf in, off, len, out, rec, ws, err, aux, flag, qref;
+    DevBuf ing_dev[vcfc_ing::Memory::N_DEV];
+    HostBuf ing_host[vcfc_ing::Memory::N_HOST];
 };
 
 namespace {
@@ -142,6 +161,53 @@ struct CtxDecodeBuffers : vcfc_dec::Buffers {
     }
 };
 
+// The ingest pipeline's buffers live in the context.
+struct CtxIngestMemory : vcfc_ing::Memory {
+    vcfc_ctx *c;
+    explicit CtxIngestMemory(vcfc_ctx *cc) : c(cc) {}
+    void *dev(int slot, uint64_t bytes) override {
+        DevBuf &b = c->ing_dev[slot];
+        return b.ensure(bytes) == hipSuccess ? b.p : nullptr;
+    }
+    void *host(int slot, uint64_t bytes) override {
+        HostBuf &b = c->ing_host[slot];
+        return b.ensure(bytes) == hipSuccess ? b.p : nullptr;
+    }
+};
+
+struct FdSource : vcfc_ing::Source {
+    int fd;
+    uint64_t n;
+    FdSource(int f, uint64_t size) : fd(f), n(size) {}
+    uint64_t size() const override { return n; }
+    bool read(uint8_t *dst, uint64_t off, uint64_t k) override {
+        while (k) {
+            const ssize_t r = pread(fd, dst, std::min<uint64_t>(k, 1ull << 30), (off_t)off);
+            if (r <= 0) return false;
+            dst += r; off += (uint64_t)r; k -= (uint64_t)r;
+        }
+        return true;
+    }
+};
+
+struct MemSource : vcfc_ing::Source {
+    const uint8_t *p;
+    uint64_t n;
+    MemSource(const uint8_t *b, uint64_t size) : p(b), n(size) {}
+    uint64_t size() const override { return n; }
+    bool read(uint8_t *dst, uint64_t off, uint64_t k) override {
+        memcpy(dst, p + off, k);
+        return true;
+    }
+};
+
+// chunk size: 128 MiB, or the whole input when smaller
+vcfc_ing::Config ingest_config(uint64_t n) {
+    vcfc_ing::Config cfg;
+    cfg.chunk = std::min<uint64_t>(128ull << 20, std::max<uint64_t>((n + 4095) & ~4095ull, 4096));
+    return cfg;
+}
+
 }  // namespace
 
 extern "C" {
@@ -185,12 +251,14 @@ void vcfc_ctx_destroy(vcfc_ctx *c) {
     c->in.release(); c->off.release(); c->len.release(); c->out.release();
     c->rec.release(); c->ws.release(); c->err.release(); c->aux.release();
     c->flag.release(); c->qref.release();
+    for (auto &b : c->ing_dev) b.release();
+    for (auto &b : c->ing_host) b.release();
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
 
 uint64_t vcfc_encode_bound(uint64_t n_rows, uint64_t total_line_bytes) {
-    return total_line_bytes + total_line_bytes / 2 + 16 * n_rows + 16;
+    return vcfc_record_bound(n_rows, total_line_bytes);
 }
 
 uint64_t vcfc_encode_workspace_size(uint64_t n_rows, uint64_t total_line_bytes) {
@@ -449,138 +517,70 @@ int vcfc_sparsify_file(vcfc_ctx *c, const char *in_path, const char *out_path) {
 
 uint64_t vcfc_compress_bound(uint64_t in_bytes) { return in_bytes + in_bytes / 2 + 64; }
 
-// compress() over an in-memory file (reference src/compress.cpp:205-257).
+// compress() (reference src/compress.cpp:205-257) through the pipelined
+// ingest (csrc/vcfc_ingest_driver.h: reader threads -> GPU line index +
+// encode -> writer thread).
 int vcfc_compress_buffer(vcfc_ctx *c, const uint8_t *in, uint64_t n, uint8_t *out, uint64_t out_cap,
                          uint64_t *out_len, int64_t *err_line) {
     if (!c || (!in && n) || !out || !out_len) return VCFC_E_ARG;
     if (err_line) *err_line = -1;
     *out_len = 0;
-    struct Pass { uint64_t before_data, off, len, lineno; };
-    std::vector<Pass> pass;           // non-data lines, with the data index they precede
-    std::vector<uint64_t> doff, dline;
-    std::vector<uint32_t> dlen;
-    int64_t hdr_err_line = -1;
-    uint64_t p = 0, lineno = 0;
-    while (p < n) {
-        const uint8_t *nl = static_cast<const uint8_t *>(memchr(in + p, '\n', n - p));
-        const uint64_t e = nl ? (uint64_t)(nl - in) : n;
-        const uint64_t len = e - p;
-        lineno++;
-        if (len > 0) {
-            if (in[p] == '#') {
-                if (!(len >= 2 && in[p + 1] == '#')) {
-                    // header line: >= 8 tab-separated non-empty terms (:230-234)
-                    uint64_t terms = 0, q = p;
-                    while (q < e) {
-                        while (q < e && in[q] == '\t') q++;
-                        if (q >= e) break;
-                        terms++;
-                        while (q < e && in[q] != '\t') q++;
-                    }
-                    if (terms < 8) { hdr_err_line = (int64_t)lineno; break; }
-                }
-                pass.push_back({doff.size(), p, len, lineno});
-            } else {
-                if (len > 0xFFFFFFFFull) return VCFC_E_ARG;
-                doff.push_back(p);
-                dlen.push_back((uint32_t)len);
-                dline.push_back(lineno);
-            }
-        }
-        p = nl ? e + 1 : n;
-    }
-    const uint64_t nd = doff.size();
+    if (hipSetDevice(c->device) != hipSuccess) return VCFC_E_HIP;
     uint64_t o = 0;
-    size_t pi = 0;
-    auto emit_pass_upto = [&](uint64_t d) -> int {
-        while (pi < pass.size() && pass[pi].before_data <= d) {
-            if (o + pass[pi].len + 1 > out_cap) return VCFC_E_NOSPACE;
-            memcpy(out + o, in + pass[pi].off, pass[pi].len);
-            o += pass[pi].len;
-            out[o++] = '\n';
-            pi++;
-        }
-        return VCFC_OK;
+    bool full = false;
+    auto sink = [&](const uint8_t *p, uint64_t k) {
+        if (o + k > out_cap) { full = true; return false; }
+        memcpy(out + o, p, k);
+        o += k;
+        return true;
     };
-    std::vector<uint64_t> rec;
-    std::vector<uint8_t> recbuf;
-    uint64_t d = 0;
-    while (d < nd) {
-        // batch [d, e): contiguous input span bounded by BATCH_BYTES
-        uint64_t e = d, bytes = 0;
-        while (e < nd && (e == d || bytes + dlen[e] + 1 <= BATCH_BYTES)) { bytes += dlen[e] + 1; e++; }
-        const uint64_t base = doff[d];
-        const uint64_t span = doff[e - 1] + dlen[e - 1] - base;
-        std::vector<uint64_t> lo(e - d);
-        for (uint64_t i = d; i < e; i++) lo[i - d] = doff[i] - base;
-        rec.assign(e - d + 1, 0);
-        recbuf.resize(vcfc_encode_bound(e - d, bytes) + 16);
-        int64_t er = -1;
-        int st = vcfc_encode_rows(c, in + base, span, lo.data(), dlen.data() + d, e - d, recbuf.data(), recbuf.size(),
-                                  rec.data(), &er);
-        const uint64_t good = st == VCFC_OK ? e - d : (er >= 0 ? (uint64_t)er : 0);
-        // interleave pass-through lines at their positions
-        uint64_t a = 0;
-        while (a < good) {
-            int s2 = emit_pass_upto(d + a);
-            if (s2) return s2;
-            uint64_t b = a + 1;
-            while (b < good && !(pi < pass.size() && pass[pi].before_data <= d + b)) b++;
-            const uint64_t nb = rec[b] - rec[a];
-            if (o + nb > out_cap) return VCFC_E_NOSPACE;
-            memcpy(out + o, recbuf.data() + rec[a], nb);
-            o += nb;
-            a = b;
-        }
-        if (st != VCFC_OK) {
-            const int64_t bad_line = er >= 0 ? (int64_t)dline[d + er] : -1;
-            if (hdr_err_line >= 0 && hdr_err_line < bad_line) break;  // header error comes first
-            int s2 = emit_pass_upto(d + good);
-            if (s2) return s2;
-            *out_len = o;
-            if (err_line) *err_line = bad_line;
-            return st;
-        }
-        d = e;
+    MemSource src(in, n);
+    CtxIngestMemory M(c);
+    vcfc_ing::Config cfg = ingest_config(n);
+    int st = vcfc_ing::compress_stream(src, sink, M, c->stream, cfg, err_line);
+    if (st == VCFC_E_ARG && !full) {   // a line longer than a chunk: the whole input as one chunk
+        o = 0;
+        cfg.chunk = n + 4096;
+        st = vcfc_ing::compress_stream(src, sink, M, c->stream, cfg, err_line);
     }
-    int s2 = emit_pass_upto(nd);
-    if (s2) return s2;
     *out_len = o;
-    if (hdr_err_line >= 0) {
-        if (err_line) *err_line = hdr_err_line;
-        return VCFC_E_HEADER;
-    }
-    return VCFC_OK;
+    if (full) return VCFC_E_NOSPACE;
+    return st;
 }
 
 int vcfc_compress_file(vcfc_ctx *c, const char *in_path, const char *out_path, int64_t *err_line) {
     if (!c || !in_path || !out_path) return VCFC_E_ARG;
+    if (err_line) *err_line = -1;
+    if (hipSetDevice(c->device) != hipSuccess) return VCFC_E_HIP;
     int fd = open(in_path, O_RDONLY);
     if (fd < 0) return VCFC_E_IO;
     struct stat st;
     if (fstat(fd, &st) != 0) { close(fd); return VCFC_E_IO; }
     const uint64_t n = (uint64_t)st.st_size;
-    const uint8_t *in = nullptr;
-    if (n) {
-        void *m = mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fd, 0);
-        if (m == MAP_FAILED) { close(fd); return VCFC_E_IO; }
-        madvise(m, n, MADV_SEQUENTIAL);
-        in = static_cast<const uint8_t *>(m);
-    }
-    std::vector<uint8_t> out(vcfc_compress_bound(n));
-    uint64_t olen = 0;
-    int s = vcfc_compress_buffer(c, in, n, out.data(), out.size(), &olen, err_line);
-    if (n) munmap(const_cast<uint8_t *>(in), n);
-    close(fd);
+    posix_fadvise(fd, 0, 0, POSIX_FADV_SEQUENTIAL);
+    // the reference opens (truncates) the output before reading the input
     int ofd = open(out_path, O_CREAT | O_TRUNC | O_WRONLY, 0644);
-    if (ofd < 0) return VCFC_E_IO;
-    uint64_t w = 0;
-    while (w < olen) {
-        ssize_t k = write(ofd, out.data() + w, std::min<uint64_t>(olen - w, 1ull << 30));
-        if (k <= 0) { close(ofd); return VCFC_E_IO; }
-        w += (uint64_t)k;
+    if (ofd < 0) { close(fd); return VCFC_E_IO; }
+    auto sink = [&](const uint8_t *p, uint64_t k) {
+        while (k) {
+            const ssize_t w = write(ofd, p, std::min<uint64_t>(k, 1ull << 30));
+            if (w <= 0) return false;
+            p += w;
+            k -= (uint64_t)w;
+        }
+        return true;
+    };
+    FdSource src(fd, n);
+    CtxIngestMemory M(c);
+    vcfc_ing::Config cfg = ingest_config(n);
+    int s = vcfc_ing::compress_stream(src, sink, M, c->stream, cfg, err_line);
+    if (s == VCFC_E_ARG) {   // a line longer than a chunk: start over with the whole input as one chunk
+        if (ftruncate(ofd, 0) != 0 || lseek(ofd, 0, SEEK_SET) != 0) { close(fd); close(ofd); return VCFC_E_IO; }
+        cfg.chunk = n + 4096;
+        s = vcfc_ing::compress_stream(src, sink, M, c->stream, cfg, err_line);
     }
-    close(ofd);
+    close(fd);
+    if (close(ofd) != 0 && s == VCFC_OK) s = VCFC_E_IO;
     return s;
 }
 

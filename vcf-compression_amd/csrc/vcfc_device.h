@@ -45,6 +45,12 @@ __host__ __device__ inline uint64_t vcfc_slot_bytes(uint32_t len) {
     return ((uint64_t)len + (len >> 1) + 48 + 15) & ~15ull;
 }
 
+// Upper bound of the records of n rows whose line bytes sum to total
+// (include/vcfc.h vcfc_encode_bound).
+__host__ __device__ inline uint64_t vcfc_record_bound(uint64_t n, uint64_t total) {
+    return total + total / 2 + 16 * n + 16;
+}
+
 // Workspace layout for n rows whose line lengths sum to <= total_line_bytes.
 VcfcWorkspaceLayout vcfc_encode_workspace_layout(uint64_t n, uint64_t total_line_bytes);
 
@@ -114,3 +120,28 @@ hipError_t vcfc_query_match(const uint8_t *in, const uint64_t *rec_start, uint64
 // one-lane byte-serial query of in[p, n) (st as vcfc_decode_stream)
 hipError_t vcfc_query_stream(const uint8_t *in, uint64_t n, uint64_t p, uint64_t S, const VcfcQuery &q, uint8_t *out,
                              uint64_t *st, hipStream_t s);
+
+// ---------------------------------------------------------------------------
+// Line index of an input chunk (vcfc_ingest.hip; reference compress()'s
+// getline loop, src/compress.cpp:218-238).
+struct VcfcLineIndex {
+    uint64_t *line_off;     // data line j: chunk offset, length, 0-based line number in the chunk
+    uint32_t *line_len;
+    uint32_t *line_no;
+    uint32_t *pass_off;     // '#' line q: chunk offset, length, line number, data lines before it
+    uint32_t *pass_len;
+    uint32_t *pass_no;
+    uint64_t *pass_before;
+    uint64_t *counts;       // {lines, data lines, pass lines}
+};
+struct VcfcLineIndexLayout {
+    uint64_t seg_cnt, seg_base, nl, partials1, total1;               // phase 1 workspace
+    uint64_t is_data, is_pass, data_rank, pass_rank, partials2, total2;   // phase 2 workspace
+};
+VcfcLineIndexLayout vcfc_line_index_layout(uint64_t chunk_bytes, uint64_t n_lines);
+// phase 1: '\n' positions of buf[0, n) (last byte '\n'); counts[0] = lines
+hipError_t vcfc_line_index(const uint8_t *buf, uint64_t n, uint8_t *ws, const VcfcLineIndexLayout &L,
+                           const VcfcLineIndex &x, hipStream_t s);
+// phase 2 (n_lines = counts[0]): data / pass line arrays; counts[1], counts[2]
+hipError_t vcfc_line_index_place(const uint8_t *buf, uint64_t n_lines, const uint8_t *ws1, uint8_t *ws2,
+                                 const VcfcLineIndexLayout &L, const VcfcLineIndex &x, hipStream_t s);

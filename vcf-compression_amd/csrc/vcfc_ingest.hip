@@ -1,0 +1,180 @@
+// vcfc_ingest.hip -- GPU line index of an input chunk (the
+// device counterpart of compress()'s getline loop, reference
+// src/compress.cpp:218-238).
+//
+// A chunk is a run of whole lines resident in HBM (every line ends with
+// '\n'; the host appends one after an unterminated last line of the file, as
+// getline still returns it).  The index gives, in line order:
+//   data lines   (non-empty, first byte not '#'): offset, length, line number
+//                -- exactly the encoder's input arrays;
+//   pass lines   (first byte '#'): offset, length, line number and the count
+//                of data lines before it (where it sits in the output);
+// empty lines are skipped (compress.cpp:219-221) but still counted.
+//
+//   k_nl_count    one wave per 16 KiB segment: '\n' count
+//   scan          segment bases (the encoder's exclusive scan)
+//   k_nl_emit     one wave per segment: '\n' positions in order (ballot-free:
+//                 per-lane masks, a wave prefix sum of their popcounts)
+//   k_line_kind   one lane per line: data / pass flags
+//   scan x2       data and pass ranks
+//   k_line_place  one lane per line: scatter into the output arrays
+#include <hip/hip_runtime.h>
+#include <vcfc_wave.h>   // angle brackets: tests/simt_emu shadows it
+#include "vcfc_device.h"
+
+namespace {
+
+constexpr uint32_t SEG = 16384;          // bytes per wave
+constexpr uint32_t WIN = 1024;           // bytes per wave step (16 per lane)
+constexpr uint32_t IX_WAVES = 4;
+
+// bit j: byte j of x is '\n' (exact per byte)
+__device__ __forceinline__ uint32_t nl_bits(uint32_t x) {
+    const uint32_t t = x ^ 0x0A0A0A0Au;
+    const uint32_t z = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t | 0x7F7F7F7Fu);
+    return ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
+}
+
+// 16-bit '\n' mask of bytes [p, p + 16) (bytes at or past n count as none)
+__device__ __forceinline__ uint32_t nl_mask16(const uint8_t *buf, uint64_t n, uint64_t p) {
+    if (p + 16 <= n) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(buf + p);
+        return nl_bits(v.x) | nl_bits(v.y) << 4 | nl_bits(v.z) << 8 | nl_bits(v.w) << 12;
+    }
+    uint32_t m = 0;
+    for (uint32_t j = 0; j < 16 && p + j < n; j++) m |= (buf[p + j] == '\n' ? 1u : 0u) << j;
+    return m;
+}
+
+__global__ __launch_bounds__(256) void k_nl_count(const uint8_t *buf, uint64_t n, uint64_t n_seg, uint32_t *seg_cnt) {
+    const uint64_t seg = (uint64_t)blockIdx.x * IX_WAVES + vw::readfirst(threadIdx.x >> 6);
+    if (seg >= n_seg) return;
+    const uint32_t l = vw::lane_id();
+    uint32_t c = 0;
+    for (uint32_t w = 0; w < SEG; w += WIN) c += __builtin_popcount(nl_mask16(buf, n, seg * SEG + w + 16 * l));
+    c = vw::scan_add(c);
+    if (l == 63) seg_cnt[seg] = c;
+}
+
+__global__ __launch_bounds__(256) void k_nl_emit(const uint8_t *buf, uint64_t n, uint64_t n_seg, const uint64_t *seg_base,
+                                                 uint32_t *nl) {
+    const uint64_t seg = (uint64_t)blockIdx.x * IX_WAVES + vw::readfirst(threadIdx.x >> 6);
+    if (seg >= n_seg) return;
+    const uint32_t l = vw::lane_id();
+    uint64_t base = seg_base[seg];
+    for (uint32_t w = 0; w < SEG; w += WIN) {
+        const uint64_t p = seg * SEG + w + 16 * l;
+        uint32_t m = nl_mask16(buf, n, p);
+        const uint32_t c = __builtin_popcount(m);
+        const uint32_t inc = vw::scan_add(c);
+        uint64_t o = base + inc - c;
+        while (m) {
+            nl[o++] = (uint32_t)(p + __builtin_ctz(m));
+            m &= m - 1;
+        }
+        base += vw::readlane(inc, 63);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_line_kind(const uint8_t *buf, const uint32_t *nl, uint64_t n_lines,
+                                                   uint32_t *is_data, uint32_t *is_pass) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_lines) return;
+    const uint32_t s = i ? nl[i - 1] + 1 : 0u;
+    const bool nonempty = nl[i] > s;
+    const bool hash = nonempty && buf[s] == '#';
+    is_data[i] = nonempty && !hash;
+    is_pass[i] = hash;
+}
+
+__global__ __launch_bounds__(256) void k_line_place(const uint32_t *nl, uint64_t n_lines, const uint64_t *data_rank,
+                                                    const uint64_t *pass_rank, VcfcLineIndex x) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_lines) return;
+    const uint32_t s = i ? nl[i - 1] + 1 : 0u;
+    const uint64_t d = data_rank[i];
+    if (data_rank[i + 1] > d) {
+        x.line_off[d] = s;
+        x.line_len[d] = nl[i] - s;
+        x.line_no[d] = (uint32_t)i;
+    }
+    const uint64_t q = pass_rank[i];
+    if (pass_rank[i + 1] > q) {
+        x.pass_off[q] = s;
+        x.pass_len[q] = nl[i] - s;
+        x.pass_no[q] = (uint32_t)i;
+        x.pass_before[q] = d;
+    }
+}
+
+}  // namespace
+
+// Phase 1 workspace depends on the chunk size only (every byte may be a
+// '\n'); phase 2 on the line count phase 1 found.
+VcfcLineIndexLayout vcfc_line_index_layout(uint64_t chunk_bytes, uint64_t n_lines) {
+    auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
+    const uint64_t lines = chunk_bytes + 1;
+    const uint64_t seg = (chunk_bytes + SEG - 1) / SEG + 1;
+    VcfcLineIndexLayout L;
+    uint64_t o = 0;
+    L.seg_cnt = o; o = al(o + 4 * seg);
+    L.seg_base = o; o = al(o + 8 * (seg + 1));
+    L.nl = o; o = al(o + 4 * lines);
+    L.partials1 = o; o = al(o + 8 * ((seg + 4095) / 4096 + 1));
+    L.total1 = o;
+    o = 0;
+    L.is_data = o; o = al(o + 4 * (n_lines + 1));
+    L.is_pass = o; o = al(o + 4 * (n_lines + 1));
+    L.data_rank = o; o = al(o + 8 * (n_lines + 1));
+    L.pass_rank = o; o = al(o + 8 * (n_lines + 1));
+    L.partials2 = o; o = al(o + 8 * ((n_lines + 4095) / 4096 + 1));
+    L.total2 = o;
+    return L;
+}
+
+// Phase 1: '\n' positions of buf[0, n) (n <= chunk_bytes of the layout; the
+// last byte must be '\n'); x.counts[0] = lines.  Phase 2 needs that count on
+// the host (its grids), as the encoder needs the data line count.  The
+// output arrays of `x` hold up to n / 2 data lines (a data line has at least
+// one byte and its '\n') and n pass lines.
+hipError_t vcfc_line_index(const uint8_t *buf, uint64_t n, uint8_t *ws, const VcfcLineIndexLayout &L,
+                           const VcfcLineIndex &x, hipStream_t s) {
+    // ws: phase 1 workspace (L.total1 bytes)
+    uint32_t *seg_cnt = reinterpret_cast<uint32_t *>(ws + L.seg_cnt);
+    uint64_t *seg_base = reinterpret_cast<uint64_t *>(ws + L.seg_base);
+    uint32_t *nl = reinterpret_cast<uint32_t *>(ws + L.nl);
+    uint64_t *partials = reinterpret_cast<uint64_t *>(ws + L.partials1);
+    hipError_t e;
+    if (n == 0) return hipMemsetAsync(x.counts, 0, 24, s);
+    const uint64_t n_seg = (n + SEG - 1) / SEG;
+    const dim3 sg((unsigned)((n_seg + IX_WAVES - 1) / IX_WAVES)), blk(64 * IX_WAVES);
+    hipLaunchKernelGGL(k_nl_count, sg, blk, 0, s, buf, n, n_seg, seg_cnt);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = vcfc_scan_u32(seg_cnt, n_seg, partials, seg_base, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_nl_emit, sg, blk, 0, s, buf, n, n_seg, seg_base, nl);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    return hipMemcpyAsync(x.counts, seg_base + n_seg, 8, hipMemcpyDeviceToDevice, s);
+}
+
+// Phase 2, once the host knows the line count (counts[0]); ws1 = phase 1's
+// workspace, ws2 = L.total2 bytes for vcfc_line_index_layout(chunk, n_lines).
+hipError_t vcfc_line_index_place(const uint8_t *buf, uint64_t n_lines, const uint8_t *ws1, uint8_t *ws2,
+                                 const VcfcLineIndexLayout &L, const VcfcLineIndex &x, hipStream_t s) {
+    const uint32_t *nl = reinterpret_cast<const uint32_t *>(ws1 + L.nl);
+    uint32_t *is_data = reinterpret_cast<uint32_t *>(ws2 + L.is_data);
+    uint32_t *is_pass = reinterpret_cast<uint32_t *>(ws2 + L.is_pass);
+    uint64_t *data_rank = reinterpret_cast<uint64_t *>(ws2 + L.data_rank);
+    uint64_t *pass_rank = reinterpret_cast<uint64_t *>(ws2 + L.pass_rank);
+    uint64_t *partials = reinterpret_cast<uint64_t *>(ws2 + L.partials2);
+    hipError_t e;
+    if (n_lines == 0) return hipMemsetAsync(x.counts + 1, 0, 16, s);
+    const dim3 g((unsigned)((n_lines + 255) / 256)), blk(256);
+    hipLaunchKernelGGL(k_line_kind, g, blk, 0, s, buf, nl, n_lines, is_data, is_pass);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = vcfc_scan_u32(is_data, n_lines, partials, data_rank, s)) != hipSuccess) return e;
+    if ((e = vcfc_scan_u32(is_pass, n_lines, partials, pass_rank, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_line_place, g, blk, 0, s, nl, n_lines, data_rank, pass_rank, x);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(x.counts + 1, data_rank + n_lines, 8, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
+    return hipMemcpyAsync(x.counts + 2, pass_rank + n_lines, 8, hipMemcpyDeviceToDevice, s);
+}

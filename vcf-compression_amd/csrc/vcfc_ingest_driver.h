@@ -1,0 +1,410 @@
+// vcfc_ingest_driver.h -- pipelined compress(), shared by
+// the C ABI (vcfc_api.cpp) and the CPU emulator harness
+// (tests/simt_emu/emu_api.cpp), so the same control flow is tested on both.
+//
+// Reference: compress() (src/compress.cpp:205-257) reads the VCF with
+// getline, copies '#' lines through with '\n', skips empty lines, encodes
+// data lines with compress_data_line and stops at the first line that
+// throws.  Here three stages run concurrently on fixed-size chunks of whole
+// lines:
+//
+//   reader  (host threads)  the input in chunks of up to `chunk` bytes into
+//                           pinned host slots; the partial line at a chunk's
+//                           end is carried to the next chunk;
+//   GPU     (calling thread) H2D -> line index (vcfc_ingest.hip) -> encode
+//                           (vcfc_encode.hip) -> D2H of the records, the
+//                           '#' lines checked on the host (>= 8 terms);
+//   writer  (host thread)   records with the '#' lines interleaved at their
+//                           places, in input order.
+//
+// The output equals the reference's up to the first failing line; that
+// line's status and 1-based number are returned.
+#pragma once
+#include <chrono>
+#include <condition_variable>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "vcfc_device.h"
+
+namespace vcfc_ing {
+
+// = include/vcfc.h codes
+constexpr int ST_OK = 0, ST_E_LT8COLS = 1, ST_E_8COLS = 2, ST_E_HEADER = 3, ST_E_NOSPACE = 4, ST_E_ARG = 5,
+              ST_E_HIP = 6, ST_E_IO = 7;
+
+// Input bytes [off, off + n) into dst; must be safe to call from several
+// threads at once.  false = I/O error.
+struct Source {
+    virtual ~Source() {}
+    virtual uint64_t size() const = 0;
+    virtual bool read(uint8_t *dst, uint64_t off, uint64_t n) = 0;
+};
+// In-order output; false = I/O error (or no space).
+using Sink = std::function<bool(const uint8_t *, uint64_t)>;
+
+// Device and pinned host buffers, owned by the caller; contents not kept
+// between calls.
+struct Memory {
+    virtual ~Memory() {}
+    enum { D_IN = 0, D_IX1, D_IX2, D_LINES, D_ENC_WS, D_OUT, D_REC, D_SMALL, N_DEV };
+    enum { H_IN0 = 0, H_IN1, H_IN2, H_OUT0, H_OUT1, H_SMALL, N_HOST };
+    virtual void *dev(int slot, uint64_t bytes) = 0;    // nullptr on failure
+    virtual void *host(int slot, uint64_t bytes) = 0;   // pinned; nullptr on failure
+};
+
+struct Config {
+    uint64_t chunk = 256ull << 20;   // input bytes per chunk (lines must be shorter)
+    int read_threads = 4;
+};
+
+// compress()'s header-line check (src/compress.cpp:230-235): split_string
+// drops empty terms (src/utils.cpp:82-116), and fewer than 8 throw.
+inline bool header_ok(const uint8_t *p, uint64_t len) {
+    uint64_t terms = 0, q = 0;
+    while (q < len) {
+        while (q < len && p[q] == '\t') q++;
+        if (q >= len) break;
+        terms++;
+        while (q < len && p[q] != '\t') q++;
+    }
+    return terms >= 8;
+}
+
+namespace detail {
+
+inline double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+template <class T>
+struct Queue {   // bounded hand-off between the stages
+    std::mutex m;
+    std::condition_variable cv;
+    std::deque<T> q;
+    bool closed = false;
+    void put(T v) {
+        std::lock_guard<std::mutex> g(m);
+        q.push_back(std::move(v));
+        cv.notify_all();
+    }
+    bool get(T &v) {   // false once closed and empty
+        std::unique_lock<std::mutex> g(m);
+        cv.wait(g, [&] { return !q.empty() || closed; });
+        if (q.empty()) return false;
+        v = std::move(q.front());
+        q.pop_front();
+        return true;
+    }
+    void close() {
+        std::lock_guard<std::mutex> g(m);
+        closed = true;
+        cv.notify_all();
+    }
+};
+
+struct InChunk {
+    int slot = -1;
+    uint64_t bytes = 0;   // whole lines, the last one ending with '\n'
+    bool ok = true;       // false: read error, or a line longer than a chunk
+    bool long_line = false;
+};
+
+struct PassLine {
+    uint64_t before;   // data lines of the chunk before it
+    uint32_t no;       // line number in the chunk
+    std::vector<uint8_t> text;
+};
+
+struct OutChunk {
+    int slot = -1;
+    uint64_t rec_bytes = 0;               // records of the good rows
+    std::vector<uint64_t> rec_off;        // only when pass lines are interleaved
+    std::vector<PassLine> pass;           // the ones to write
+    bool last = false;
+};
+
+}  // namespace detail
+
+// Compress `src` into `sink`.  *err_line = 1-based line of the failing line
+// (-1 if none).  ST_E_ARG: a line longer than cfg.chunk (the lines before it
+// may have been written; the caller restarts with a larger chunk).
+inline int compress_stream(Source &src, const Sink &sink, Memory &M, hipStream_t s, const Config &cfg,
+                           int64_t *err_line) {
+    using namespace detail;
+    if (err_line) *err_line = -1;
+    const uint64_t N = src.size();
+    const uint64_t C = cfg.chunk;
+    const uint64_t CX = C + 16;   // a chunk may gain the '\n' after an unterminated last line
+    if (N == 0) return ST_OK;
+    uint8_t *hin[3];
+    for (int k = 0; k < 3; k++)
+        if (!(hin[k] = static_cast<uint8_t *>(M.host(Memory::H_IN0 + k, CX + 64)))) return ST_E_HIP;
+    uint8_t *hout[2];
+    const uint64_t out_cap = vcfc_record_bound(CX / 2 + 1, CX) + 64;
+    for (int k = 0; k < 2; k++)
+        if (!(hout[k] = static_cast<uint8_t *>(M.host(Memory::H_OUT0 + k, out_cap)))) return ST_E_HIP;
+    uint64_t *hsmall = static_cast<uint64_t *>(M.host(Memory::H_SMALL, 64));
+    uint8_t *d_in = static_cast<uint8_t *>(M.dev(Memory::D_IN, CX + 64));
+    const VcfcLineIndexLayout L1 = vcfc_line_index_layout(CX, 0);
+    uint8_t *d_ix1 = static_cast<uint8_t *>(M.dev(Memory::D_IX1, L1.total1));
+    uint64_t *d_small = static_cast<uint64_t *>(M.dev(Memory::D_SMALL, 64));
+    if (!hsmall || !d_in || !d_ix1 || !d_small) return ST_E_HIP;
+
+    // ---- reader ------------------------------------------------------------
+    Queue<InChunk> filled;
+    Queue<int> free_in;
+    for (int k = 0; k < 3; k++) free_in.put(k);
+    std::vector<uint8_t> carry;
+    const bool trace = getenv("VCFC_INGEST_TRACE") != nullptr;
+    double t_read = 0, t_gpu = 0, t_write = 0, t_wait_in = 0, t_wait_out = 0;
+    const double t_begin = now_s();
+    std::thread reader([&] {
+        uint64_t pos = 0;
+        while (pos < N) {
+            int slot;
+            if (!free_in.get(slot)) break;
+            uint8_t *b = hin[slot];
+            InChunk ch;
+            ch.slot = slot;
+            const uint64_t c0 = carry.size();
+            if (c0) memcpy(b, carry.data(), c0);
+            const uint64_t want = std::min<uint64_t>(C - c0, N - pos);
+            // parallel reads of [pos, pos + want)
+            const int T = want >= (1u << 20) ? std::max(1, cfg.read_threads) : 1;
+            std::vector<std::thread> ts;
+            std::vector<char> ok(T, 1);
+            const uint64_t per = (want + T - 1) / T;
+            for (int t = 0; t < T; t++) {
+                const uint64_t a = t * per, e = std::min(want, a + per);
+                if (a >= e) continue;
+                ts.emplace_back([&, t, a, e] { ok[t] = src.read(b + c0 + a, pos + a, e - a) ? 1 : 0; });
+            }
+            const double r0 = now_s();
+            for (auto &t : ts) t.join();
+            t_read += now_s() - r0;
+            for (char o : ok) ch.ok = ch.ok && o;
+            pos += want;
+            uint64_t total = c0 + want;
+            carry.clear();
+            if (pos >= N) {
+                if (total && b[total - 1] != '\n') b[total++] = '\n';   // getline returns an unterminated last line
+                ch.bytes = total;
+            } else {
+                const uint8_t *nl = static_cast<const uint8_t *>(memrchr(b, '\n', total));
+                if (!nl) {   // a line longer than a chunk
+                    ch.ok = false;
+                    ch.long_line = true;
+                } else {
+                    ch.bytes = (uint64_t)(nl - b) + 1;
+                    carry.assign(b + ch.bytes, b + total);
+                }
+            }
+            filled.put(ch);
+            if (!ch.ok) break;
+        }
+        filled.close();
+    });
+
+    // ---- writer ------------------------------------------------------------
+    Queue<OutChunk> to_write;
+    Queue<int> free_out;
+    free_out.put(0);
+    free_out.put(1);
+    bool write_failed = false;
+    std::thread writer([&] {
+        OutChunk oc;
+        while (to_write.get(oc)) {
+            const uint8_t *r = hout[oc.slot];
+            const double w0 = now_s();
+            if (!write_failed) {
+                if (oc.pass.empty()) {
+                    if (oc.rec_bytes && !sink(r, oc.rec_bytes)) write_failed = true;
+                } else {
+                    uint64_t at = 0;   // records written so far
+                    for (const PassLine &p : oc.pass) {
+                        const uint64_t upto = oc.rec_off[p.before];
+                        if (upto > at && !sink(r + at, upto - at)) { write_failed = true; break; }
+                        at = std::max(at, upto);
+                        if (!sink(p.text.data(), p.text.size())) { write_failed = true; break; }
+                    }
+                    if (!write_failed && oc.rec_bytes > at && !sink(r + at, oc.rec_bytes - at)) write_failed = true;
+                }
+            }
+            t_write += now_s() - w0;
+            free_out.put(oc.slot);
+        }
+    });
+
+    // ---- GPU stage (this thread) --------------------------------------------
+    int status = ST_OK;
+    uint64_t line_base = 0;   // lines of the chunks before
+    auto finish = [&](int st) {
+        status = st;
+        free_in.close();
+        to_write.close();
+        reader.join();
+        writer.join();
+        if (status == ST_OK && write_failed) status = ST_E_IO;
+        if (trace)
+            fprintf(stderr, "vcfc ingest: %.3f s total; read %.3f s, gpu stage %.3f s (waiting for input %.3f s, "
+                            "for an output slot %.3f s), write %.3f s\n",
+                    now_s() - t_begin, t_read, t_gpu, t_wait_in, t_wait_out, t_write);
+        return status;
+    };
+    auto sync = [&]() { return hipStreamSynchronize(s) == hipSuccess; };
+    InChunk ch;
+    for (;;) {
+        double g0 = now_s();
+        if (!filled.get(ch)) break;
+        t_wait_in += now_s() - g0;
+        g0 = now_s();
+        struct Acc {
+            double &t, g;
+            ~Acc() { t += now_s() - g; }
+        } acc{t_gpu, g0};
+        if (!ch.ok) return finish(ch.long_line ? ST_E_ARG : ST_E_IO);
+        const uint64_t n = ch.bytes;
+        const uint8_t *h = hin[ch.slot];
+        VcfcLineIndex x;
+        x.counts = d_small;
+        // phase 1: '\n' positions
+        if (hipMemcpyAsync(d_in, h, n, hipMemcpyHostToDevice, s) != hipSuccess ||
+            vcfc_line_index(d_in, n, d_ix1, L1, x, s) != hipSuccess ||
+            hipMemcpyAsync(hsmall, d_small, 8, hipMemcpyDeviceToHost, s) != hipSuccess || !sync())
+            return finish(ST_E_HIP);
+        const uint64_t n_lines = hsmall[0];
+        // phase 2: data and '#' lines
+        const VcfcLineIndexLayout L = vcfc_line_index_layout(CX, n_lines);
+        const uint64_t max_data = n_lines;
+        uint8_t *d_ix2 = static_cast<uint8_t *>(M.dev(Memory::D_IX2, L.total2));
+        uint8_t *d_lines = static_cast<uint8_t *>(M.dev(Memory::D_LINES, 32 * (max_data + 1)));
+        if (!d_ix2 || !d_lines) return finish(ST_E_HIP);
+        uint8_t *q = d_lines;
+        x.line_off = reinterpret_cast<uint64_t *>(q); q += 8 * (max_data + 1);
+        x.pass_before = reinterpret_cast<uint64_t *>(q); q += 8 * (max_data + 1);
+        x.line_len = reinterpret_cast<uint32_t *>(q); q += 4 * (max_data + 1);
+        x.line_no = reinterpret_cast<uint32_t *>(q); q += 4 * (max_data + 1);
+        std::vector<uint32_t> pass_off, pass_len, pass_no;
+        std::vector<uint64_t> pass_before;
+        // the pass arrays (off, len, no) share one buffer with the record offsets
+        const uint64_t rec_bytes_needed = 8 * (max_data + 1) + 12 * (max_data + 1);
+        uint8_t *d_rec = static_cast<uint8_t *>(M.dev(Memory::D_REC, rec_bytes_needed));
+        if (!d_rec) return finish(ST_E_HIP);
+        uint64_t *d_rec_off = reinterpret_cast<uint64_t *>(d_rec);
+        x.pass_off = reinterpret_cast<uint32_t *>(d_rec + 8 * (max_data + 1));
+        x.pass_len = x.pass_off + (max_data + 1);
+        x.pass_no = x.pass_len + (max_data + 1);
+        if (vcfc_line_index_place(d_in, n_lines, d_ix1, d_ix2, L, x, s) != hipSuccess ||
+            hipMemcpyAsync(hsmall, d_small, 24, hipMemcpyDeviceToHost, s) != hipSuccess || !sync())
+            return finish(ST_E_HIP);
+        const uint64_t n_data = hsmall[1], n_pass = hsmall[2];
+        // '#' lines: bytes from the host copy, checked in order; the first
+        // header line with < 8 terms stops the input there
+        std::vector<PassLine> pass;
+        int64_t hdr_err = -1;   // chunk line number
+        uint64_t hdr_before = 0;
+        if (n_pass) {
+            pass_off.resize(n_pass); pass_len.resize(n_pass); pass_no.resize(n_pass); pass_before.resize(n_pass);
+            if (hipMemcpyAsync(pass_off.data(), x.pass_off, 4 * n_pass, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                hipMemcpyAsync(pass_len.data(), x.pass_len, 4 * n_pass, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                hipMemcpyAsync(pass_no.data(), x.pass_no, 4 * n_pass, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                hipMemcpyAsync(pass_before.data(), x.pass_before, 8 * n_pass, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                !sync())
+                return finish(ST_E_HIP);
+            for (uint64_t k = 0; k < n_pass; k++) {
+                const uint8_t *p = h + pass_off[k];
+                const uint64_t len = pass_len[k];
+                if (!(len >= 2 && p[1] == '#') && !header_ok(p, len)) {
+                    hdr_err = pass_no[k];
+                    hdr_before = pass_before[k];
+                    break;
+                }
+                PassLine pl;
+                pl.before = pass_before[k];
+                pl.no = pass_no[k];
+                pl.text.assign(p, p + len);
+                pl.text.push_back('\n');
+                pass.push_back(std::move(pl));
+            }
+        }
+        free_in.put(ch.slot);   // the host copy is no longer needed
+        // encode the data lines
+        int oslot;
+        const double o0 = now_s();
+        if (!free_out.get(oslot)) return finish(ST_E_HIP);
+        t_wait_out += now_s() - o0;
+        OutChunk oc;
+        oc.slot = oslot;
+        uint64_t good = n_data;   // rows to write
+        int st = ST_OK;
+        int64_t bad_line = -1;
+        uint8_t *d_out = nullptr;
+        oc.rec_off.assign(1, 0);
+        if (n_data) {
+            const VcfcWorkspaceLayout W = vcfc_encode_workspace_layout(n_data, n);
+            uint8_t *ws = static_cast<uint8_t *>(M.dev(Memory::D_ENC_WS, W.total));
+            const uint64_t cap = vcfc_record_bound(n_data, n) + 64;
+            d_out = static_cast<uint8_t *>(M.dev(Memory::D_OUT, cap));
+            if (!ws || !d_out) return finish(ST_E_HIP);
+            VcfcEncodeArgs a;
+            a.buf = d_in; a.line_off = x.line_off; a.line_len = x.line_len; a.n = n_data;
+            a.out = d_out; a.out_cap = cap; a.rec_off = d_rec_off;
+            a.slot_off = reinterpret_cast<uint64_t *>(ws + W.slot_off);
+            a.rec_size = reinterpret_cast<uint32_t *>(ws + W.rec_size);
+            a.partials = reinterpret_cast<uint64_t *>(ws + W.partials);
+            a.err = d_small + 4;
+            a.retry = reinterpret_cast<uint32_t *>(ws + W.retry);
+            a.retry_count = reinterpret_cast<uint32_t *>(ws + W.retry_count);
+            a.slots = ws + W.slots;
+            a.slots_cap = W.total - W.slots;
+            oc.rec_off.resize(n_data + 1);
+            if (vcfc_encode_device(a, s) != hipSuccess ||
+                hipMemcpyAsync(oc.rec_off.data(), d_rec_off, 8 * (n_data + 1), hipMemcpyDeviceToHost, s) != hipSuccess ||
+                hipMemcpyAsync(hsmall + 4, d_small + 4, 8, hipMemcpyDeviceToHost, s) != hipSuccess || !sync())
+                return finish(ST_E_HIP);
+            const uint64_t errw = hsmall[4];
+            if (errw != VCFCD_NO_ERROR) {
+                good = errw >> 8;
+                st = (int)(errw & 0xFF);
+                uint32_t ln = 0;
+                if (hipMemcpyAsync(&ln, x.line_no + good, 4, hipMemcpyDeviceToHost, s) != hipSuccess || !sync())
+                    return finish(ST_E_HIP);
+                bad_line = ln;
+            }
+        }
+        // the first failing line of the chunk: a header line or a data line
+        bool stop = false;
+        if (hdr_err >= 0 && (bad_line < 0 || hdr_err < bad_line)) {
+            good = hdr_before;
+            st = ST_E_HEADER;
+            bad_line = hdr_err;
+            stop = true;
+        } else if (bad_line >= 0) {
+            stop = true;
+            while (!pass.empty() && pass.back().before > good) pass.pop_back();   // '#' lines after the failing row
+        }
+        oc.rec_bytes = oc.rec_off[good];
+        if (oc.rec_bytes &&
+            (hipMemcpyAsync(hout[oslot], d_out, oc.rec_bytes, hipMemcpyDeviceToHost, s) != hipSuccess || !sync()))
+            return finish(ST_E_HIP);
+        oc.pass = std::move(pass);
+        if (oc.pass.empty()) oc.rec_off.clear();
+        to_write.put(std::move(oc));
+        if (stop) {
+            if (err_line) *err_line = (int64_t)(line_base + (uint64_t)bad_line + 1);
+            return finish(st);
+        }
+        line_base += n_lines;
+    }
+    return finish(ST_OK);
+}
+
+}  // namespace vcfc_ing
