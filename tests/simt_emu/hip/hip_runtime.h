@@ -41,6 +41,13 @@ inline hipError_t hipMemcpyAsync(void *d, const void *s, size_t n, int, hipStrea
 #define hipMemcpyHostToDevice 1
 #define hipMemcpyDeviceToHost 2
 inline hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
+#define hipStreamNonBlocking 1
+#define hipEventDisableTiming 2
+inline hipError_t hipStreamCreateWithFlags(hipStream_t *s, unsigned) { *s = nullptr; return hipSuccess; }
+inline hipError_t hipStreamDestroy(hipStream_t) { return hipSuccess; }
+inline hipError_t hipEventCreateWithFlags(hipEvent_t *e, unsigned) { *e = nullptr; return hipSuccess; }
+inline hipError_t hipEventDestroy(hipEvent_t) { return hipSuccess; }
+inline hipError_t hipStreamWaitEvent(hipStream_t, hipEvent_t, unsigned) { return hipSuccess; }
 
 inline void __syncthreads() { emu::collective(emu::OP_SYNCTHREADS, 0, 0, 0); }
 

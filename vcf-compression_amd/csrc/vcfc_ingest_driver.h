@@ -11,7 +11,10 @@
 //   reader  (host threads)  the input in chunks of up to `chunk` bytes into
 //                           pinned host slots; the partial line at a chunk's
 //                           end is carried to the next chunk;
-//   GPU     (calling thread) H2D -> line index (vcfc_ingest.hip) -> encode
+//   uploader (host thread)  H2D of each chunk into one of two device slots on
+//                           its own stream, so the copy of chunk k+1 overlaps
+//                           the GPU work on chunk k;
+//   GPU     (calling thread) line index (vcfc_ingest.hip) -> encode
 //                           (vcfc_encode.hip) -> D2H of the records, the
 //                           '#' lines checked on the host (>= 8 terms);
 //   writer  (host thread)   records with the '#' lines interleaved at their
@@ -54,7 +57,7 @@ using Sink = std::function<bool(const uint8_t *, uint64_t)>;
 // between calls.
 struct Memory {
     virtual ~Memory() {}
-    enum { D_IN = 0, D_IX1, D_IX2, D_LINES, D_ENC_WS, D_OUT, D_REC, D_SMALL, N_DEV };
+    enum { D_IN0 = 0, D_IN1, D_IX1, D_IX2, D_LINES, D_ENC_WS, D_OUT, D_REC, D_SMALL, N_DEV };
     enum { H_IN0 = 0, H_IN1, H_IN2, H_OUT0, H_OUT1, H_SMALL, N_HOST };
     virtual void *dev(int slot, uint64_t bytes) = 0;    // nullptr on failure
     virtual void *host(int slot, uint64_t bytes) = 0;   // pinned; nullptr on failure
@@ -62,7 +65,7 @@ struct Memory {
 
 struct Config {
     uint64_t chunk = 256ull << 20;   // input bytes per chunk (lines must be shorter)
-    int read_threads = 4;
+    int read_threads = 8;
 };
 
 // compress()'s header-line check (src/compress.cpp:230-235): split_string
@@ -112,6 +115,7 @@ struct Queue {   // bounded hand-off between the stages
 
 struct InChunk {
     int slot = -1;
+    int dslot = -1;       // device copy (set by the uploader)
     uint64_t bytes = 0;   // whole lines, the last one ending with '\n'
     bool ok = true;       // false: read error, or a line longer than a chunk
     bool long_line = false;
@@ -152,11 +156,22 @@ inline int compress_stream(Source &src, const Sink &sink, Memory &M, hipStream_t
     for (int k = 0; k < 2; k++)
         if (!(hout[k] = static_cast<uint8_t *>(M.host(Memory::H_OUT0 + k, out_cap)))) return ST_E_HIP;
     uint64_t *hsmall = static_cast<uint64_t *>(M.host(Memory::H_SMALL, 64));
-    uint8_t *d_in = static_cast<uint8_t *>(M.dev(Memory::D_IN, CX + 64));
+    uint8_t *d_inb[2] = {static_cast<uint8_t *>(M.dev(Memory::D_IN0, CX + 64)),
+                         static_cast<uint8_t *>(M.dev(Memory::D_IN1, CX + 64))};
     const VcfcLineIndexLayout L1 = vcfc_line_index_layout(CX, 0);
     uint8_t *d_ix1 = static_cast<uint8_t *>(M.dev(Memory::D_IX1, L1.total1));
     uint64_t *d_small = static_cast<uint64_t *>(M.dev(Memory::D_SMALL, 64));
-    if (!hsmall || !d_in || !d_ix1 || !d_small) return ST_E_HIP;
+    if (!hsmall || !d_inb[0] || !d_inb[1] || !d_ix1 || !d_small) return ST_E_HIP;
+    hipStream_t s_copy = nullptr;
+    hipEvent_t ev_up[2] = {nullptr, nullptr};
+    if (hipStreamCreateWithFlags(&s_copy, hipStreamNonBlocking) != hipSuccess) return ST_E_HIP;
+    if (hipEventCreateWithFlags(&ev_up[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ev_up[1], hipEventDisableTiming) != hipSuccess) {
+        for (hipEvent_t e : ev_up)
+            if (e) (void)hipEventDestroy(e);
+        (void)hipStreamDestroy(s_copy);
+        return ST_E_HIP;
+    }
 
     // ---- reader ------------------------------------------------------------
     Queue<InChunk> filled;
@@ -213,6 +228,28 @@ inline int compress_stream(Source &src, const Sink &sink, Memory &M, hipStream_t
         filled.close();
     });
 
+    // ---- uploader ------------------------------------------------------------
+    Queue<InChunk> uploaded;
+    Queue<int> free_dev;
+    free_dev.put(0);
+    free_dev.put(1);
+    std::thread uploader([&] {
+        InChunk ch;
+        while (filled.get(ch)) {
+            if (ch.ok) {
+                int ds;
+                if (!free_dev.get(ds)) break;
+                ch.dslot = ds;
+                if (hipMemcpyAsync(d_inb[ds], hin[ch.slot], ch.bytes, hipMemcpyHostToDevice, s_copy) != hipSuccess ||
+                    hipEventRecord(ev_up[ds], s_copy) != hipSuccess)
+                    ch.ok = false;
+            }
+            uploaded.put(ch);
+            if (!ch.ok) break;
+        }
+        uploaded.close();
+    });
+
     // ---- writer ------------------------------------------------------------
     Queue<OutChunk> to_write;
     Queue<int> free_out;
@@ -249,9 +286,16 @@ inline int compress_stream(Source &src, const Sink &sink, Memory &M, hipStream_t
     auto finish = [&](int st) {
         status = st;
         free_in.close();
+        free_dev.close();
+        filled.close();
         to_write.close();
         reader.join();
+        uploader.join();
         writer.join();
+        (void)hipStreamSynchronize(s_copy);
+        (void)hipEventDestroy(ev_up[0]);
+        (void)hipEventDestroy(ev_up[1]);
+        (void)hipStreamDestroy(s_copy);
         if (status == ST_OK && write_failed) status = ST_E_IO;
         if (trace)
             fprintf(stderr, "vcfc ingest: %.3f s total; read %.3f s, gpu stage %.3f s (waiting for input %.3f s, "
@@ -263,20 +307,21 @@ inline int compress_stream(Source &src, const Sink &sink, Memory &M, hipStream_t
     InChunk ch;
     for (;;) {
         double g0 = now_s();
-        if (!filled.get(ch)) break;
+        if (!uploaded.get(ch)) break;
         t_wait_in += now_s() - g0;
         g0 = now_s();
         struct Acc {
             double &t, g;
             ~Acc() { t += now_s() - g; }
         } acc{t_gpu, g0};
-        if (!ch.ok) return finish(ch.long_line ? ST_E_ARG : ST_E_IO);
+        if (!ch.ok) return finish(ch.long_line ? ST_E_ARG : ch.dslot >= 0 ? ST_E_HIP : ST_E_IO);
         const uint64_t n = ch.bytes;
         const uint8_t *h = hin[ch.slot];
+        uint8_t *d_in = d_inb[ch.dslot];
         VcfcLineIndex x;
         x.counts = d_small;
         // phase 1: '\n' positions
-        if (hipMemcpyAsync(d_in, h, n, hipMemcpyHostToDevice, s) != hipSuccess ||
+        if (hipStreamWaitEvent(s, ev_up[ch.dslot], 0) != hipSuccess ||
             vcfc_line_index(d_in, n, d_ix1, L1, x, s) != hipSuccess ||
             hipMemcpyAsync(hsmall, d_small, 8, hipMemcpyDeviceToHost, s) != hipSuccess || !sync())
             return finish(ST_E_HIP);
@@ -397,6 +442,7 @@ inline int compress_stream(Source &src, const Sink &sink, Memory &M, hipStream_t
             return finish(ST_E_HIP);
         oc.pass = std::move(pass);
         if (oc.pass.empty()) oc.rec_off.clear();
+        free_dev.put(ch.dslot);   // its records are on the host
         to_write.put(std::move(oc));
         if (stop) {
             if (err_line) *err_line = (int64_t)(line_base + (uint64_t)bad_line + 1);
