@@ -39,18 +39,28 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--rows", type=int, default=1_000_000, help="rows per GPU")
-    ap.add_argument("--samples", type=int, default=2504)
+    ap.add_argument("--rows", type=int, default=None, help="rows per GPU (default 1M; 100k in --mode biobank)")
+    ap.add_argument("--samples", type=int, default=None, help="samples (default 2504; 100k in --mode biobank)")
     ap.add_argument("--law", type=int, default=1, help="1 = chr22-shaped (headline), 0 = random_vcf law")
-    ap.add_argument("--cpu-rows", type=int, default=120_000, help="rows in the CPU-baseline sample")
+    ap.add_argument("--cpu-rows", type=int, default=None,
+                    help="rows in the CPU-baseline sample (default: about 1.2 GB of lines)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify-rows", type=int, default=64, help="rows checked against the CPU path")
-    ap.add_argument("--mode", choices=["encode", "decode", "query", "ingest"], default="encode",
-                    help="encode = the headline (BASELINE metric); decode = row f1; query = row f2; "
-                         "ingest = row f4 (end-to-end file compress)")
+    ap.add_argument("--mode", choices=["encode", "biobank", "decode", "query", "ingest"], default="encode",
+                    help="encode = the headline (BASELINE metric, configs[1]); biobank = configs[3] "
+                         "(100k samples, one 100k-row batch of a 5M-row shard per GPU); decode = row f1; "
+                         "query = row f2; ingest = row f4 (end-to-end file compress, configs[2])")
     ap.add_argument("--ingest-rows", type=int, default=200_000, help="rows of the --mode ingest file")
     ap.add_argument("--query-frac", type=float, default=0.125, help="rows selected by the --mode query range")
-    return ap.parse_args()
+    a = ap.parse_args()
+    big = a.mode == "biobank"
+    if a.samples is None:
+        a.samples = 100_000 if big else 2504
+    if a.rows is None:
+        a.rows = 100_000 if big else 1_000_000
+    if a.cpu_rows is None:
+        a.cpu_rows = max(1, int(1.2e9 // (4 * a.samples + 180)))   # ~120k rows at 2504 samples
+    return a
 
 
 def cpu_baseline(rows, torch, args):
@@ -383,7 +393,7 @@ def bench_ingest(args, torch, vcfc, workload):
 
 def main():
     args = parse()
-    if args.mode in ("decode", "query", "ingest"):
+    if args.mode not in ("encode", "biobank"):
         import torch
         import vcfc
         import workload
@@ -453,16 +463,23 @@ def main():
     alg = rows.line_bytes + out_bytes
     wl = "chr22-shaped" if args.law == 1 else "random_vcf-law"
     wkey = "%s/%dx%d" % (wl, S, n)
+    if args.mode == "biobank":
+        metric = "input GT bytes/sec encoded, 100k-sample x 5M-variant VCF, row-sharded"
+        wdesc = ("%s %d samples x %d-variant batch per GPU (BASELINE configs[3]: one batch of the "
+                 "5M/N-row shard; batches are independent and run back to back)" % (wl, S, n))
+    else:
+        metric = "input GT bytes/sec encoded, 2504-sample x 1M-variant VCF"
+        wdesc = "%s %d samples x %d variants per GPU (BASELINE configs[1])" % (wl, S, n)
     roof = {"kernel": "k_encode", "bound": "hbm", "achieved": round(alg / (k_ms * 1e-3) / 1e9, 1),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(alg / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "traffic": load_pmc(wkey),
             "algorithmic_bytes_per_launch": alg, "avg_launch_ms": round(k_ms, 4),
             "stages_ms": {k: round(v / max(calls, 1), 4) for k, v in stages.items()}}
-    res = {"metric": "input GT bytes/sec encoded, 2504-sample x 1M-variant VCF",
+    res = {"metric": metric,
            "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic (generated in HBM)",
-           "config": {"workload": "%s %d samples x %d variants per GPU (BASELINE configs[1])" % (wl, S, n),
+           "config": {"workload": wdesc,
                       "samples": S, "rows_per_gpu": n, "gt_bytes_per_gpu": rows.gt_bytes,
                       "line_bytes_per_gpu": rows.line_bytes, "record_bytes_per_gpu": out_bytes,
                       "compression_ratio": round(out_bytes / rows.line_bytes, 4),

@@ -114,7 +114,8 @@ def _device_encode(torch, vcfc, rows):
     return out, rec.cpu().numpy().astype(np.uint64), int(err.cpu().numpy().view(np.uint64)[0])
 
 
-@pytest.mark.parametrize("law,samples,n", [(0, 2504, 3000), (1, 2504, 3000), (0, 100, 20000), (1, 5003, 700)])
+@pytest.mark.parametrize("law,samples,n", [(0, 2504, 3000), (1, 2504, 3000), (0, 100, 20000), (1, 5003, 700),
+                                           (1, 100_000, 48), (0, 100_000, 24)])   # last two: configs[3] rows
 def test_synthetic_rows_all_vs_oracle(torch, vcfc, law, samples, n):
     import workload
     rows = workload.DeviceRows(torch, vcfc, n, samples, law, seed=7 + law, device="cuda:0")

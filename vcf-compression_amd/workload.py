@@ -21,8 +21,11 @@ import numpy as np
 BASES = np.array(list("ATGC"))
 
 
-def prefixes(n, law, seed, row0=0):
-    """Return (prefix bytes blob, prefix_off[n+1] int64, row_af float32 or None, POS int64[n])."""
+def prefixes(n, law, seed, row0=0, samples=2504):
+    """Return (prefix bytes blob, prefix_off[n+1] int64, row_af float32 or None, POS int64[n]).
+
+    law 1 scales with the sample count: k ~ 1/k on [1, 2S-1], AN = 2S, NS = S
+    (at S = 2504 these are the 1000 Genomes values)."""
     rng = np.random.default_rng(seed)
     ref = rng.integers(0, 4, n)
     if law == 0:
@@ -36,9 +39,10 @@ def prefixes(n, law, seed, row0=0):
     else:
         gaps = rng.geometric(1.0 / 32.0, n)
         pos = 16050075 + row0 * 32 + np.cumsum(gaps) - gaps[0]
-        k = np.floor(np.exp(rng.random(n) * np.log(5008.0))).astype(np.int64)
-        k = np.clip(k, 1, 5007)
-        afv = k / 5008.0
+        an = 2 * samples
+        k = np.floor(np.exp(rng.random(n) * np.log(float(an)))).astype(np.int64)
+        k = np.clip(k, 1, an - 1)
+        afv = k / float(an)
         alt = (ref + rng.integers(1, 4, n)) % 4
         dp = rng.integers(10000, 30000, n)
         pops = np.clip(afv[:, None] * rng.uniform(0.2, 1.8, (n, 5)), 0, 1)
@@ -47,9 +51,9 @@ def prefixes(n, law, seed, row0=0):
         rows = []
         for i in range(n):
             p = pops[i]
-            rows.append("22\t%d\trs%d\t%s\t%s\t100\tPASS\tAC=%d;AF=%.4g;AN=5008;NS=2504;DP=%d;"
+            rows.append("22\t%d\trs%d\t%s\t%s\t100\tPASS\tAC=%d;AF=%.4g;AN=%d;NS=%d;DP=%d;"
                         "EAS_AF=%.4g;AMR_AF=%.4g;AFR_AF=%.4g;EUR_AF=%.4g;SAS_AF=%.4g;AA=.|||;VT=SNP\tGT\t"
-                        % (pos[i], rs[i], BASES[ref[i]], BASES[alt[i]], k[i], afv[i], dp[i],
+                        % (pos[i], rs[i], BASES[ref[i]], BASES[alt[i]], k[i], afv[i], an, samples, dp[i],
                            p[0], p[1], p[2], p[3], p[4]))
         af = (afv + multi.astype(np.float64)).astype(np.float32)
     blob = "".join(rows).encode()
@@ -73,7 +77,7 @@ class DeviceRows:
     """A synthetic batch resident in HBM (torch tensors)."""
 
     def __init__(self, torch, vcfc, n, samples, law, seed, device, row0=0):
-        blob, poff, af, self.pos = prefixes(n, law, seed, row0)
+        blob, poff, af, self.pos = prefixes(n, law, seed, row0, samples)
         self.chrom = "1" if law == 0 else "22"
         line_off, line_len, total = layout(poff, samples)
         dev = torch.device(device)
