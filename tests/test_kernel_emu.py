@@ -164,3 +164,38 @@ def test_dense_rows_wrap_the_ring(seed):
         assert E.LAST_RETRIES[0] == 0
         for i, ln in enumerate(lines):
             assert out[int(ro[i]):int(ro[i + 1])] == G.oracle_encode_line(ln)[1], (lead, i)
+
+
+@pytest.mark.parametrize("seed", [41, 42, 43])
+def test_escape_rows_on_the_three_byte_path(seed):
+    """3-byte escape tokens (multi-allelic, missing, unphased, raw high bytes)
+    at every density, at token 0, at chunk edges (512-token chunks), at the
+    row end, in runs of escapes, and right after runs that end on the caps:
+    the escape path of the fast kernel (esc8), with and without an escape as
+    the incoming class of a chunk."""
+    rnd = random.Random(seed)
+    plain = [b"0|0", b"0|1", b"1|0", b"1|1"]
+    escs = [b"0|2", b"2|0", b"./.", b".|.", b"0/1", b"1/1", b"2|2", b"\xff|\x80", b"0|\r", b"3|1"]
+    lens = [1, 2, 30, 31, 32, 126, 127, 128, 511, 512, 513]
+    lines = []
+    for i in range(24):
+        target = rnd.choice([1, 2, 511, 512, 513, 1024, 1025, 2504, 5000])
+        dens = rnd.choice([0.0005, 0.01, 0.04, 0.3, 1.0])
+        toks = []
+        while len(toks) < target:
+            if rnd.random() < dens:
+                toks += [rnd.choice(escs)] * rnd.choice([1, 1, 1, 2, 5])
+            else:
+                toks += [rnd.choice(plain)] * rnd.choice(lens)
+        toks = toks[:target]
+        for p in rnd.sample([0, 510, 511, 512, 1023, 1024, target - 1], 3):
+            if 0 <= p < target:
+                toks[p] = rnd.choice(escs)
+        pfx = b"22\t%d\trs%d\tA\tG,T\t100\tPASS\t%s\tGT\t" % (100 + i, i, b"Y" * rnd.randint(1, 60))
+        lines.append(pfx + b"\t".join(toks))
+    for lead in (0, 3, 9):
+        st, out, ro, err = run(lines, lead=lead)
+        assert err == (1 << 64) - 1
+        assert E.LAST_RETRIES[0] == 0   # escapes stay on the fast kernel
+        for i, ln in enumerate(lines):
+            assert out[int(ro[i]):int(ro[i + 1])] == G.oracle_encode_line(ln)[1], (lead, i)

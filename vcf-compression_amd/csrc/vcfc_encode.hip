@@ -498,8 +498,134 @@ __device__ __forceinline__ void clean8(const uint32_t (&d)[TPL8], int32_t t0, in
     ring_flush(r, false);
 }
 
-// Genotype chunk C (2 KiB) on the skip / clean paths.  false = not handled
-// (nothing written): the chunk needs the general step.
+// Escape chunk: every slot in [0, T) is a 3-byte token followed by one TAB
+// (the last token by the line end) -- the shape of multi-allelic ("0|2"),
+// missing ("./.") and unphased ("0/1") genotypes.  Escapes get class 4 (class
+// byte 0x94) and always start a run.  Per lane, in token order: the full-chunk
+// byte of the entering run (as clean8), then per start its lead byte -- TAB
+// after an escape, else the pending byte of the run it closes (for the first
+// start only if that run's last chunk is partial; runs closed by a further
+// start are shorter than any cap) -- and, for an escape, 0xE1 + its 3 bytes.
+// The incoming class may be an escape (p0 == 4 makes slot 0 a start whose
+// lead byte is TAB).  EDGE: slots past T-1 take token T-1's class and are
+// masked out of the starts and escapes.
+template <bool EDGE>
+__device__ __forceinline__ void esc8(const uint32_t (&d)[TPL8], int32_t t0, int32_t tf, FastState &f, Ring &r) {
+    constexpr uint32_t Z = 0x09307C30u;
+    uint32_t eL = 0, eH = 0;   // 0xFF in the byte of each escape slot
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        eL |= ((d[j] ^ Z) & 0x00FEFFFEu) ? (0xFFu << (8 * j)) : 0u;
+        eH |= ((d[j + 4] ^ Z) & 0x00FEFFFEu) ? (0xFFu << (8 * j)) : 0u;
+    }
+    // class bytes from the low bits of bytes 0 and 2 only (an escape's bytes
+    // must not carry into its neighbours), escapes then set to 0x94
+    uint32_t q[TPL8];
+#pragma unroll
+    for (int j = 0; j < (int)TPL8; j++) q[j] = (d[j] & 0x00010001u) | 0x00300030u;
+    uint32_t cbL = (class_bytes(q[0], q[1], q[2], q[3]) & ~eL) | (0x94949494u & eL);
+    uint32_t cbH = (class_bytes(q[4], q[5], q[6], q[7]) & ~eH) | (0x94949494u & eH);
+    if (f.pcls == CLS_NONE) {   // first chunk: see clean8 (an escape token 0 -> class 0: no lead byte)
+        f.pcls = vw::readlane(cbL, 0) & 3u;
+        f.prs = 1;
+    }
+    const uint32_t T = f.T;
+    uint32_t vbits = 0x11111111u;   // bit 4j: slot j holds a token
+    if (EDGE) {
+        const uint32_t ol = (uint32_t)((int32_t)T - 1 - tf);
+        const uint32_t cw = vw::readlane((ol & 4u) ? cbH : cbL, ol >> 3);
+        const uint32_t cL = (cw >> (8u * (ol & 3u))) & 7u;
+        const int32_t nv = (int32_t)T - t0;
+        const uint32_t fill = 0x90909090u | (cL * 0x01010101u);
+        const uint32_t mL = nv >= 4 ? 0u : (nv <= 0 ? ~0u : (~0u << (8 * nv)));
+        const uint32_t mH = nv >= 8 ? 0u : (nv <= 4 ? ~0u : (~0u << (8 * (nv - 4))));
+        cbL = (cbL & ~mL) | (fill & mL);
+        cbH = (cbH & ~mH) | (fill & mH);
+        vbits = nv >= 8 ? 0x11111111u : (nv <= 0 ? 0u : (0x11111111u & ((1u << (4 * nv)) - 1u)));
+    }
+    const uint32_t pw = vw::shr1(cbH, (0x90u | f.pcls) << 24);
+    const uint32_t cpL = vw::alignbyte(cbL, pw, 3), cpH = vw::alignbyte(cbH, cbL, 3);
+    const uint32_t xL = cbL ^ cpL, xH = cbH ^ cpH;
+    // a start: class differs from the predecessor's (bits 0-2), or an escape (bit 2 of the class byte)
+    const uint32_t sL = (xL | (xL >> 1) | (xL >> 2) | (cbL >> 2)) & 0x01010101u;
+    const uint32_t sH = (xH | (xH >> 1) | (xH >> 2) | (cbH >> 2)) & 0x01010101u;
+    const uint32_t sb = stride4(sL, sH) & vbits;
+    const uint32_t eb = stride4((cbL >> 2) & 0x01010101u, (cbH >> 2) & 0x01010101u) & vbits;   // escape slots
+    const uint32_t cp4 = stride4(cpL & 0x07070707u, cpH & 0x07070707u);       // class of slot j-1 at bits 4j
+    const uint32_t lane_rs = sb ? (uint32_t)(t0 + 8) - ((uint32_t)__builtin_clz(sb) >> 2) : 0u;
+    const uint32_t incl = vw::scan_max(lane_rs);
+    const uint32_t rin = vw::umax(vw::shr1z(incl), f.prs);
+    const uint32_t p0 = cpL & 7u;
+    const bool is00 = p0 == 0;
+    const uint32_t cap = is00 ? 127u : 31u;
+    const uint32_t mp = mod_cap((uint32_t)(t0 + (int32_t)MOD_BIAS) - rin, is00);
+    const uint32_t fb1 = sb ? (uint32_t)__builtin_ctz(sb) : 32u;
+    const uint32_t j1 = fb1 >> 2;
+    const uint32_t m0 = vw::perm(0x80C0A000u, 0x80C0A000u, p0 & 3u);
+    const uint32_t jf = cap - 2u - mp;
+    bool full = p0 < CLS_ESC && jf < j1;
+    if (EDGE) full = full && (uint32_t)(t0 + (int32_t)jf) < T;
+    uint32_t rr = mp + j1;
+    rr = umin32(rr, rr - cap);
+    const bool pesc = p0 == CLS_ESC;
+    const bool lead1 = j1 < TPL8 && (pesc || rr != cap - 1u);
+    const uint32_t b1 = pesc ? 0x09u : (m0 | (rr + 1u));
+    const uint32_t n2 = (uint32_t)__builtin_popcount(sb & (sb - 1u));
+    const uint32_t cnt = (full ? 1u : 0u) + (lead1 ? 1u : 0u) + n2 + 4u * (uint32_t)__builtin_popcount(eb);
+    const uint32_t incl2 = vw::scan_add(cnt);
+    uint32_t pos = r.wpos + incl2 - cnt;
+    if (full) ring_put(r, pos, m0 | cap);
+    pos += full ? 1u : 0u;
+    bool seen = false;
+    uint32_t jp = 0;
+#pragma unroll
+    for (int j = 0; j < (int)TPL8; j++) {
+        const bool s = (sb >> (4 * j)) & 1u;
+        const bool e = (eb >> (4 * j)) & 1u;
+        const uint32_t pc = (cp4 >> (4 * j)) & 7u;
+        const bool lead = s && (seen || lead1);
+        const uint32_t b = !seen ? b1
+                         : (pc == CLS_ESC ? 0x09u : (vw::perm(0x80C0A000u, 0x80C0A000u, pc) | ((uint32_t)j - jp)));
+        if (lead) ring_put(r, pos, b);
+        pos += lead ? 1u : 0u;
+        if (e) {
+            ring_put(r, pos, 0xE1u);
+            ring_put(r, pos + 1u, d[j] & 0xFFu);
+            ring_put(r, pos + 2u, (d[j] >> 8) & 0xFFu);
+            ring_put(r, pos + 3u, (d[j] >> 16) & 0xFFu);
+            pos += 4u;
+        }
+        if (s) { seen = true; jp = (uint32_t)j; }
+    }
+    r.wpos += vw::readlane(incl2, 63);
+    f.pcls = (vw::readlane(cbH, 63) >> 24) & 7u;
+    f.prs = vw::umax(vw::readlane(incl, 63), f.prs);
+    ring_flush(r, false);
+}
+
+// every slot of the lane is "xyz\t" with x, y, z not TAB (the last token: no
+// TAB needed; slots past it ignored)
+template <bool EDGE>
+__device__ __forceinline__ bool shape3(const uint32_t (&d)[TPL8], int32_t t0, uint32_t T) {
+    bool bad = false;
+#pragma unroll
+    for (int j = 0; j < (int)TPL8; j++) {
+        const uint32_t x = d[j] ^ 0x09090909u;
+        const uint32_t zb = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);   // 0x80 per TAB byte
+        if (EDGE) {
+            const int32_t t = t0 + j;
+            const uint32_t want = (uint32_t)t + 1u == T ? 0u : 0x80000000u;
+            const uint32_t m = (uint32_t)t + 1u == T ? 0x00808080u : 0x80808080u;
+            bad |= (uint32_t)t < T && (zb & m) != want;
+        } else {
+            bad |= zb != 0x80000000u;
+        }
+    }
+    return bad;
+}
+
+// Genotype chunk C (2 KiB) on the skip / clean / escape paths.  false = not
+// handled (nothing written): the chunk needs the general step.
 __device__ __forceinline__ bool gt_step8(const Chunk8 &cur, uint32_t C, FastState &f, Ring &r) {
     const uint32_t l = vw::lane_id();
     const uint32_t T = f.T, phi = f.phi;
@@ -510,42 +636,49 @@ __device__ __forceinline__ bool gt_step8(const Chunk8 &cur, uint32_t C, FastStat
 #pragma unroll
     for (int j = 0; j < (int)TPL8; j++) d[j] = vw::alignbyte(cur.w(j + 1), cur.w(j), phi);
     const int32_t t0 = tf + (int32_t)(TPL8 * l);
-    if (f.pcls < CLS_ESC || f.pcls == CLS_NONE) {
-        if (tf + (int32_t)SLOTS8 < (int32_t)T) {
-            // interior chunk: every slot a token, none of them the last
-            const uint32_t o = ((d[0] ^ Z) | (d[1] ^ Z)) | ((d[2] ^ Z) | (d[3] ^ Z)) |
-                               ((d[4] ^ Z) | (d[5] ^ Z)) | ((d[6] ^ Z) | (d[7] ^ Z));
-            if (f.pcls == 0 && vw::ballot(o != 0) == 0) {
-                // one 0|0 run through the whole chunk: only full 127-chunks
-                // complete.  Token t has run offset t + 1 - prs; count the
-                // multiples of 127 in [a0 + 1, a0 + 512].
-                const uint32_t a0 = (uint32_t)tf + 1 - f.prs;
-                const uint32_t kfull = (a0 + SLOTS8) / 127 - a0 / 127;
-                if (l < kfull) ring_put(r, r.wpos + l, 0x7Fu);
-                r.wpos += kfull;
-                ring_flush(r, false);
-                return true;
-            }
-            if (vw::ballot((o & 0xFFFEFFFEu) != 0) == 0) {
-                clean8<false>(d, t0, tf, f, r);
-                return true;
-            }
-        } else {
-            // last chunk: slots past T-1 are ignored; token T-1 has no TAB after it
-            bool bad = false;
+    const bool pclean = f.pcls < CLS_ESC || f.pcls == CLS_NONE;
+    if (tf + (int32_t)SLOTS8 < (int32_t)T) {
+        // interior chunk: every slot a token, none of them the last
+        const uint32_t o = ((d[0] ^ Z) | (d[1] ^ Z)) | ((d[2] ^ Z) | (d[3] ^ Z)) |
+                           ((d[4] ^ Z) | (d[5] ^ Z)) | ((d[6] ^ Z) | (d[7] ^ Z));
+        if (f.pcls == 0 && vw::ballot(o != 0) == 0) {
+            // one 0|0 run through the whole chunk: only full 127-chunks
+            // complete.  Token t has run offset t + 1 - prs; count the
+            // multiples of 127 in [a0 + 1, a0 + 512].
+            const uint32_t a0 = (uint32_t)tf + 1 - f.prs;
+            const uint32_t kfull = (a0 + SLOTS8) / 127 - a0 / 127;
+            if (l < kfull) ring_put(r, r.wpos + l, 0x7Fu);
+            r.wpos += kfull;
+            ring_flush(r, false);
+            return true;
+        }
+        if (pclean && vw::ballot((o & 0xFFFEFFFEu) != 0) == 0) {
+            clean8<false>(d, t0, tf, f, r);
+            return true;
+        }
+        if (vw::ballot(shape3<false>(d, t0, T)) == 0) {
+            esc8<false>(d, t0, tf, f, r);
+            return true;
+        }
+    } else {
+        // last chunk: slots past T-1 are ignored; token T-1 has no TAB after it
+        bool bad = false;
 #pragma unroll
-            for (int j = 0; j < (int)TPL8; j++) {
-                const int32_t t = t0 + j;
-                const uint32_t m = (uint32_t)t < T ? ((uint32_t)t + 1u == T ? 0x00FEFFFEu : 0xFFFEFFFEu) : 0u;
-                bad |= ((d[j] ^ Z) & m) != 0;
-            }
-            if (vw::ballot(bad) == 0) {
-                clean8<true>(d, t0, tf, f, r);
-                return true;
-            }
+        for (int j = 0; j < (int)TPL8; j++) {
+            const int32_t t = t0 + j;
+            const uint32_t m = (uint32_t)t < T ? ((uint32_t)t + 1u == T ? 0x00FEFFFEu : 0xFFFEFFFEu) : 0u;
+            bad |= ((d[j] ^ Z) & m) != 0;
+        }
+        if (pclean && vw::ballot(bad) == 0) {
+            clean8<true>(d, t0, tf, f, r);
+            return true;
+        }
+        if (vw::ballot(shape3<true>(d, t0, T)) == 0) {
+            esc8<true>(d, t0, tf, f, r);
+            return true;
         }
     }
-    return false;   // escapes or odd bytes: the caller runs gt_general on this chunk
+    return false;   // tokens of another length or empty fields: the caller runs gt_general on this chunk
 }
 
 __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring &r, uint32_t *rec_bytes) {
