@@ -14,6 +14,7 @@
  *   vcfo_sparse_offset <- SparsificationConfiguration::compute_sparse_offset
  *                                                 src/sparse.cpp:18-51
  *   vcfo_sparsify      <- sparsify_file           src/sparse.cpp:290-580
+ *   vcfo_sparse_query  <- query_sparse_file_fd    src/main.cpp:235-582
  *
  * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
  * load this file's library, and only as the checker -- never as the thing that
@@ -508,4 +509,150 @@ int vcfo_sparsify(const uint8_t *in, size_t n, const char *out_path) {
     close(fd);
     /* a trailing partial header is "Failed to read line length headers" (:365-368) */
     return ip == n ? VCFO_OK : VCFO_E_FORMAT;
+}
+
+/* ------------------------------------------------------------------ */
+/* Sparse-file query: query_sparse_file_fd (src/main.cpp:235-582).      */
+/* The same lseek/read sequence on the file as the reference; each line */
+/* (decompress2_data_line_FILEwrapper, src/compress.cpp:483-739) is     */
+/* decoded by dec_line over a window of the file from the line start,  */
+/* grown until the parse ends inside it or the window reaches EOF.      */
+
+static uint64_t rd_be64(const uint8_t *b) {
+    uint64_t v = 0;
+    for (int i = 0; i < 8; i++) v = (v << 8) | b[i];
+    return v;
+}
+
+/* one line at file offset p; *end = where the parse ended */
+static int sq_decode_at(int fd, uint64_t fsize, uint64_t p, uint64_t S, uint8_t *out, size_t cap, size_t *o_io,
+                        uint64_t *end) {
+    size_t w = 1 << 16;
+    for (;;) {
+        uint64_t avail = p < fsize ? fsize - p : 0;
+        size_t n = avail < w ? (size_t)avail : w;
+        uint8_t *buf = malloc(n ? n : 1);
+        if (!buf) return VCFO_E_IO;
+        size_t got = 0;
+        while (got < n) {
+            ssize_t k = pread(fd, buf + got, n - got, (off_t)(p + got));
+            if (k <= 0) break;
+            got += (size_t)k;
+        }
+        size_t ip = 0, o = *o_io;
+        int st = dec_line(buf, got, &ip, S, out, cap, &o);
+        free(buf);
+        if (st == VCFO_OK) { *o_io = o; *end = p + ip; return VCFO_OK; }
+        if (st == VCFO_E_NOSPACE) return st;
+        /* status 0 (EOF) and < 0 both throw (main.cpp:324-328, 482-486) */
+        if (got == avail || w >= ((size_t)1 << 30)) return VCFO_E_FORMAT;
+        w *= 4;
+    }
+}
+
+int vcfo_sparse_query(const char *path, const uint8_t *qref, size_t qref_len, int has_range, uint64_t qstart,
+                      uint64_t qend, uint8_t *out, size_t cap, size_t *out_len) {
+    const off_t M = 4 * 4096;   /* multiplication_factor * block_size (sparse.hpp:29-32) */
+    size_t o = 0;
+    *out_len = 0;
+    int fd = open(path, O_RDONLY);
+    if (fd < 0) return VCFO_E_IO;   /* "Failed to open file" */
+    struct stat sb;
+    if (fstat(fd, &sb) != 0) { close(fd); return VCFO_E_IO; }
+    const uint64_t fsize = (uint64_t)sb.st_size;
+    /* decompress2_metadata_headers_fd (compress.cpp:1108-1211) over a
+     * growing prefix of the file */
+    size_t data = 0;
+    uint64_t S = 0;
+    for (size_t hn = 1 << 16;; hn *= 4) {
+        size_t n = fsize < hn ? (size_t)fsize : hn;
+        uint8_t *buf = malloc(n ? n : 1);
+        size_t got = 0, dummy = 0;
+        while (got < n) {
+            ssize_t k = pread(fd, buf + got, n - got, (off_t)got);
+            if (k <= 0) break;
+            got += (size_t)k;
+        }
+        int st = parse_headers(buf, got, NULL, 0, &dummy, &data, &S);
+        free(buf);
+        if (st == VCFO_OK) break;
+        if (got == fsize) { close(fd); return VCFO_E_FORMAT; }
+    }
+    lseek(fd, (off_t)data, SEEK_SET);
+    const off_t data_start = (off_t)data + 8;   /* main.cpp:263-267 */
+    uint64_t first_line_offset = 0;             /* host byte order (:268-272) */
+    if (read(fd, &first_line_offset, 8) < 8) { close(fd); return VCFO_E_FORMAT; }
+    const int has_criteria = qref_len > 0 || has_range;   /* has_criteria (:153-157) */
+    int st = VCFO_OK;
+    if (has_criteria && qstart == qend) {
+        /* single variant lookup (:278-333) */
+        off_t new_offset = (off_t)((uint64_t)data_start + vcfo_sparse_offset(qstart));
+        off_t init = lseek(fd, new_offset, SEEK_SET);
+        if (init != new_offset) goto done;      /* perror, return */
+        uint8_t h[16] = {0};                    /* (a short read leaves stack bytes there; zero here) */
+        ssize_t k = read(fd, h, 16);
+        if (k == 0) { st = VCFO_E_FORMAT; goto done; }
+        uint64_t dprev = rd_be64(h);            /* read in host order there: only zero-ness matters */
+        if (dprev == 0 && init != (off_t)(first_line_offset + (uint64_t)data_start)) goto done;
+        uint64_t end = 0;
+        st = sq_decode_at(fd, fsize, (uint64_t)lseek(fd, 0, SEEK_CUR), S, out, cap, &o, &end);
+        goto done;
+    } else if (has_criteria) {
+        /* range (:335-567) */
+        off_t init = lseek(fd, (off_t)((uint64_t)data_start + vcfo_sparse_offset(qstart)), SEEK_SET);
+        off_t sd = lseek(fd, init, SEEK_DATA);
+        if (sd < init) { st = VCFO_E_FORMAT; goto done; }
+        if (init != sd && (sd - data_start) % M != 0) {
+            off_t next = M - ((sd - data_start) % M);
+            off_t cur = lseek(fd, 0, SEEK_CUR);
+            if (lseek(fd, next, SEEK_CUR) != next + cur) goto done;   /* perror, return */
+        }
+        for (;;) {                                                    /* first data line (:381-421) */
+            uint8_t h[16] = {0};
+            ssize_t k = read(fd, h, 16);
+            if (k < 16) { st = VCFO_E_FORMAT; goto done; }
+            if (rd_be64(h) == 0 && init != (off_t)(first_line_offset + (uint64_t)data_start)) {
+                lseek(fd, M - 16, SEEK_CUR);
+            } else {
+                lseek(fd, -16, SEEK_CUR);
+                break;
+            }
+        }
+        for (;;) {                                                    /* linear traversal (:436-566) */
+            off_t ls = lseek(fd, 0, SEEK_CUR);
+            uint8_t h[16] = {0};
+            if (read(fd, h, 16) < 16) { st = VCFO_E_FORMAT; goto done; }
+            uint64_t dprev = rd_be64(h), dnext = rd_be64(h + 8);
+            if (dprev == 0 && dnext == 0) { st = VCFO_E_FORMAT; goto done; }
+            int eor = dnext == 0;
+            size_t o0 = o;
+            uint64_t end = 0;
+            st = sq_decode_at(fd, fsize, (uint64_t)ls + 16, S, out, cap, &o, &end);
+            if (st) goto done;
+            lseek(fd, (off_t)end, SEEK_SET);                          /* FILEwrapper's lseek to ftell (:728) */
+            dnext -= end - (uint64_t)ls;
+            /* SplitIterator(line, "\t"): CHROM, POS (split_iterator.cpp) */
+            const uint8_t *L = out + o0;
+            size_t n = o - o0, t1 = 0;
+            while (t1 < n && L[t1] != '\t') t1++;
+            if (t1 >= n) { o = o0; st = VCFO_E_FORMAT; goto done; }   /* no second term: throws */
+            size_t t2 = t1 + 1;
+            while (t2 < n && L[t2] != '\t') t2++;
+            uint64_t pos = 0;
+            if (t2 > t1 + 1 && !vcfo_strtoul_whole(L + t1 + 1, t2 - t1 - 1, &pos)) { o = o0; st = VCFO_E_FORMAT; goto done; }
+            if (t1 == qref_len && memcmp(L, qref, qref_len) == 0 && pos <= qend) {
+                if (eor || pos >= qend) goto done;
+                lseek(fd, (off_t)dnext, SEEK_CUR);
+            } else {
+                o = o0;
+                goto done;
+            }
+        }
+    } else {
+        st = VCFO_E_FORMAT;   /* "sparse query with no filter is not yet implemented" */
+    }
+done:
+    close(fd);
+    *out_len = o;
+    return st;
 }

@@ -27,6 +27,8 @@ int vcfo_query(const uint8_t *in, size_t n, const uint8_t *qref, size_t qref_len
                uint64_t qstart, uint64_t qend, uint8_t *out, size_t cap, size_t *out_len);
 uint64_t vcfo_sparse_offset(uint64_t pos);
 int vcfo_sparsify(const uint8_t *in, size_t n, const char *out_path);
+int vcfo_sparse_query(const char *path, const uint8_t *qref, size_t qref_len, int has_range, uint64_t qstart,
+                      uint64_t qend, uint8_t *out, size_t cap, size_t *out_len);
 int vcfo_strtoul_whole(const uint8_t *s, size_t n, uint64_t *out);
 #ifdef __cplusplus
 }

@@ -117,3 +117,79 @@ def query_cases():
     for c in d["cases"]:
         f = c["file"]
         yield c, files[f] if f in files else gz(f)
+
+
+def oracle_sparse_query(path, q, cap=1 << 26):
+    """query_sparse_file_fd over a sparse file: (status, stdout bytes)."""
+    lib = oracle()
+    if not hasattr(lib, "_sq"):
+        lib.vcfo_sparse_query.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int,
+                                          ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_size_t,
+                                          ctypes.POINTER(ctypes.c_size_t)]
+        lib._sq = True
+    ref, hr, a, b = oracle_parse_query(q)
+    buf = ctypes.create_string_buffer(cap)
+    n = ctypes.c_size_t(0)
+    st = lib.vcfo_sparse_query(path.encode(), ref, len(ref), int(hr), a, b, buf, cap, ctypes.byref(n))
+    return st, buf.raw[:n.value]
+
+
+def oracle_sparsify(vcfc, path):
+    st = oracle().vcfo_sparsify(vcfc, len(vcfc), path.encode())
+    assert st == 0, st
+
+
+def _header_end(v):
+    p = 0
+    while v[p:p + 1] == b"#":
+        p = v.index(b"\n", p) + 1
+    return p
+
+
+def _samples_delta(v, delta):
+    h = _header_end(v)
+    lines = v[:h].split(b"\n")[:-1]
+    cols = lines[-1].split(b"\t")
+    cols = cols + [b"EXTRA"] * delta if delta > 0 else cols[:len(cols) + delta]
+    lines[-1] = b"\t".join(cols)
+    return b"\n".join(lines) + b"\n" + v[h:]
+
+
+def sparse_query_cases():
+    """json of tests/golden/sparse_query_cases.json."""
+    return json.load(open(os.path.join(GOLDEN, "sparse_query_cases.json")))
+
+
+def build_sparse_file(d, name, path, sparsify):
+    """Recreate sparse file `name` of the sparse-query goldens at `path`:
+    sparsify(vcfc_bytes, path) (this build's or the oracle's), then the
+    recorded patches and truncation."""
+    spec = d["files"][name]
+    base = d["bases"][spec["base"]]
+    src = base["vcfc"]
+    if src.startswith("inline:"):
+        v = dict((k, bytes.fromhex(x)) for k, x in json.load(open(os.path.join(GOLDEN, "query_cases.json")))
+                 ["inline_files"].items())[src[7:]]
+    else:
+        v = gz(src)
+    if base["samples_delta"]:
+        v = _samples_delta(v, base["samples_delta"])
+    sparsify(v, path)
+    with open(path, "r+b") as f:
+        for off, hx in spec["patches"]:
+            f.seek(off)
+            f.write(bytes.fromhex(hx))
+        if spec["truncate"] is not None:
+            f.truncate(spec["truncate"])
+
+
+def check_sparse_case(c, st, out):
+    """A result against a golden case: exact stdout when the reference exits
+    0; where it aborts (uncaught throw: rc -6/134), the reference's stdout is
+    the flushed prefix of the lines before the throw, so ours must extend it
+    and report VCFC_E_FORMAT (8)."""
+    import hashlib
+    if c["rc"] == 0:
+        return st == 0 and len(out) == c["stdout_len"] and hashlib.sha256(out).hexdigest() == c["stdout_sha256"]
+    return st == 8 and len(out) >= c["stdout_len"] and \
+        hashlib.sha256(out[:c["stdout_len"]]).hexdigest() == c["stdout_sha256"]
