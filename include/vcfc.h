@@ -192,6 +192,17 @@ int vcfc_query_match_device(const uint8_t *d_in, const uint64_t *d_rec_start, ui
  * between records).  The GPU plans offsets and prefixes; the host writes. */
 uint64_t vcfc_sparse_offset(uint64_t pos);
 int vcfc_sparsify_file(vcfc_ctx *ctx, const char *in_vcfc, const char *out_sparse);
+/* Sparse-file query: query_sparse_file_fd (reference src/main.cpp:235-582)
+ * over a file written by sparsify, stdout-identical to the reference's
+ * `main sparse-query`: start == end looks up the one slot of `start` and
+ * writes its line unfiltered; otherwise the lines from the first record at or
+ * after start's slot while CHROM equals `ref` and POS <= end (no filter at
+ * all: the reference throws).  Lines go to out_fd as they are decoded (on the
+ * GPU).  VCFC_E_FORMAT where the reference throws (every line it writes
+ * before is written); VCFC_E_IO when the file does not open. */
+int vcfc_sparse_query_file(vcfc_ctx *ctx, const char *in_sparse, const char *ref, uint64_t ref_len, int has_range,
+                           uint64_t start, uint64_t end, int out_fd);
+
 /* Device plan: records d_recs[d_rec_off[i] .. d_rec_off[i+1]); outputs
  * d_file_off[i] and d_prefix16[16 i ..]; d_status[0] = ~0 or (row << 8 |
  * VCFC_E_FORMAT) of the first record whose POS does not parse, d_status[1] =

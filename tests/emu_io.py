@@ -26,6 +26,7 @@ def lib():
         u64 = ctypes.c_uint64
         L.emu_query.argtypes = [ctypes.c_char_p, u64, ctypes.c_char_p, u64, ctypes.c_int, u64, u64, vp, u64,
                                 ctypes.POINTER(u64), u64]
+        L.emu_sparse_query.argtypes = [ctypes.c_char_p, ctypes.c_char_p, u64, ctypes.c_int, u64, u64, ctypes.c_int]
         L.emu_compress.argtypes = [ctypes.c_char_p, u64, vp, u64, ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_int64),
                                    u64, ctypes.c_int]
         _lib = L
@@ -103,6 +104,15 @@ def emu_query(data, ref, has_range, start, end, out_batch=1 << 16, cap=None):
     st = lib().emu_query(data, len(data), ref, len(ref), int(has_range), start, end, out.ctypes.data, cap,
                          ctypes.byref(n), out_batch)
     return st, out[:n.value].tobytes()
+
+
+def emu_sparse_query(path, ref, has_range, start, end):
+    """The product sparse-query driver + kernels on the emulator: (status, bytes)."""
+    import tempfile
+    with tempfile.TemporaryFile() as f:
+        st = lib().emu_sparse_query(path.encode(), ref, len(ref), int(has_range), start, end, f.fileno())
+        f.seek(0)
+        return st, f.read()
 
 
 def emu_compress(vcf, chunk=4096, read_threads=2, cap=None):

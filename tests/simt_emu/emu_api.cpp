@@ -100,6 +100,22 @@ extern "C" int emu_query(const uint8_t *in, uint64_t n, const uint8_t *ref, uint
     return st;
 }
 
+// Sparse-file query through the product driver (vcfc_dec::sparse_query) on a
+// real file; lines to out_fd.
+#include <fcntl.h>
+extern "C" int emu_sparse_query(const char *path, const uint8_t *ref, uint64_t ref_len, int has_range,
+                                uint64_t qstart, uint64_t qend, int out_fd) {
+    const int fd = open(path, O_RDONLY);
+    if (fd < 0) return vcfc_dec::ST_E_IO;
+    auto sink = [&](const uint8_t *p, uint64_t k) { return write(out_fd, p, k) == (ssize_t)k; };
+    vcfc_dec::SparseQuery q;
+    q.ref = ref; q.ref_len = ref_len; q.has_range = has_range; q.start = qstart; q.end = qend;
+    HostBuffers B;
+    const int st = vcfc_dec::sparse_query(fd, q, B, nullptr, sink);
+    close(fd);
+    return st;
+}
+
 // Pipelined compress() through the product driver (vcfc_ing::compress_stream)
 // with a small chunk size, so carries across chunks and the '#' line
 // interleave are exercised on small inputs.

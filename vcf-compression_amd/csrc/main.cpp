@@ -1,6 +1,6 @@
 // main.cpp -- CLI with the reference's argv contract (src/main.cpp:4028-4185)
 // for the codec path: `main compress|decompress|sparsify <in> <out>` and
-// `main query <in> <query>`.  Data lines are
+// `main query|sparse-query <in> <query>`.  Data lines are
 // encoded on the GPU through libvcfc.so.  Error messages mirror the
 // reference's exceptions (which terminate the reference process).
 #include <cstdio>
@@ -12,7 +12,7 @@
 
 static int usage() {
     fprintf(stderr, "./main [compress|decompress|sparsify] <input_file> <output_file>\n"
-                    "./main query <input_file> <ref>[:<start>-<end>]\n");
+                    "./main [query|sparse-query] <input_file> <ref>[:<start>-<end>]\n");
     return 1;
 }
 
@@ -115,11 +115,13 @@ int main(int argc, char **argv) {
         }
         return 0;
     }
-    if (action == "query") {
+    if (action == "query" || action == "sparse-query") {
         // src/main.cpp:4057-4069 -> parse_coordinate_string (:3993-4026),
-        // query_compressed_file (:3777-3929); matching lines go to stdout
+        // query_compressed_file (:3777-3929); src/main.cpp:4086-4096 ->
+        // query_sparse_file_fd (:235-582).  Matching lines go to stdout.
+        const bool sparse = action == "sparse-query";
         if (argc < 4) return usage();
-        if (!file_exists(argv[2])) printf("Input file does not exist: %s\n", argv[2]);
+        if (!sparse && !file_exists(argv[2])) printf("Input file does not exist: %s\n", argv[2]);
         const std::string q(argv[3]);
         uint64_t ref_len = 0, start = 0, end = 0;
         int has_range = 0;
@@ -139,8 +141,15 @@ int main(int argc, char **argv) {
             return 1;
         }
         fflush(stdout);
-        st = vcfc_query_file(ctx, argv[2], q.data(), ref_len, has_range, start, end, 1);
+        st = sparse ? vcfc_sparse_query_file(ctx, argv[2], q.data(), ref_len, has_range, start, end, 1)
+                    : vcfc_query_file(ctx, argv[2], q.data(), ref_len, has_range, start, end, 1);
         vcfc_ctx_destroy(ctx);
+        if (st == VCFC_E_IO && sparse) {
+            perror("open");
+            fprintf(stderr, "terminate called after throwing an instance of 'std::runtime_error'\n"
+                            "  what():  Failed to open file: %s\n", argv[2]);
+            return 134;
+        }
         if (st != VCFC_OK) {
             fprintf(stderr, "terminate called after throwing an instance of 'VcfValidationError'\n"
                             "  what():  %s\n", vcfc_strerror(st));

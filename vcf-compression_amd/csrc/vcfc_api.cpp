@@ -727,6 +727,32 @@ int vcfc_query_file(vcfc_ctx *c, const char *in_path, const char *ref, uint64_t 
                                    has_range, start, end, B, c->stream, sink);
 }
 
+// ---- sparse-file query: query_sparse_file_fd, reference
+// src/main.cpp:235-582 ------------------------------------------------------
+int vcfc_sparse_query_file(vcfc_ctx *c, const char *in_path, const char *ref, uint64_t ref_len, int has_range,
+                           uint64_t start, uint64_t end, int out_fd) {
+    if (!c || !in_path || (!ref && ref_len) || out_fd < 0) return VCFC_E_ARG;
+    if (hipSetDevice(c->device) != hipSuccess) return VCFC_E_HIP;
+    const int fd = open(in_path, O_RDONLY);
+    if (fd < 0) return VCFC_E_IO;
+    auto sink = [&](const uint8_t *p, uint64_t k) {
+        while (k) {
+            const ssize_t w = write(out_fd, p, std::min<uint64_t>(k, 1ull << 30));
+            if (w <= 0) return false;
+            p += w;
+            k -= (uint64_t)w;
+        }
+        return true;
+    };
+    vcfc_dec::SparseQuery q;
+    q.ref = reinterpret_cast<const uint8_t *>(ref); q.ref_len = ref_len; q.has_range = has_range;
+    q.start = start; q.end = end;
+    CtxDecodeBuffers B(c);
+    const int st = vcfc_dec::sparse_query(fd, q, B, c->stream, sink);
+    close(fd);
+    return st;
+}
+
 int vcfc_query_match_device(const uint8_t *d_in, const uint64_t *d_rec_start, uint64_t n, const uint8_t *d_ref,
                             uint64_t ref_len, int has_range, uint64_t start, uint64_t end, uint8_t *d_flag,
                             uint64_t *d_err, void *stream) {

@@ -481,15 +481,16 @@ __global__ __launch_bounds__(256) void k_dec_write(VcfcDecodeArgs a, uint64_t fi
         write_one(a, first + g + (uint64_t)__builtin_ctzll(m) * G, sb, W);
 }
 
-// Byte-serial decode of [p, n): mode 0 counts (lines, bytes, end state),
-// mode 1 writes.  One lane.  st[0] = DL_END (clean end) or DL_ERR; st[1] =
-// bytes; st[2] = lines.
-__global__ void k_dec_stream(const uint8_t *in, uint64_t n, uint64_t p, uint64_t S, uint8_t *out,
+// Byte-serial decode of [p, n), at most max_lines lines: out == nullptr
+// counts (lines, bytes, end state), else writes.  One lane.  st[0] = DL_OK
+// (max_lines reached), DL_END (clean end) or DL_ERR; st[1] = bytes; st[2] =
+// lines; st[3] = where the parse stopped.
+__global__ void k_dec_stream(const uint8_t *in, uint64_t n, uint64_t p, uint64_t S, uint64_t max_lines, uint8_t *out,
                              uint64_t *st) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     uint64_t o = 0, lines = 0;
-    int r;
-    for (;;) {
+    int r = DL_OK;
+    while (lines < max_lines) {
         uint64_t size = 0, end = 0;
         r = dec_line_seq(in, n, p, S, out ? out + o : nullptr, &size, &end);
         if (r != DL_OK) break;
@@ -500,6 +501,7 @@ __global__ void k_dec_stream(const uint8_t *in, uint64_t n, uint64_t p, uint64_t
     st[0] = (uint64_t)r;
     st[1] = o;
     st[2] = lines;
+    st[3] = p;
 }
 
 
@@ -688,9 +690,9 @@ hipError_t vcfc_decode_write(const VcfcDecodeArgs &a, uint64_t first, uint64_t l
     return hipGetLastError();
 }
 
-hipError_t vcfc_decode_stream(const uint8_t *in, uint64_t n, uint64_t p, uint64_t S, uint8_t *out, uint64_t *st,
-                              hipStream_t s) {
-    hipLaunchKernelGGL(k_dec_stream, dim3(1), dim3(64), 0, s, in, n, p, S, out, st);
+hipError_t vcfc_decode_stream(const uint8_t *in, uint64_t n, uint64_t p, uint64_t S, uint64_t max_lines,
+                              uint8_t *out, uint64_t *st, hipStream_t s) {
+    hipLaunchKernelGGL(k_dec_stream, dim3(1), dim3(64), 0, s, in, n, p, S, max_lines, out, st);
     return hipGetLastError();
 }
 

@@ -12,7 +12,13 @@
 //   5. VCFC_E_FORMAT where the reference throws, after sinking every line
 //      the reference would have written first.
 #pragma once
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
 #include <cstdint>
+#include <cstring>
 #include <functional>
 #include <vector>
 
@@ -91,10 +97,11 @@ inline void hop(const uint8_t *in, uint64_t n, std::vector<uint64_t> &rec) {
 // get no line.  Stops early at the first record the reference would not
 // leave at its end: *stop = 1 where it throws (lines before it sunk), 2 where
 // its parse ends off the record end, at *cont (its line sunk).  *stop = 0:
-// all records decoded.
+// all records decoded.  line_end (optional): the end of every sunk line,
+// counted from the first byte this call sinks.
 inline int decode_records(const uint8_t *d_in, uint64_t n, uint64_t S, const uint64_t *d_rec, const uint8_t *d_select,
                           uint64_t nrec, Buffers &B, hipStream_t s, const Sink &sink, uint64_t out_batch, int *stop,
-                          uint64_t *cont) {
+                          uint64_t *cont, std::vector<uint64_t> *line_end = nullptr) {
     *stop = 0;
     if (!nrec) return ST_OK;
     const VcfcDecodeLayout L = vcfc_decode_workspace_layout(nrec);
@@ -166,6 +173,8 @@ inline int decode_records(const uint8_t *d_in, uint64_t n, uint64_t S, const uin
         if (hipMemcpyAsync(host.data(), d_out, bytes, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
             return ST_E_HIP;
         if (!sink(host.data(), bytes)) return ST_E_IO;
+        if (line_end)
+            for (uint64_t i = i0; i < i1; i++) line_end->push_back(loff[i + 1] - loff[0]);
         i0 = i1;
     }
     return ST_OK;
@@ -214,7 +223,7 @@ inline int decode_section(const uint8_t *h_in, uint64_t n, uint64_t S, Buffers &
     if (st) return st;
     if (stop == 1) return ST_E_FORMAT;
     if (n - p_stream < 8) return ST_OK;   // clean end (:768-774)
-    return stream_tail(B, s, sink, [&](uint8_t *out, uint64_t *dst) { return vcfc_decode_stream(d_in, n, p_stream, S, out, dst, s); });
+    return stream_tail(B, s, sink, [&](uint8_t *out, uint64_t *dst) { return vcfc_decode_stream(d_in, n, p_stream, S, ~0ull, out, dst, s); });
 }
 
 // Range query over a .vcfc data section (query_compressed_file, reference
@@ -264,6 +273,298 @@ inline int query_section(const uint8_t *h_in, uint64_t n, uint64_t S, const uint
     }
     if (p_stream >= n) return ST_OK;
     return stream_tail(B, s, sink, [&](uint8_t *out, uint64_t *dst) { return vcfc_query_stream(d_in, n, p_stream, S, q, out, dst, s); });
+}
+
+
+// ---------------------------------------------------------------------------
+// Sparse-file query: query_sparse_file_fd, reference
+// src/main.cpp:235-582, over a file written by sparsify (record i at
+// data_start + (3e8 + POS_i) * 16384 behind BE dist_to_prev / dist_to_next).
+// The walk is host I/O with the reference's own lseek/read sequence (header,
+// single-slot lookup or SEEK_DATA + slot alignment + hole skipping, then the
+// dist_to_next hops).  The lines are decoded on the GPU: the walk runs ahead
+// in geometrically growing batches of records, each batch decodes in one
+// decode_records call, and the reference's per-line verdicts (CHROM/POS of
+// the decoded line, end of range, end of reference) are then applied in
+// order.  A line whose parse leaves its record (the reference reads on into
+// the hole or the next record) is decoded again from a window of the file
+// (k_dec_stream, one line), grown until the parse ends inside it.
+struct SparseQuery {
+    const uint8_t *ref;
+    uint64_t ref_len;
+    int has_range;
+    uint64_t start, end;
+};
+
+constexpr int64_t SQ_STRIDE = 4 * 4096;   // multiplication_factor * block_size (src/sparse.hpp:29-32)
+
+inline uint64_t sq_be64(const uint8_t *b) {
+    uint64_t v = 0;
+    for (int i = 0; i < 8; i++) v = (v << 8) | b[i];
+    return v;
+}
+// compute_sparse_offset (src/sparse.cpp:18-51; the name is ignored)
+inline uint64_t sq_slot(uint64_t pos) { return (300000000ull + pos) * (uint64_t)SQ_STRIDE; }
+
+// bytes read at off (short only at EOF); -1 on a read error
+inline int64_t sq_pread(int fd, uint8_t *b, uint64_t k, uint64_t off) {
+    uint64_t got = 0;
+    while (got < k) {
+        const ssize_t r = pread(fd, b + got, std::min<uint64_t>(k - got, 1ull << 30), (off_t)(off + got));
+        if (r < 0) return -1;
+        if (r == 0) break;
+        got += (uint64_t)r;
+    }
+    return (int64_t)got;
+}
+
+// strtoul(s, &end, 10) with end == s + n required; "" is 0 (main.cpp:520-524)
+inline bool sq_strtoul_whole(const uint8_t *s, uint64_t n, uint64_t *out) {
+    if (n == 0) { *out = 0; return true; }
+    uint64_t i = 0;
+    while (i < n && (s[i] == ' ' || (s[i] >= '\t' && s[i] <= '\r'))) i++;
+    bool neg = false;
+    if (i < n && (s[i] == '+' || s[i] == '-')) { neg = s[i] == '-'; i++; }
+    if (i >= n || s[i] < '0' || s[i] > '9') return false;
+    uint64_t v = 0;
+    bool ovf = false;
+    for (; i < n && s[i] >= '0' && s[i] <= '9'; i++) {
+        const uint64_t d = (uint64_t)(s[i] - '0');
+        ovf = ovf || v > (~0ull - d) / 10;
+        v = v * 10 + d;
+    }
+    if (i != n) return false;
+    *out = ovf ? ~0ull : (neg ? 0ull - v : v);
+    return true;
+}
+
+// One line the reference's way from file offset p
+// (decompress2_data_line_FILEwrapper, src/compress.cpp:483-739), on the GPU
+// over a window of the file grown x4 until the parse ends inside it or the
+// window reaches EOF (1 GiB at most).  Appends the line, sets *end.
+inline int sq_line_window(int fd, uint64_t fsize, uint64_t p, uint64_t S, Buffers &B, hipStream_t s,
+                          std::vector<uint8_t> &line, uint64_t *end) {
+    std::vector<uint8_t> win;
+    for (uint64_t w = 1ull << 16;; w *= 4) {
+        const uint64_t avail = p < fsize ? fsize - p : 0;
+        const uint64_t n = std::min(w, avail);
+        win.resize(n);
+        const int64_t got = sq_pread(fd, win.data(), n, p);
+        if (got < 0) return ST_E_IO;
+        const uint8_t *d_win = upload(B, Buffers::FLAG, win.data(), (uint64_t)got, s);
+        uint64_t *d_small = static_cast<uint64_t *>(B.get(Buffers::SMALL, 64));
+        if (!d_win || !d_small) return ST_E_HIP;
+        uint64_t st[4] = {0, 0, 0, 0};
+        if (vcfc_decode_stream(d_win, (uint64_t)got, 0, S, 1, nullptr, d_small, s) != hipSuccess ||
+            hipMemcpyAsync(st, d_small, 32, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+            return ST_E_HIP;
+        if (st[2] == 1) {
+            uint8_t *d_out = static_cast<uint8_t *>(B.get(Buffers::OUT, st[1] + 64));
+            if (!d_out) return ST_E_HIP;
+            const uint64_t o = line.size();
+            line.resize(o + st[1]);
+            if (vcfc_decode_stream(d_win, (uint64_t)got, 0, S, 1, d_out, d_small, s) != hipSuccess ||
+                hipMemcpyAsync(line.data() + o, d_out, st[1], hipMemcpyDeviceToHost, s) != hipSuccess ||
+                hipStreamSynchronize(s) != hipSuccess)
+                return ST_E_HIP;
+            *end = p + st[3];
+            return ST_OK;
+        }
+        // EOF at the line start (status 0) and a failed parse both throw (main.cpp:324-328, 482-486)
+        if ((uint64_t)got == avail || w >= (1ull << 30)) return ST_E_FORMAT;
+    }
+}
+
+// the walk's view of one record
+struct SqRec {
+    uint64_t ls;      // line_start_offset: its 16 distance bytes
+    uint64_t dnext;   // dist_to_next (0: end of reference)
+    int walk;         // 0, or ST_E_FORMAT: the reference throws reading its distances
+    bool sync;        // the hop's lseek fails: the next read starts where this line's parse ends
+    uint64_t pre, npre;   // the first bytes from ls, read with the distances: pre[pre, + npre)
+};
+constexpr uint64_t SQ_PRE = 1024;   // bytes read per hop (holds most records whole)
+
+// Walk up to `want` records from ls (linear traversal, main.cpp:436-566):
+// stops after an end-of-reference record, a walk error, or a failing hop.
+inline int sq_walk(int fd, uint64_t ls, uint64_t want, std::vector<SqRec> &recs, std::vector<uint8_t> &pre) {
+    recs.clear();
+    pre.clear();
+    while (recs.size() < want) {
+        const uint64_t o = pre.size();
+        pre.resize(o + SQ_PRE);
+        const int64_t k = sq_pread(fd, pre.data() + o, SQ_PRE, ls);
+        if (k < 0) return ST_E_IO;
+        pre.resize(o + (uint64_t)k);
+        uint8_t h[16] = {0};
+        memcpy(h, pre.data() + o, std::min<uint64_t>(16, (uint64_t)k));
+        SqRec r;
+        r.ls = ls; r.dnext = sq_be64(h + 8); r.walk = 0; r.sync = false; r.pre = o; r.npre = (uint64_t)k;
+        if (k < 16) { r.walk = ST_E_FORMAT; recs.push_back(r); break; }                  // :454-456
+        if (sq_be64(h) == 0 && r.dnext == 0) { r.walk = ST_E_FORMAT; recs.push_back(r); break; }   // :464-466
+        const int64_t next = (int64_t)(ls + r.dnext);   // lseek64(dnext - bytes read, SEEK_CUR) lands here
+        if (r.dnext && (next < 0 || lseek(fd, (off_t)next, SEEK_SET) != (off_t)next)) r.sync = true;
+        recs.push_back(r);
+        if (r.dnext == 0 || r.sync) break;
+        ls = (uint64_t)next;
+    }
+    return ST_OK;
+}
+
+inline int sparse_query(int fd, const SparseQuery &q, Buffers &B, hipStream_t s, const Sink &sink) {
+    struct stat sb;
+    if (fstat(fd, &sb) != 0) return ST_E_IO;
+    const uint64_t fsize = (uint64_t)sb.st_size;
+    // decompress2_metadata_headers_fd (compress.cpp:1108-1211) over a growing prefix
+    uint64_t data = 0, S = 0;
+    std::vector<uint8_t> hb;
+    for (uint64_t hn = 1ull << 16;; hn *= 4) {
+        hb.resize(std::min(hn, fsize));
+        const int64_t got = sq_pread(fd, hb.data(), hb.size(), 0);
+        if (got < 0) return ST_E_IO;
+        if (parse_header(hb.data(), (uint64_t)got, &data, &S) == ST_OK) break;
+        if ((uint64_t)got >= fsize) return ST_E_FORMAT;
+    }
+    const int64_t data_start = (int64_t)data + 8;   // main.cpp:263-267
+    uint8_t fb[8] = {0};
+    if (sq_pread(fd, fb, 8, data) < 8) return ST_E_FORMAT;   // :268-272
+    uint64_t first = 0;
+    for (int i = 7; i >= 0; i--) first = (first << 8) | fb[i];   // host (little-endian) order
+    const bool has_criteria = q.ref_len > 0 || q.has_range;
+    if (!has_criteria) return ST_E_FORMAT;   // "sparse query with no filter is not yet implemented"
+    std::vector<uint8_t> line;
+    if (q.start == q.end) {
+        // single variant lookup (:278-333): the line at the slot, unfiltered
+        const off_t nw = (off_t)((uint64_t)data_start + sq_slot(q.start));
+        if (lseek(fd, nw, SEEK_SET) != nw) return ST_OK;   // perror, return
+        uint8_t h[16] = {0};   // (a short read leaves stack bytes there; zero here)
+        const int64_t k = sq_pread(fd, h, 16, (uint64_t)nw);
+        if (k < 0) return ST_E_IO;
+        if (k == 0) return ST_E_FORMAT;   // "Reached end of file unexpectedly"
+        if (sq_be64(h) == 0 && nw != (off_t)(first + (uint64_t)data_start)) return ST_OK;
+        uint64_t end = 0;
+        const int st = sq_line_window(fd, fsize, (uint64_t)nw + (uint64_t)k, S, B, s, line, &end);
+        if (st) return st;
+        return sink(line.data(), line.size()) ? ST_OK : ST_E_IO;
+    }
+    // range (:335-421): the slot of start, SEEK_DATA, the next slot boundary,
+    // then slots whose dist_to_prev is 0 are holes (unless the first line's)
+    const off_t init = lseek(fd, (off_t)((uint64_t)data_start + sq_slot(q.start)), SEEK_SET);
+    const off_t sd = lseek(fd, init, SEEK_DATA);
+    if (sd < init) return ST_E_FORMAT;
+    if (init != sd && (sd - data_start) % SQ_STRIDE != 0) {
+        const off_t nx = SQ_STRIDE - ((sd - data_start) % SQ_STRIDE);
+        const off_t cur = lseek(fd, 0, SEEK_CUR);
+        if (lseek(fd, nx, SEEK_CUR) != nx + cur) return ST_OK;   // perror, return
+    }
+    for (;;) {
+        uint8_t h[16] = {0};
+        const ssize_t k = read(fd, h, 16);
+        if (k < 16) return ST_E_FORMAT;
+        if (sq_be64(h) == 0 && init != (off_t)(first + (uint64_t)data_start)) {
+            lseek(fd, SQ_STRIDE - 16, SEEK_CUR);
+        } else {
+            lseek(fd, -16, SEEK_CUR);
+            break;
+        }
+    }
+    uint64_t ls = (uint64_t)lseek(fd, 0, SEEK_CUR);
+    // linear traversal (:436-566) in batches
+    std::vector<SqRec> recs;
+    std::vector<uint8_t> pre, hbuf, lines;
+    std::vector<uint64_t> roff, lend, lineof, pend;
+    std::vector<int> lst;
+    for (uint64_t want = 32;; want = std::min<uint64_t>(want * 4, 1ull << 16)) {
+        int st = sq_walk(fd, ls, want, recs, pre);
+        if (st) return st;
+        const uint64_t nr = recs.size();
+        // record bytes [ls + 16, + 4 + LEN) of the records with sane headers
+        hbuf.clear(); roff.clear();
+        std::vector<uint64_t> reg;   // record index of each regular record
+        lst.assign(nr, ST_OK);
+        pend.assign(nr, 0);
+        for (uint64_t i = 0; i < nr; i++) {
+            if (recs[i].walk) break;
+            const SqRec &r = recs[i];
+            const uint64_t rs = r.ls + 16;
+            if (r.npre < 24) continue;
+            const uint8_t *h8 = pre.data() + r.pre + 16;
+            if ((h8[0] >> 6) != 3u || (h8[4] >> 6) != 3u) continue;
+            const uint64_t L = ((uint64_t)(h8[0] & 0x3Fu) << 24) | ((uint64_t)h8[1] << 16) | ((uint64_t)h8[2] << 8) | h8[3];
+            if (L < 4) continue;
+            const uint64_t o = hbuf.size();
+            hbuf.resize(o + 4 + L);
+            if (20 + L <= r.npre) {
+                memcpy(hbuf.data() + o, h8, 4 + L);
+            } else if (sq_pread(fd, hbuf.data() + o, 4 + L, rs) != (int64_t)(4 + L)) {
+                hbuf.resize(o);
+                continue;
+            }
+            roff.push_back(o);
+            reg.push_back(i);
+        }
+        // decode the regular records on the GPU; lines[lineof[i], lineof[i + 1]) of record i
+        lines.clear();
+        std::vector<uint64_t> lo(nr, ~0ull), le(nr, 0);
+        const uint64_t nreg = reg.size();
+        if (nreg) {
+            roff.push_back(hbuf.size());
+            const uint8_t *d_in = upload(B, Buffers::IN, hbuf.data(), hbuf.size(), s);
+            const uint64_t *d_rec = reinterpret_cast<const uint64_t *>(
+                upload(B, Buffers::REC, reinterpret_cast<const uint8_t *>(roff.data()), 8 * roff.size(), s));
+            if (!d_in || !d_rec) return ST_E_HIP;
+            uint64_t j0 = 0;
+            while (j0 < nreg) {
+                int stop = 0;
+                uint64_t cont = 0;
+                lend.clear();
+                const uint64_t base = lines.size();
+                auto lsink = [&](const uint8_t *p, uint64_t k) { lines.insert(lines.end(), p, p + k); return true; };
+                st = decode_records(d_in, hbuf.size(), S, d_rec + j0, nullptr, nreg - j0, B, s, lsink, 1ull << 30,
+                                    &stop, &cont, &lend);
+                if (st) return st;
+                uint64_t got = lend.size();
+                if (stop == 2) { got--; lines.resize(base + (got ? lend[got - 1] : 0)); }   // its line read past the record
+                for (uint64_t k = 0; k < got; k++) {
+                    const uint64_t i = reg[j0 + k];
+                    lo[i] = base + (k ? lend[k - 1] : 0);
+                    le[i] = base + lend[k];
+                    pend[i] = recs[i].ls + 16 + (roff[j0 + k + 1] - roff[j0 + k]);
+                }
+                if (stop == 0) break;
+                j0 += got + 1;   // the stopping record: window path below
+            }
+        }
+        // evaluate in order
+        for (uint64_t i = 0; i < nr; i++) {
+            const SqRec &r = recs[i];
+            if (r.walk) return r.walk;
+            const uint8_t *L;
+            uint64_t n;
+            std::vector<uint8_t> one;
+            if (lo[i] != ~0ull) {
+                L = lines.data() + lo[i];
+                n = le[i] - lo[i];
+            } else {
+                if ((st = sq_line_window(fd, fsize, r.ls + 16, S, B, s, one, &pend[i]))) return st;
+                L = one.data();
+                n = one.size();
+            }
+            // SplitIterator(line, "\t"): CHROM, POS (split_iterator.cpp); strtoul whole (:520-524)
+            uint64_t t1 = 0;
+            while (t1 < n && L[t1] != '\t') t1++;
+            if (t1 >= n) return ST_E_FORMAT;   // no second term
+            uint64_t t2 = t1 + 1;
+            while (t2 < n && L[t2] != '\t') t2++;
+            uint64_t pos = 0;
+            if (!sq_strtoul_whole(L + t1 + 1, t2 - t1 - 1, &pos)) return ST_E_FORMAT;
+            if (!(t1 == q.ref_len && memcmp(L, q.ref, q.ref_len) == 0 && pos <= q.end)) return ST_OK;
+            if (!sink(L, n)) return ST_E_IO;
+            if (r.dnext == 0 || pos >= q.end) return ST_OK;
+            if (r.sync) ls = pend[i];   // the failed lseek leaves the parse end
+            else ls = r.ls + r.dnext;
+        }
+    }
 }
 
 }  // namespace vcfc_dec

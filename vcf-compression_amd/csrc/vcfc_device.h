@@ -94,10 +94,11 @@ VcfcDecodeLayout vcfc_decode_workspace_layout(uint64_t n);
 hipError_t vcfc_decode_plan(const VcfcDecodeArgs &a, bool exact, hipStream_t s);
 // write lines [first, last) at a.out + line_off[i] (their plan status must not be an error)
 hipError_t vcfc_decode_write(const VcfcDecodeArgs &a, uint64_t first, uint64_t last, hipStream_t s);
-// one-lane byte-serial decode of in[p, n): out == nullptr counts; st[0..2] =
-// {0 clean end | 2 reference error, bytes, lines}
-hipError_t vcfc_decode_stream(const uint8_t *in, uint64_t n, uint64_t p, uint64_t S, uint8_t *out, uint64_t *st,
-                              hipStream_t s);
+// one-lane byte-serial decode of in[p, n), at most max_lines lines: out ==
+// nullptr counts; st[0..3] = {0 max_lines reached | 1 clean end | 2 reference
+// error, bytes, lines, parse end}
+hipError_t vcfc_decode_stream(const uint8_t *in, uint64_t n, uint64_t p, uint64_t S, uint64_t max_lines,
+                              uint8_t *out, uint64_t *st, hipStream_t s);
 // exclusive u32 -> u64 scan with out[n] = total (shared with the encoder)
 hipError_t vcfc_scan_u32(const uint32_t *in, uint64_t n, uint64_t *partials, uint64_t *out, hipStream_t s);
 

@@ -34,7 +34,7 @@ EXPORTS = [
     "vcfc_sparse_offset", "vcfc_sparsify_file", "vcfc_sparse_plan_device",
     "vcfc_decompress_buffer", "vcfc_decompress_file", "vcfc_decode_workspace_size",
     "vcfc_decode_records_device", "vcfc_parse_query", "vcfc_query_buffer", "vcfc_query_file",
-    "vcfc_query_match_device", "vcfc_decode_selected_device",
+    "vcfc_query_match_device", "vcfc_decode_selected_device", "vcfc_sparse_query_file",
 ]
 
 
@@ -95,6 +95,8 @@ def lib():
     L.vcfc_query_file.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, u64, ctypes.c_int, u64, u64, ctypes.c_int]
     L.vcfc_decode_selected_device.argtypes = [vp, u64, vp, vp, u64, u64, vp, u64, vp, vp, u64, vp, ctypes.c_int, vp]
     L.vcfc_query_match_device.argtypes = [vp, vp, u64, vp, u64, ctypes.c_int, u64, u64, vp, vp, vp]
+    L.vcfc_sparse_query_file.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, u64, ctypes.c_int, u64, u64,
+                                         ctypes.c_int]
     _lib = L
     return L
 
@@ -250,6 +252,28 @@ class Context:
             query = parse_coordinate_string(query)
         raise_for(lib().vcfc_query_file(self._h, in_path.encode(), query.reference_name, len(query.reference_name),
                                         int(query.has_range), query.start, query.end, out_fd))
+
+    def sparse_query_status(self, in_path, query):
+        """query_sparse_file_fd (reference src/main.cpp:235-582) over a sparse
+        file: (status, stdout bytes); E_FORMAT where the reference throws (the
+        bytes are every line it writes before)."""
+        import tempfile
+        if not isinstance(query, VcfCoordinateQuery):
+            query = parse_coordinate_string(query)
+        with tempfile.TemporaryFile() as f:
+            st = lib().vcfc_sparse_query_file(self._h, in_path.encode(), query.reference_name,
+                                              len(query.reference_name), int(query.has_range), query.start,
+                                              query.end, f.fileno())
+            f.seek(0)
+            return st, f.read()
+
+    def sparse_query_file(self, in_path, query, out_fd=1):
+        """Lines of a sparse file written to out_fd, as `main sparse-query`."""
+        if not isinstance(query, VcfCoordinateQuery):
+            query = parse_coordinate_string(query)
+        raise_for(lib().vcfc_sparse_query_file(self._h, in_path.encode(), query.reference_name,
+                                               len(query.reference_name), int(query.has_range), query.start,
+                                               query.end, out_fd))
 
     def sparsify_file(self, in_path, out_path):
         """sparsify_file (reference src/sparse.cpp:290-580)."""
