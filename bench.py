@@ -46,10 +46,12 @@ def parse():
                     help="rows in the CPU-baseline sample (default: about 1.2 GB of lines)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify-rows", type=int, default=64, help="rows checked against the CPU path")
-    ap.add_argument("--mode", choices=["encode", "biobank", "decode", "query", "ingest"], default="encode",
+    ap.add_argument("--mode", choices=["encode", "biobank", "decode", "query", "ingest", "sparse"], default="encode",
                     help="encode = the headline (BASELINE metric, configs[1]); biobank = configs[3] "
                          "(100k samples, one 100k-row batch of a 5M-row shard per GPU); decode = row f1; "
-                         "query = row f2; ingest = row f4 (end-to-end file compress, configs[2])")
+                         "query = row f2; ingest = row f4 (end-to-end file compress, configs[2]); "
+                         "sparse = rows a7-a9 + f3 (sparsify, sparse-file query)")
+    ap.add_argument("--sparse-rows", type=int, default=200_000, help="rows of the --mode sparse file")
     ap.add_argument("--ingest-rows", type=int, default=200_000, help="rows of the --mode ingest file")
     ap.add_argument("--query-frac", type=float, default=0.125, help="rows selected by the --mode query range")
     a = ap.parse_args()
@@ -391,13 +393,101 @@ def bench_ingest(args, torch, vcfc, workload):
         os.rmdir(tmp)
 
 
+def bench_sparse(args, torch, vcfc, workload):
+    """Rows a7-a9 + f3: `sparsify` of a .vcfc file (GPU plan + one pwritev
+    per record) and `sparse-query` of the middle --query-frac of its rows
+    (host walk of the dist_to_next hops, GPU decode of the walked records)
+    over --sparse-rows GPU-encoded rows.  Both are file -> file paths bound by
+    host I/O (one pread / pwrite per record), so there is no kernel roofline;
+    the reference CLI runs beside them on the same files."""
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    args.rows = args.sparse_rows
+    n, S = args.rows, args.samples
+    rows, recs, rec, rec_bytes = encoded_shard(args, torch, vcfc, workload, dev)
+    header = sample_header(S)
+    tmp = tempfile.mkdtemp(dir="/tmp")
+    src, sp = os.path.join(tmp, "in.vcfc"), os.path.join(tmp, "out.sparse")
+    with open(src, "wb") as f:
+        f.write(header)
+        f.write(recs[:rec_bytes].cpu().numpy().tobytes())
+    del recs
+    a = int(n * (0.5 - args.query_frac / 2))
+    b = min(n - 1, a + max(1, int(n * args.query_frac)) - 1)
+    q = "%s:%d-%d" % (rows.chrom, int(rows.pos[a]), int(rows.pos[b]))
+    lo = rows.line_off.cpu().numpy()
+    want = rows.buf[int(lo[a]):int(lo[b + 1]) if b + 1 < n else rows.total_bytes].cpu().numpy().tobytes()
+    ref = os.path.join(REPO, "oracle", "_ref", "main")
+    try:
+        with vcfc.Context(0) as ctx:
+            ts = []
+            for k in range(max(1, args.warmup) + 3):
+                if os.path.exists(sp):
+                    os.unlink(sp)
+                t0 = time.perf_counter()
+                ctx.sparsify_file(src, sp)
+                ts.append(time.perf_counter() - t0)
+            t_sp = min(ts[max(1, args.warmup):])
+            qp = os.path.join(tmp, "q.out")
+            for _ in range(args.warmup):
+                st, got = ctx.sparse_query_status(sp, q)
+            identical = st == 0 and got == want
+            fd = os.open(qp, os.O_CREAT | os.O_TRUNC | os.O_WRONLY, 0o600)
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                os.ftruncate(fd, 0)
+                os.lseek(fd, 0, 0)
+                ctx.sparse_query_file(sp, q, fd)
+            elapsed = time.perf_counter() - t0
+            os.close(fd)
+        res = {"metric": "sparse-query output VCF bytes/sec over a sparsified 2504-sample .vcfc (rows a7-a9, f3)",
+               "value": round(len(want) * args.steps / elapsed / 1e9, 3), "unit": "GB/s", "n_gpus": 1,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
+               "higher_is_better": True, "scaling": "replicas", "vs_baseline": None, "dtype": "u8",
+               "data": "synthetic (generated and encoded in HBM, files in the page cache)",
+               "config": {"workload": "chr22-shaped %d samples x %d variants, sparse-query %s (%d records)"
+                                      % (S, n, q, b - a + 1),
+                          "vcfc_bytes": len(header) + rec_bytes, "query_output_bytes": len(want)},
+               "records_per_sec": round((b - a + 1) * args.steps / elapsed, 1),
+               "sparsify": {"seconds": round(t_sp, 4), "records_per_sec": round(n / t_sp, 1),
+                            "vcfc_bytes_per_sec": round((len(header) + rec_bytes) / t_sp / 1e9, 4)},
+               "roofline": None, "roofline_note": "host-I/O bound: one pread (query) / pwritev (sparsify) per record",
+               "output_identical_to_selected_rows": identical}
+        if not args.no_cpu_baseline and os.path.exists(ref):
+            with open(os.path.join(tmp, "r.out"), "wb") as so:
+                t0 = time.perf_counter()
+                r = subprocess.run([ref, "sparse-query", sp, q], stdout=so, stderr=subprocess.PIPE)
+                dt = time.perf_counter() - t0
+            same = r.returncode == 0 and open(os.path.join(tmp, "r.out"), "rb").read() == want
+            k = min(n, 3000)
+            ksrc, ksp = os.path.join(tmp, "k.vcfc"), os.path.join(tmp, "k.sparse")
+            with open(src, "rb") as f:
+                kb = f.read(len(header) + int(rec[k].item()))
+            with open(ksrc, "wb") as f:
+                f.write(kb)
+            t0 = time.perf_counter()
+            r2 = subprocess.run([ref, "sparsify", ksrc, ksp], capture_output=True)
+            dt2 = time.perf_counter() - t0
+            res["cpu_baseline"] = {"value": round(len(want) / dt / 1e9, 4), "unit": "GB/s", "cores": 1,
+                                   "kind": "reference",
+                                   "sample": "`main sparse-query %s` on the same sparse file, wall time %.3f s" % (q, dt),
+                                   "output_identical": same,
+                                   "sparsify": {"records": k, "seconds": round(dt2, 3),
+                                                "records_per_sec": round(k / dt2, 1), "rc": r2.returncode}}
+        print(json.dumps(res), flush=True)
+    finally:
+        for f in os.listdir(tmp):
+            os.unlink(os.path.join(tmp, f))
+        os.rmdir(tmp)
+
+
 def main():
     args = parse()
     if args.mode not in ("encode", "biobank"):
         import torch
         import vcfc
         import workload
-        fn = {"decode": bench_decode, "query": bench_query, "ingest": bench_ingest}[args.mode]
+        fn = {"decode": bench_decode, "query": bench_query, "ingest": bench_ingest, "sparse": bench_sparse}[args.mode]
         return fn(args, torch, vcfc, workload)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -22,6 +22,7 @@ for s in $STEPS; do
     profbio) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/profbio" -o run -- python3 "$R/bench.py" --mode biobank --steps 3 --warmup 1 --no-cpu-baseline > "$O/profbio.log" 2>&1) || { echo "profbio failed rc=$?"; tail -30 "$O/profbio.log"; exit 1; } ;;
     wtests) timeout -k 10 900 python -u -m pytest tests/test_gpu_encode.py -x -v -k synthetic -p no:cacheprovider --timeout 300 --timeout-method thread > "$O/pytest_w.log" 2>&1 || { echo "wtests failed rc=$?"; tail -40 "$O/pytest_w.log"; exit 1; } ;;
     benchdec) timeout -k 10 600 python bench.py --mode decode > "$O/bench_decode.json" 2> "$O/bench_decode.err" || { echo "benchdec failed"; tail -30 "$O/bench_decode.err"; exit 1; } ; cat "$O/bench_decode.json" ;;
+    benchsp) timeout -k 10 900 python bench.py --mode sparse --steps 5 --warmup 1 > "$O/bench_sparse.json" 2> "$O/bench_sparse.err" || { echo "benchsp failed"; tail -30 "$O/bench_sparse.err"; exit 1; } ; cat "$O/bench_sparse.json" ;;
     benchq) timeout -k 10 600 python bench.py --mode query > "$O/bench_query.json" 2> "$O/bench_query.err" || { echo "benchq failed"; tail -30 "$O/bench_query.err"; exit 1; } ; cat "$O/bench_query.json" ;;
     profq) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/profq" -o run -- python3 "$R/bench.py" --mode query --steps 10 --warmup 2 --no-cpu-baseline > "$O/profq.log" 2>&1) || { echo "profq failed rc=$?"; tail -30 "$O/profq.log"; exit 1; } ;;
     qtests) timeout -k 10 900 python -m pytest tests/test_gpu_query.py tests/test_gpu_decode.py -x -q -p no:cacheprovider > "$O/pytest_q.log" 2>&1 || { echo "qtests failed rc=$?"; tail -40 "$O/pytest_q.log"; exit 1; } ;;

@@ -56,11 +56,12 @@ struct HostBuf {
     size_t cap = 0;
     hipError_t ensure(size_t bytes) {
         if (bytes <= cap && p) return hipSuccess;
+        const size_t want = std::max<size_t>(std::max<size_t>(bytes, 2 * cap), 4096);   // geometric growth
         if (p) (void)hipHostFree(p);
         p = nullptr;
         cap = 0;
-        hipError_t e = hipHostMalloc(&p, std::max<size_t>(bytes, 4096), hipHostMallocDefault);
-        if (e == hipSuccess) cap = std::max<size_t>(bytes, 4096);
+        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        if (e == hipSuccess) cap = want;
         return e;
     }
     void release() {
@@ -83,6 +84,7 @@ struct vcfc_ctx {
     DevBuf in, off, len, out, rec, ws, err, aux, flag, qref;
     DevBuf ing_dev[vcfc_ing::Memory::N_DEV];
     HostBuf ing_host[vcfc_ing::Memory::N_HOST];
+    HostBuf dec_host[vcfc_dec::Buffers::N_HOST];
 };
 
 namespace {
@@ -158,6 +160,10 @@ struct CtxDecodeBuffers : vcfc_dec::Buffers {
                   : slot == LINE_OFF ? &c->off : slot == FLAG ? &c->flag
                   : slot == QREF ? &c->qref : &c->err;
         return b->ensure(bytes) == hipSuccess ? b->p : nullptr;
+    }
+    uint8_t *host(int slot, uint64_t bytes) override {   // pinned staging
+        HostBuf &b = c->dec_host[slot];
+        return b.ensure(bytes) == hipSuccess ? static_cast<uint8_t *>(b.p) : nullptr;
     }
 };
 
@@ -253,6 +259,7 @@ void vcfc_ctx_destroy(vcfc_ctx *c) {
     c->flag.release(); c->qref.release();
     for (auto &b : c->ing_dev) b.release();
     for (auto &b : c->ing_host) b.release();
+    for (auto &b : c->dec_host) b.release();
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }

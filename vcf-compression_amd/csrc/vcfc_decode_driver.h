@@ -17,7 +17,10 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <vector>
@@ -33,6 +36,14 @@ struct Buffers {
     virtual ~Buffers() {}
     enum { IN = 0, REC, WS, OUT, LINE_OFF, SMALL, FLAG, QREF, N_SLOTS };
     virtual void *get(int slot, uint64_t bytes) = 0;   // nullptr on failure
+    // host staging (pinned where the implementation can): HOST_OUT receives
+    // decoded lines (D2H), HOST_IN assembles uploads; contents not kept
+    enum { HOST_OUT = 0, HOST_IN, N_HOST };
+    virtual uint8_t *host(int slot, uint64_t bytes) {
+        if (hv[slot].size() < bytes) hv[slot].resize(bytes);
+        return hv[slot].data();
+    }
+    std::vector<uint8_t> hv[N_HOST];
 };
 
 // Appends decoded bytes (host memory); false aborts with ST_E_IO.
@@ -151,7 +162,6 @@ inline int decode_records(const uint8_t *d_in, uint64_t n, uint64_t S, const uin
     };
     int pst = plan();
     if (pst) return pst;
-    std::vector<uint8_t> host;
     for (uint64_t i0 = 0; i0 < n_lines;) {
         uint64_t i1 = i0 + 1;
         while (i1 < n_lines && loff[i1 + 1] - loff[i0] <= out_batch) i1++;
@@ -169,10 +179,11 @@ inline int decode_records(const uint8_t *d_in, uint64_t n, uint64_t S, const uin
             if ((pst = plan())) return pst;
             continue;   // same i0, exact sizes
         }
-        host.resize(bytes);
-        if (hipMemcpyAsync(host.data(), d_out, bytes, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+        uint8_t *host = B.host(Buffers::HOST_OUT, bytes);
+        if (!host) return ST_E_HIP;
+        if (hipMemcpyAsync(host, d_out, bytes, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
             return ST_E_HIP;
-        if (!sink(host.data(), bytes)) return ST_E_IO;
+        if (!sink(host, bytes)) return ST_E_IO;
         if (line_end)
             for (uint64_t i = i0; i < i1; i++) line_end->push_back(loff[i + 1] - loff[0]);
         i0 = i1;
@@ -385,9 +396,23 @@ struct SqRec {
 };
 constexpr uint64_t SQ_PRE = 1024;   // bytes read per hop (holds most records whole)
 
+// The largest offset lseek(SEEK_SET) accepts on this file (validity is
+// monotonic: 0 <= x <= the filesystem's maximum file size), by bisection.
+inline int64_t sq_max_seek(int fd) {
+    int64_t lo = 0, hi = INT64_MAX;
+    if (lseek(fd, (off_t)hi, SEEK_SET) == (off_t)hi) return hi;
+    while (hi - lo > 1) {
+        const int64_t mid = lo + (hi - lo) / 2;
+        if (lseek(fd, (off_t)mid, SEEK_SET) == (off_t)mid) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
 // Walk up to `want` records from ls (linear traversal, main.cpp:436-566):
 // stops after an end-of-reference record, a walk error, or a failing hop.
-inline int sq_walk(int fd, uint64_t ls, uint64_t want, std::vector<SqRec> &recs, std::vector<uint8_t> &pre) {
+inline int sq_walk(int fd, uint64_t ls, uint64_t want, int64_t max_seek, std::vector<SqRec> &recs,
+                   std::vector<uint8_t> &pre) {
     recs.clear();
     pre.clear();
     while (recs.size() < want) {
@@ -403,7 +428,7 @@ inline int sq_walk(int fd, uint64_t ls, uint64_t want, std::vector<SqRec> &recs,
         if (k < 16) { r.walk = ST_E_FORMAT; recs.push_back(r); break; }                  // :454-456
         if (sq_be64(h) == 0 && r.dnext == 0) { r.walk = ST_E_FORMAT; recs.push_back(r); break; }   // :464-466
         const int64_t next = (int64_t)(ls + r.dnext);   // lseek64(dnext - bytes read, SEEK_CUR) lands here
-        if (r.dnext && (next < 0 || lseek(fd, (off_t)next, SEEK_SET) != (off_t)next)) r.sync = true;
+        if (r.dnext && (next < 0 || next > max_seek)) r.sync = true;
         recs.push_back(r);
         if (r.dnext == 0 || r.sync) break;
         ls = (uint64_t)next;
@@ -469,47 +494,88 @@ inline int sparse_query(int fd, const SparseQuery &q, Buffers &B, hipStream_t s,
         }
     }
     uint64_t ls = (uint64_t)lseek(fd, 0, SEEK_CUR);
-    // linear traversal (:436-566) in batches
+    // stage times (VCFC_SQ_TRACE=1 prints them to stderr)
+    struct Trace {
+        bool on = getenv("VCFC_SQ_TRACE") != nullptr;
+        double walk = 0, body = 0, dec = 0, eval = 0;
+        uint64_t recs = 0, batches = 0;
+        static double now() {
+            return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+        }
+        ~Trace() {
+            if (on)
+                fprintf(stderr, "sparse_query: %llu records in %llu batches: walk %.1f ms, record bytes %.1f ms, "
+                                "GPU decode %.1f ms, verdicts+sink %.1f ms\n", (unsigned long long)recs,
+                        (unsigned long long)batches, walk * 1e3, body * 1e3, dec * 1e3, eval * 1e3);
+        }
+    } tr;
+    // linear traversal (:436-566) in batches (growing to SQ_BATCH records:
+    // the walk runs at most one batch past the reference's last record)
+    const int64_t max_seek = sq_max_seek(fd);
+    constexpr uint64_t SQ_BATCH = 4096;
     std::vector<SqRec> recs;
-    std::vector<uint8_t> pre, hbuf, lines;
-    std::vector<uint64_t> roff, lend, lineof, pend;
+    std::vector<uint8_t> pre, lines;
+    std::vector<uint64_t> roff, lend, lineof, pend, rlen;
     std::vector<int> lst;
-    for (uint64_t want = 32;; want = std::min<uint64_t>(want * 4, 1ull << 16)) {
-        int st = sq_walk(fd, ls, want, recs, pre);
+    for (uint64_t want = 32;; want = std::min<uint64_t>(want * 4, SQ_BATCH)) {
+        double t0 = Trace::now();
+        int st = sq_walk(fd, ls, want, max_seek, recs, pre);
         if (st) return st;
         const uint64_t nr = recs.size();
-        // record bytes [ls + 16, + 4 + LEN) of the records with sane headers
-        hbuf.clear(); roff.clear();
+        tr.recs += nr;
+        tr.batches++;
+        double t1 = Trace::now();
+        tr.walk += t1 - t0;
+        // record bytes [ls + 16, + 4 + LEN) of the records with sane headers,
+        // assembled in the upload staging buffer
+        roff.clear(); rlen.clear();
         std::vector<uint64_t> reg;   // record index of each regular record
         lst.assign(nr, ST_OK);
         pend.assign(nr, 0);
+        uint64_t hbytes = 0;
         for (uint64_t i = 0; i < nr; i++) {
             if (recs[i].walk) break;
             const SqRec &r = recs[i];
-            const uint64_t rs = r.ls + 16;
             if (r.npre < 24) continue;
             const uint8_t *h8 = pre.data() + r.pre + 16;
             if ((h8[0] >> 6) != 3u || (h8[4] >> 6) != 3u) continue;
             const uint64_t L = ((uint64_t)(h8[0] & 0x3Fu) << 24) | ((uint64_t)h8[1] << 16) | ((uint64_t)h8[2] << 8) | h8[3];
             if (L < 4) continue;
-            const uint64_t o = hbuf.size();
-            hbuf.resize(o + 4 + L);
-            if (20 + L <= r.npre) {
-                memcpy(hbuf.data() + o, h8, 4 + L);
-            } else if (sq_pread(fd, hbuf.data() + o, 4 + L, rs) != (int64_t)(4 + L)) {
-                hbuf.resize(o);
-                continue;
-            }
-            roff.push_back(o);
+            roff.push_back(hbytes);
+            rlen.push_back(4 + L);
             reg.push_back(i);
+            hbytes += 4 + L;
         }
+        uint8_t *hbuf = B.host(Buffers::HOST_IN, hbytes + 64);
+        if (!hbuf) return ST_E_HIP;
+        {
+            uint64_t w = 0, q = 0;
+            for (uint64_t j = 0; j < reg.size(); j++) {
+                const SqRec &r = recs[reg[j]];
+                const uint64_t k = rlen[j];
+                if (16 + k <= r.npre) {
+                    memcpy(hbuf + w, pre.data() + r.pre + 16, k);
+                } else if (sq_pread(fd, hbuf + w, k, r.ls + 16) != (int64_t)k) {
+                    continue;   // short (EOF): the window path decides
+                }
+                roff[q] = w;
+                reg[q] = reg[j];
+                q++;
+                w += k;
+            }
+            roff.resize(q);
+            reg.resize(q);
+            hbytes = w;
+        }
+        t0 = Trace::now();
+        tr.body += t0 - t1;
         // decode the regular records on the GPU; lines[lineof[i], lineof[i + 1]) of record i
         lines.clear();
         std::vector<uint64_t> lo(nr, ~0ull), le(nr, 0);
         const uint64_t nreg = reg.size();
         if (nreg) {
-            roff.push_back(hbuf.size());
-            const uint8_t *d_in = upload(B, Buffers::IN, hbuf.data(), hbuf.size(), s);
+            roff.push_back(hbytes);
+            const uint8_t *d_in = upload(B, Buffers::IN, hbuf, hbytes, s);
             const uint64_t *d_rec = reinterpret_cast<const uint64_t *>(
                 upload(B, Buffers::REC, reinterpret_cast<const uint8_t *>(roff.data()), 8 * roff.size(), s));
             if (!d_in || !d_rec) return ST_E_HIP;
@@ -520,7 +586,7 @@ inline int sparse_query(int fd, const SparseQuery &q, Buffers &B, hipStream_t s,
                 lend.clear();
                 const uint64_t base = lines.size();
                 auto lsink = [&](const uint8_t *p, uint64_t k) { lines.insert(lines.end(), p, p + k); return true; };
-                st = decode_records(d_in, hbuf.size(), S, d_rec + j0, nullptr, nreg - j0, B, s, lsink, 1ull << 30,
+                st = decode_records(d_in, hbytes, S, d_rec + j0, nullptr, nreg - j0, B, s, lsink, 1ull << 30,
                                     &stop, &cont, &lend);
                 if (st) return st;
                 uint64_t got = lend.size();
@@ -535,10 +601,19 @@ inline int sparse_query(int fd, const SparseQuery &q, Buffers &B, hipStream_t s,
                 j0 += got + 1;   // the stopping record: window path below
             }
         }
-        // evaluate in order
+        t1 = Trace::now();
+        tr.dec += t1 - t0;
+        struct EvalTime {
+            Trace &t; double t1;
+            ~EvalTime() { t.eval += Trace::now() - t1; }
+        } et{tr, t1};
+        // evaluate in order; accepted lines that lie back to back in `lines`
+        // leave in one write
+        uint64_t ps = 0, pe = 0;   // pending span of `lines`
+        auto flush = [&]() { bool ok = pe == ps || sink(lines.data() + ps, pe - ps); ps = pe = 0; return ok; };
         for (uint64_t i = 0; i < nr; i++) {
             const SqRec &r = recs[i];
-            if (r.walk) return r.walk;
+            if (r.walk) return flush() ? r.walk : ST_E_IO;
             const uint8_t *L;
             uint64_t n;
             std::vector<uint8_t> one;
@@ -546,6 +621,7 @@ inline int sparse_query(int fd, const SparseQuery &q, Buffers &B, hipStream_t s,
                 L = lines.data() + lo[i];
                 n = le[i] - lo[i];
             } else {
+                if (!flush()) return ST_E_IO;
                 if ((st = sq_line_window(fd, fsize, r.ls + 16, S, B, s, one, &pend[i]))) return st;
                 L = one.data();
                 n = one.size();
@@ -553,17 +629,25 @@ inline int sparse_query(int fd, const SparseQuery &q, Buffers &B, hipStream_t s,
             // SplitIterator(line, "\t"): CHROM, POS (split_iterator.cpp); strtoul whole (:520-524)
             uint64_t t1 = 0;
             while (t1 < n && L[t1] != '\t') t1++;
-            if (t1 >= n) return ST_E_FORMAT;   // no second term
-            uint64_t t2 = t1 + 1;
+            uint64_t t2 = t1 + 1, pos = 0;
             while (t2 < n && L[t2] != '\t') t2++;
-            uint64_t pos = 0;
-            if (!sq_strtoul_whole(L + t1 + 1, t2 - t1 - 1, &pos)) return ST_E_FORMAT;
-            if (!(t1 == q.ref_len && memcmp(L, q.ref, q.ref_len) == 0 && pos <= q.end)) return ST_OK;
-            if (!sink(L, n)) return ST_E_IO;
-            if (r.dnext == 0 || pos >= q.end) return ST_OK;
+            if (t1 >= n || !sq_strtoul_whole(L + t1 + 1, t2 - t1 - 1, &pos))   // no second term / bad POS: throws
+                return flush() ? ST_E_FORMAT : ST_E_IO;
+            if (!(t1 == q.ref_len && memcmp(L, q.ref, q.ref_len) == 0 && pos <= q.end)) return flush() ? ST_OK : ST_E_IO;
+            if (lo[i] != ~0ull && pe == lo[i] && pe > ps) {
+                pe = le[i];
+            } else if (lo[i] != ~0ull) {
+                if (!flush()) return ST_E_IO;
+                ps = lo[i];
+                pe = le[i];
+            } else if (!sink(L, n)) {
+                return ST_E_IO;
+            }
+            if (r.dnext == 0 || pos >= q.end) return flush() ? ST_OK : ST_E_IO;
             if (r.sync) ls = pend[i];   // the failed lseek leaves the parse end
             else ls = r.ls + r.dnext;
         }
+        if (!flush()) return ST_E_IO;
     }
 }
 
