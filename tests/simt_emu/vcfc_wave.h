@@ -78,9 +78,9 @@ inline uint32_t bload_dw(brsrc r, uint32_t off) {
     if ((uint64_t)off + 4 > r.bytes) return 0u;   // per-dword range check
     uint32_t v; memcpy(&v, r.base + off, 4); return v;
 }
-inline uint4 bload16(brsrc r, uint32_t off) {
+inline uint4 bload16(brsrc r, uint32_t off, int = 0) {   // (cache policy: no effect here)
     return make_uint4(bload_dw(r, off), bload_dw(r, off + 4), bload_dw(r, off + 8), bload_dw(r, off + 12));
 }
-inline uint32_t bload4(brsrc r, uint32_t off) { return bload_dw(r, off); }
+inline uint32_t bload4(brsrc r, uint32_t off, int = 0) { return bload_dw(r, off); }
 inline void pin_loads() {}
 }  // namespace vw

@@ -163,11 +163,34 @@ struct Chunk {
     }
 };
 
+// cache policy of the encoder's line loads (read once): VCFC_PRE_AUX for the
+// prefix / general-step chunks, VCFC_GT_AUX for the genotype stream (2 = nt)
+#ifndef VCFC_PRE_AUX
+#define VCFC_PRE_AUX 0
+#endif
+#ifndef VCFC_GT_AUX
+#define VCFC_GT_AUX 0
+#endif
+
+// The look-ahead dword after a lane's bytes is the next lane's first dword:
+// only lane 63 loads it (the other lanes' offsets lie past the range, so
+// they make no memory request -- a 4-byte load from every lane costs ~8 % of
+// the stream, tools/stream_probe.hip), and look_ahead() fills the others by
+// DPP once the chunk is consumed.
+constexpr uint32_t LA_OFF = 0x80000000u;   // past any row's range (records < 1 GiB)
+__device__ __forceinline__ uint32_t la_off(uint32_t lane_bytes, uint32_t last) {
+    return lane_bytes == last ? 0u : LA_OFF;
+}
+
 __device__ __forceinline__ Chunk load_chunk(vw::brsrc rs, uint32_t c, uint32_t lo16) {
     Chunk k;
     const uint32_t off = c * CHUNK + lo16;   // lo16 = 16 * lane
-    k.a = vw::bload16(rs, off);
-    k.y = vw::bload4(rs, off + 16u);
+    k.a = vw::bload16(rs, off, VCFC_PRE_AUX);
+    k.y = vw::bload4(rs, off + 16u + la_off(lo16, 63 * BPL), VCFC_PRE_AUX);
+    return k;
+}
+__device__ __forceinline__ Chunk look_ahead(Chunk k) {
+    k.y = vw::shl1(k.a.x, k.y);
     return k;
 }
 
@@ -391,9 +414,9 @@ struct Chunk8 {
 __device__ __forceinline__ Chunk8 load_chunk8(vw::brsrc rs, uint32_t C, uint32_t lo32) {
     Chunk8 k;
     const uint32_t off = C * CHUNK8 + lo32;   // lo32 = 32 * lane
-    k.a = vw::bload16(rs, off);
-    k.b = vw::bload16(rs, off + 16u);
-    k.y = vw::bload4(rs, off + 32u);
+    k.a = vw::bload16(rs, off, VCFC_GT_AUX);
+    k.b = vw::bload16(rs, off + 16u, VCFC_GT_AUX);
+    k.y = vw::bload4(rs, off + 32u + la_off(lo32, 63 * BPL8), VCFC_GT_AUX);   // lane 63 only (see load_chunk)
     return k;
 }
 
@@ -633,8 +656,9 @@ __device__ __forceinline__ bool gt_step8(const Chunk8 &cur, uint32_t C, FastStat
     const int32_t tf = (int32_t)(C * SLOTS8);
     if (tf >= (int32_t)T) return true;
     uint32_t d[TPL8];
+    const uint32_t ya = vw::shl1(cur.a.x, cur.y);   // look-ahead dword (see load_chunk)
 #pragma unroll
-    for (int j = 0; j < (int)TPL8; j++) d[j] = vw::alignbyte(cur.w(j + 1), cur.w(j), phi);
+    for (int j = 0; j < (int)TPL8; j++) d[j] = vw::alignbyte(j + 1 == (int)TPL8 ? ya : cur.w(j + 1), cur.w(j), phi);
     const int32_t t0 = tf + (int32_t)(TPL8 * l);
     const bool pclean = f.pcls < CLS_ESC || f.pcls == CLS_NONE;
     if (tf + (int32_t)SLOTS8 < (int32_t)T) {
@@ -701,7 +725,7 @@ __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring
     Chunk b = load_chunk(rsA, 0, lo16);
     int st;
     for (;;) {
-        st = (int)vw::readfirst((uint32_t)fast_prefix_step(b, c, lead, len, f, r));
+        st = (int)vw::readfirst((uint32_t)fast_prefix_step(look_ahead(b), c, lead, len, f, r));
         if (st != 0) break;
         c = vw::readfirst(c + 1);
         if (c >= nch) return false;   // < 10 fields
@@ -742,7 +766,7 @@ __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring
         if (ok) break;
         // chunk `gen`: the general step over its two 1 KiB halves
         for (uint32_t h = 0; h < 2; h++) {
-            const Chunk hc = load_chunk(rsG, 2 * gen + h, lo16);
+            const Chunk hc = look_ahead(load_chunk(rsG, 2 * gen + h, lo16));
             if (!vw::readfirst(gt_general(hc, (int32_t)(gen * SLOTS8 + h * 64 * TPL), f, r))) return false;
         }
         C0 = vw::readfirst(gen + 1);

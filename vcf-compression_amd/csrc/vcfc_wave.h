@@ -131,12 +131,15 @@ typedef __amdgpu_buffer_rsrc_t brsrc;
 __device__ __forceinline__ brsrc make_rsrc(const void *base, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, (int)bytes, 0x00020000);
 }
-__device__ __forceinline__ uint4 bload16(brsrc r, uint32_t off) {
-    const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+// aux: cache policy bits (0 default, 2 nt)
+__device__ __forceinline__ uint4 bload16(brsrc r, uint32_t off, const int aux = 0) {
+    const v4u v = aux == 2 ? __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 2)
+                           : __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
     return make_uint4(v.x, v.y, v.z, v.w);
 }
-__device__ __forceinline__ uint32_t bload4(brsrc r, uint32_t off) {
-    return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+__device__ __forceinline__ uint32_t bload4(brsrc r, uint32_t off, const int aux = 0) {
+    return aux == 2 ? __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 2)
+                    : __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
 }
 // Keep just-issued prefetch loads where they are: the memory clobber stops
 // LLVM from sinking them towards their (next-iteration) use, which would
