@@ -98,9 +98,39 @@ def cpu_baseline(rows, torch, args):
             assert st == 0
             out = out[len(header):]
             kind = "port"
-    return ({"value": round(gt / dt / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": kind,
-             "sample": "first %d rows of the rank-0 shard (%d GT bytes, %.1f MB file), `main compress` wall time %.2f s"
-                       % (k, gt, (len(header) + len(body)) / 1e6, dt)}, out, k)
+        par = None
+        if kind == "reference":
+            # the same sample over P processes (byte-balanced row shards, each a
+            # VCF with the header): the reference's CPU path on the box's share
+            # of host cores (SURVEY §8 d)
+            P = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "16")), os.cpu_count() or 1, 16))
+            cut = [0]
+            for q in range(1, P):
+                c = body.find(b"\n", max(len(body) * q // P, cut[-1])) + 1
+                cut.append(c if c > 0 else len(body))
+            cut.append(len(body))
+            paths = []
+            for q in range(P):
+                pq = os.path.join(d, "p%d.vcf" % q)
+                with open(pq, "wb") as f:
+                    f.write(header + body[cut[q]:cut[q + 1]])
+                paths.append(pq)
+            t0 = time.perf_counter()
+            procs = [subprocess.Popen([ref, "compress", pq, pq + "c"], stdout=subprocess.DEVNULL,
+                                      stderr=subprocess.DEVNULL) for pq in paths]
+            rcs = [pr.wait() for pr in procs]
+            dtp = time.perf_counter() - t0
+            same = all(r == 0 for r in rcs) and b"".join(open(pq + "c", "rb").read()[len(header):]
+                                                         for pq in paths) == out
+            par = {"value": round(gt / dtp / 1e9, 4), "unit": "GB/s", "cores": P, "kind": "reference",
+                   "sample": "the same %d rows as %d byte-balanced shards, %d concurrent `main compress` "
+                             "processes, wall time %.2f s" % (k, P, P, dtp), "output_identical": same}
+    res = {"value": round(gt / dt / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": kind,
+           "sample": "first %d rows of the rank-0 shard (%d GT bytes, %.1f MB file), `main compress` wall time %.2f s"
+                     % (k, gt, (len(header) + len(body)) / 1e6, dt)}
+    if par:
+        res["parallel"] = par
+    return (res, out, k)
 
 
 def load_pmc(workload_key):
@@ -170,6 +200,25 @@ def cpu_reference_run(rows, recs, rec, args, verb_args):
         dt = time.perf_counter() - t0
         assert st == 0
         return dt, k, "port"
+
+
+def measured_copy_gbs(torch, dev, nbytes=4 << 30):
+    """Device-to-device copy rate on this GPU (read + write bytes / time):
+    the practical HBM ceiling beside the 8 TB/s spec peak."""
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(5):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    gbs = 2 * nbytes * 5 / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del a, b
+    torch.cuda.empty_cache()
+    return round(gbs, 1)
 
 
 def timed(torch, dev, args, step):
@@ -545,6 +594,7 @@ def main():
     e = int(err.cpu().numpy().view(np.uint64)[0])
     if e != vcfc.NO_ERROR:
         raise RuntimeError("encode reported row error %x" % e)
+    copy_gbs = measured_copy_gbs(torch, dev)
     out_bytes = int(rec[n].item())
     ms_step = elapsed * 1e3 / args.steps
     gt_total = rows.gt_bytes * world
@@ -564,6 +614,7 @@ def main():
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(alg / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "traffic": load_pmc(wkey),
             "algorithmic_bytes_per_launch": alg, "avg_launch_ms": round(k_ms, 4),
+            "measured_torch_copy_gbs": copy_gbs,
             "stages_ms": {k: round(v / max(calls, 1), 4) for k, v in stages.items()}}
     res = {"metric": metric,
            "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,

@@ -169,3 +169,36 @@ def test_sparsify_matches_reference(ctx, name, key):
                            capture_output=True, timeout=300)
         assert r.returncode == 0, r.stderr
         assert sparse_digest.digest(dst + "2") == G.manifest()[key]
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_logical_shards_stitch_on_one_gpu(vcfc, world):
+    """the multi-GPU stitch with 1/2/4/8 logical shards on one
+    device (one thread and one context per shard, a fake all-gather): the
+    output is byte-identical to the reference's for every shard count."""
+    import threading
+    import dist_compress as D
+    data = G.gz("random_100x10000.vcf.gz")
+    want = G.gz("random_100x10000.vcfc.gz")
+    with tempfile.TemporaryDirectory() as d:
+        ip, op = os.path.join(d, "in.vcf"), os.path.join(d, "out.vcfc")
+        with open(ip, "wb") as f:
+            f.write(data)
+        open(op, "wb").close()
+        slots, bar, res = [None] * world, threading.Barrier(world), [None] * world
+
+        def worker(rank):
+            with vcfc.Context(0) as ctx:
+                def allgather(vals):
+                    slots[rank] = vals
+                    bar.wait()
+                    return list(slots)
+                res[rank] = D.compress_shard(ip, op, rank, world, ctx.compress_status, allgather)
+
+        ts = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(120)
+        assert all(r is not None and r[0] == 0 for r in res), res
+        assert open(op, "rb").read() == want

@@ -79,6 +79,14 @@ def test_gloo_stitch_fuzz_and_error_line():
     k = len(lines) * 3 // 4
     lines[k] = b"1\t2\t3"
     bad = b"\n".join(lines)
-    st1, _, line1 = G.oracle_compress(bad)
+    st1, out1, line1 = G.oracle_compress(bad)
     res, out = _run(2, bad, 29508)
     assert st1 == 1 and all(r[1] == 1 and r[3] == line1 for r in res)
+    assert out == out1   # everything before the failing line, as one process writes it
+    # failing line in the first shard: the second shard writes nothing
+    lines = data.split(b"\n")
+    lines[len(lines) // 5] = b"1\t2\t3"
+    bad = b"\n".join(lines)
+    st1, out1, line1 = G.oracle_compress(bad)
+    res, out = _run(2, bad, 29509)
+    assert st1 == 1 and all(r[1] == 1 and r[3] == line1 for r in res) and out == out1

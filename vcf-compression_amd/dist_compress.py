@@ -43,9 +43,12 @@ def exclusive_offsets(counts):
 
 
 def compress_shard(in_path, out_path, rank, world, encode, allgather):
-    """encode(bytes) -> (status, out_bytes, err_line_in_slice);
+    """encode(bytes) -> (status, out_bytes, err_line_in_slice), where on a
+    failing line out_bytes holds the output of the slice's lines before it;
     allgather(list_of_ints_local) -> list of per-rank lists.
-    Returns (status, total_bytes, global_err_line)."""
+    Returns (status, total_bytes, global_err_line).  The output file equals
+    the single-process output: on a failure, everything before the first
+    failing line in file order (the reference stops there)."""
     size = os.path.getsize(in_path)
     with open(in_path, "rb") as f:
         def read_at(off, n):
@@ -64,16 +67,15 @@ def compress_shard(in_path, out_path, rank, world, encode, allgather):
             left -= len(b)
     st, out, err_line = encode(mine)
     g = allgather([len(out), st, (lines_before + err_line) if st else -1])
-    counts = [x[0] for x in g]
+    # the first failing rank (shards are in file order) holds the first
+    # failing line: it writes its partial output, later ranks write nothing
+    first_bad = next((r for r, x in enumerate(g) if x[1] != 0), world)
+    counts = [x[0] if r <= first_bad else 0 for r, x in enumerate(g)]
     offs, total = exclusive_offsets(counts)
-    # the first failing line in file order decides the status (the reference
-    # stops there); ranks after it still write their bytes so the output holds
-    # everything up to the failure
-    bad = [(x[2], x[1]) for x in g if x[1] != 0]
-    status, gline = (min(bad)[1], min(bad)[0]) if bad else (0, -1)
+    status, gline = (g[first_bad][1], g[first_bad][2]) if first_bad < world else (0, -1)
     fd = os.open(out_path, os.O_WRONLY | os.O_CREAT, 0o644)
     try:
-        if out:
+        if out and rank <= first_bad:
             os.pwrite(fd, out, offs[rank])
         if rank == world - 1:
             os.ftruncate(fd, total)
@@ -102,12 +104,10 @@ def main():
     ctx = vcfc.Context(local)
 
     def encode(buf):
-        try:
-            return 0, ctx.compress_buffer(buf), -1
-        except vcfc.VcfValidationError as e:
-            return vcfc.E_LT8COLS, b"", int(str(e).split("line ")[-1].rstrip(")"))
-        except vcfc.LengthError as e:
-            return vcfc.E_8COLS, b"", int(str(e).split("line ")[-1].rstrip(")"))
+        st, out, line = ctx.compress_status(buf)
+        if st not in (vcfc.OK, vcfc.E_LT8COLS, vcfc.E_8COLS, vcfc.E_HEADER):
+            vcfc.raise_for(st)
+        return st, out, line
 
     def allgather(vals):
         if world == 1:

@@ -187,6 +187,19 @@ class Context:
         raise_for(st, "line %d" % line.value)
         return out[:n.value].tobytes()
 
+    def compress_status(self, data):
+        """Like compress_buffer without raising: (status, bytes, err_line).
+        On a failing line the bytes are everything the reference writes
+        before it throws; err_line is its 1-based line number."""
+        cap = lib().vcfc_compress_bound(len(data))
+        out = np.empty(cap, dtype=np.uint8)
+        n = ctypes.c_uint64(0)
+        line = ctypes.c_int64(-1)
+        src = np.frombuffer(data, dtype=np.uint8)
+        st = lib().vcfc_compress_buffer(self._h, src.ctypes.data, len(data), out.ctypes.data, cap,
+                                        ctypes.byref(n), ctypes.byref(line))
+        return st, out[:n.value].tobytes(), line.value
+
     def compress_file(self, in_path, out_path):
         line = ctypes.c_int64(-1)
         st = lib().vcfc_compress_file(self._h, in_path.encode(), out_path.encode(), ctypes.byref(line))
