@@ -14,7 +14,11 @@ _lib = None
 def lib():
     global _lib
     if _lib is None:
-        subprocess.run(["make", "-s", "-C", os.path.join(REPO, "tests", "simt_emu")], check=True)
+        import fcntl
+        os.makedirs(os.path.dirname(EMU_SO), exist_ok=True)
+        with open(EMU_SO + ".lock", "w") as lk:   # one build at a time (pytest -n workers)
+            fcntl.flock(lk, fcntl.LOCK_EX)
+            subprocess.run(["make", "-s", "-C", os.path.join(REPO, "tests", "simt_emu")], check=True)
         L = ctypes.CDLL(EMU_SO)
         vp = ctypes.c_void_p
         L.emu_encode_rows.argtypes = [vp, vp, vp, ctypes.c_uint64, vp, ctypes.c_uint64, vp,

@@ -20,14 +20,8 @@ extern "C" int emu_encode_rows(const uint8_t *buf, const uint64_t *line_off, con
     VcfcEncodeArgs a;
     a.buf = buf; a.line_off = line_off; a.line_len = line_len; a.n = n;
     a.out = out; a.out_cap = out_cap; a.rec_off = rec_off;
-    a.slot_off = (uint64_t *)(ws + L.slot_off);
-    a.rec_size = (uint32_t *)(ws + L.rec_size);
-    a.partials = (uint64_t *)(ws + L.partials);
+    vcfc_encode_args_workspace(a, ws, L);
     a.err = (uint64_t *)(ws + L.err);
-    a.retry = (uint32_t *)(ws + L.retry);
-    a.retry_count = (uint32_t *)(ws + L.retry_count);
-    a.slots = ws + L.slots;
-    a.slots_cap = L.total - L.slots;
     emu::g.switches = 0;
     int st = (int)vcfc_encode_device(a, nullptr);
     *err_word = *a.err;

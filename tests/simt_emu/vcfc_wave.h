@@ -19,6 +19,7 @@ inline uint32_t dpp(uint32_t old, uint32_t src, int ctrl, int rm, int bm, bool b
 inline uint32_t shr1(uint32_t v, uint32_t fill) { return dpp(fill, v, 0x138, 0xf, 0xf, false); }
 inline uint32_t shr1z(uint32_t v) { return shr1(v, 0u); }
 inline uint32_t shl1(uint32_t v, uint32_t fill) { return dpp(fill, v, 0x130, 0xf, 0xf, false); }
+inline uint32_t row_shl1(uint32_t v) { return dpp(0u, v, 0x101, 0xf, 0xf, false); }
 inline uint32_t scan_add(uint32_t v) {
     v += dpp(0u, v, 0x111, 0xf, 0xf, false);
     v += dpp(0u, v, 0x112, 0xf, 0xf, false);

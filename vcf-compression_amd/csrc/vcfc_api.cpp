@@ -289,14 +289,8 @@ static int encode_rows_device_impl(const uint8_t *d_buf, const uint64_t *d_line_
     a.out = d_out;
     a.out_cap = out_cap;
     a.rec_off = d_rec_off;
-    a.slot_off = reinterpret_cast<uint64_t *>(ws + L.slot_off);
-    a.rec_size = reinterpret_cast<uint32_t *>(ws + L.rec_size);
-    a.partials = reinterpret_cast<uint64_t *>(ws + L.partials);
+    vcfc_encode_args_workspace(a, ws, L);
     a.err = d_err;
-    a.retry = reinterpret_cast<uint32_t *>(ws + L.retry);
-    a.retry_count = reinterpret_cast<uint32_t *>(ws + L.retry_count);
-    a.slots = ws + L.slots;
-    a.slots_cap = L.total - L.slots;
     return vcfc_encode_device(a, static_cast<hipStream_t>(stream), ev) == hipSuccess ? VCFC_OK : VCFC_E_HIP;
 }
 

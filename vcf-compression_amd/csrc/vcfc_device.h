@@ -31,12 +31,19 @@ struct VcfcEncodeArgs {
     uint64_t *err;             // 1 word
     uint32_t *retry;           // rows the fast kernel hands to the general one
     uint32_t *retry_count;
-    uint8_t *slots;            // per-row staging slots
+    uint8_t *prim;             // per-row primary staging: record bytes [0, VCFC_PRIM) at prim + VCFC_PRIM * row
+    uint8_t *slots;            // per-row overflow slots: record bytes [VCFC_PRIM, ...) at slots + slot_off[row]
     uint64_t slots_cap;
 };
 
+// Record staging: the first VCFC_PRIM bytes of every record go to a dense
+// per-row array (the compaction then reads most records from consecutive
+// kilobytes), the rest (records of rare escape-heavy rows) to a per-row
+// overflow slot sized for the worst case.
+#define VCFC_PRIM 1024u
+
 struct VcfcWorkspaceLayout {
-    uint64_t slot_off, rec_size, partials, err, retry, retry_count, slots, total;
+    uint64_t slot_off, rec_size, partials, err, retry, retry_count, prim, slots, total;
 };
 
 // Bytes of per-row staging for a line of `len` bytes: covers the worst-case
@@ -53,6 +60,18 @@ __host__ __device__ inline uint64_t vcfc_record_bound(uint64_t n, uint64_t total
 
 // Workspace layout for n rows whose line lengths sum to <= total_line_bytes.
 VcfcWorkspaceLayout vcfc_encode_workspace_layout(uint64_t n, uint64_t total_line_bytes);
+
+// Point a's workspace arrays into ws (err is the caller's).
+inline void vcfc_encode_args_workspace(VcfcEncodeArgs &a, uint8_t *ws, const VcfcWorkspaceLayout &L) {
+    a.slot_off = reinterpret_cast<uint64_t *>(ws + L.slot_off);
+    a.rec_size = reinterpret_cast<uint32_t *>(ws + L.rec_size);
+    a.partials = reinterpret_cast<uint64_t *>(ws + L.partials);
+    a.retry = reinterpret_cast<uint32_t *>(ws + L.retry);
+    a.retry_count = reinterpret_cast<uint32_t *>(ws + L.retry_count);
+    a.prim = ws + L.prim;
+    a.slots = ws + L.slots;
+    a.slots_cap = L.total - L.slots;
+}
 
 // Enqueue the whole encode on `stream` (no host synchronisation, capturable).
 // If `ev` is non-null, ev[0..4] are recorded before the slot scan, after it,

@@ -5,11 +5,11 @@
 //
 //   scan<BOUND>  slot_off[i] = sum_{k<i} slot_bytes(len_k)     (tiny)
 //   k_encode_fast     one wave64 per row: tokenise, RLE-encode, stage the
-//                     record in an LDS ring, stream it to the row's slot in
+//                     record in an LDS ring, stream it to the row's staging in
 //                     1 KiB bursts; rows of another shape are queued
 //   k_encode_general  persistent waves encode the queued rows (any shape)
 //   scan<IDENT>  rec_off[i] = sum_{k<i} rec_size_k             (tiny)
-//   k_compact    16 lanes per row: slot -> final offset, 16-byte stores
+//   k_compact    16 lanes per row: staging -> final offset, 16-byte stores
 //
 // Record layout (reference compress.cpp:32-100,188-199):
 //   [LEN:4 BE|0xC0][REQ:4 BE|0xC0][cols 0..7 '\t'-joined]['\t'FORMAT]['\t']
@@ -65,24 +65,32 @@ __device__ __forceinline__ uint32_t byte_of(uint4 v, uint32_t i) {
 __device__ __forceinline__ uint32_t umin32(uint32_t a, uint32_t b) { return a < b ? a : b; }
 
 // ---------------------------------------------------------------------------
-// LDS ring: record bytes [fpos, wpos) are pending; slot = global staging.
+// LDS ring: record bytes [fpos, wpos) are pending.  Global staging: record
+// bytes [0, VCFC_PRIM) at prim, the rest at slot (see vcfc_device.h).
 struct Ring {
     uint8_t *lds;
+    uint8_t *prim;
     uint8_t *slot;
     uint32_t wpos, fpos;
 };
+static_assert(VCFC_PRIM % 1024 == 0, "bursts must not straddle the staging regions");
 
 __device__ __forceinline__ void ring_put(Ring &r, uint32_t pos, uint32_t b) {
     r.lds[pos & RMASK] = (uint8_t)b;
 }
 
-// Stream complete 1 KiB bursts to the slot.  A 2 KiB chunk adds < 2.5 KiB to
+// Stream complete 1 KiB bursts to the staging.  A 2 KiB chunk adds < 2.5 KiB to
 // a ring holding < 1 KiB, so three unrolled bursts suffice (no loop: a store
 // loop of unknown trip count makes hipcc's vmcnt tracking give up on the
 // prefetch).
+// staging address of record byte f (a burst lies wholly in one region)
+__device__ __forceinline__ void ring_stage(Ring &r, uint32_t f, uint4 v) {
+    if (r.fpos < VCFC_PRIM) vw::gstore16(r.prim, f, v);
+    else vw::gstore16(r.slot, f - VCFC_PRIM, v);
+}
 __device__ __forceinline__ void ring_burst(Ring &r, uint32_t l) {
     const uint4 v = *reinterpret_cast<const uint4 *>(r.lds + ((r.fpos + 16u * l) & RMASK));
-    vw::gstore16(r.slot, r.fpos + 16u * l, v);
+    ring_stage(r, r.fpos + 16u * l, v);
     r.fpos += BURST;
 }
 __device__ __forceinline__ void ring_flush(Ring &r, bool final) {
@@ -101,15 +109,15 @@ __device__ __forceinline__ void ring_flush(Ring &r, bool final) {
         const uint32_t rem = r.wpos - r.fpos;  // < BURST
         if (16u * l < rem) {
             const uint4 v = *reinterpret_cast<const uint4 *>(r.lds + ((r.fpos + 16u * l) & RMASK));
-            vw::gstore16(r.slot, r.fpos + 16u * l, v);
+            ring_stage(r, r.fpos + 16u * l, v);
         }
         r.fpos = r.wpos;
     }
     vw::wave_sync();
 }
 
-// Finish a record: header words go straight to the slot (lane 0 also wrote
-// the slot's first 16 bytes during the flush, so program order keeps them).
+// Finish a record: header words go straight to the staging (lane 0 also
+// wrote its first 16 bytes during the flush, so program order keeps them).
 __device__ void ring_finish(Ring &r, uint32_t req) {
     ring_flush(r, true);
     if (vw::lane_id() == 0) {
@@ -118,8 +126,8 @@ __device__ void ring_finish(Ring &r, uint32_t req) {
                             (((L >> 8) & 0xFFu) << 16) | ((L & 0xFFu) << 24);
         const uint32_t h1 = (((req >> 24) & 0xFFu) | 0xC0u) | (((req >> 16) & 0xFFu) << 8) |
                             (((req >> 8) & 0xFFu) << 16) | ((req & 0xFFu) << 24);
-        reinterpret_cast<uint32_t *>(r.slot)[0] = h0;
-        reinterpret_cast<uint32_t *>(r.slot)[1] = h1;
+        reinterpret_cast<uint32_t *>(r.prim)[0] = h0;
+        reinterpret_cast<uint32_t *>(r.prim)[1] = h1;
     }
 }
 
@@ -900,6 +908,7 @@ __device__ uint32_t encode_general(const uint8_t *__restrict__ line, uint32_t le
 // Row prologue shared by both encode kernels: slot bounds check + ring setup.
 __device__ __forceinline__ bool row_setup(const VcfcEncodeArgs &a, uint64_t row, uint8_t *lds, Ring &r) {
     r.lds = lds;
+    r.prim = a.prim + (uint64_t)VCFC_PRIM * row;
     r.slot = a.slots + a.slot_off[row];
     r.wpos = 8;
     r.fpos = 0;
@@ -953,8 +962,8 @@ __global__ __launch_bounds__(256) void k_encode_general(VcfcEncodeArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Compaction: 16 lanes per row copy slot -> out[rec_off[row]] with aligned
-// 16-byte stores (unaligned head/tail bytes stored singly).
+// Compaction: staging -> out[rec_off[row]] with aligned 16-byte stores.
+// realign16: bytes [sh, sh + 16) of the 32 bytes (lo, hi).
 __device__ __forceinline__ uint4 realign16(uint4 lo, uint4 hi, uint32_t sh) {
     const uint32_t q = sh >> 2, s = sh & 3u;
     const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
@@ -968,37 +977,53 @@ __device__ __forceinline__ uint4 realign16(uint4 lo, uint4 hi, uint32_t sh) {
                       vw::alignbyte(o[3], o[2], s), vw::alignbyte(o[4], o[3], s));
 }
 
-__global__ __launch_bounds__(256) void k_compact(const uint8_t *__restrict__ slots,
+// 16 lanes per row (four rows per wave): per pass, lane g of a row's group
+// loads the aligned 16-B staging block b0 + g (one load per lane) and takes
+// block b0 + g + 1 from lane g + 1 by DPP row_shl (the group is one DPP
+// row), so lanes 0..14 store 15 aligned, realigned 16-B output blocks.  The
+// destination's unaligned head and tail bytes are stored singly, their loads
+// issued with the blocks'.  Record bytes [0, VCFC_PRIM) come from the dense
+// primary array, the rest from the row's overflow slot.
+__device__ __forceinline__ uint4 stage_blk(const uint8_t *prim, const uint8_t *slot, uint64_t k) {
+    return k < VCFC_PRIM / 16 ? vw::gload16(prim, (uint32_t)k) : vw::gload16(slot, (uint32_t)(k - VCFC_PRIM / 16));
+}
+__device__ __forceinline__ uint8_t stage_byte(const uint8_t *prim, const uint8_t *slot, uint64_t x) {
+    return x < VCFC_PRIM ? prim[x] : slot[x - VCFC_PRIM];
+}
+__global__ __launch_bounds__(256) void k_compact(const uint8_t *__restrict__ prims,
+                                                 const uint8_t *__restrict__ slots,
                                                  const uint64_t *__restrict__ slot_off,
                                                  const uint64_t *__restrict__ rec_off, uint64_t n,
                                                  uint8_t *__restrict__ out, uint64_t out_cap,
                                                  uint64_t *err) {
     const uint32_t g = threadIdx.x >> 4, gl = threadIdx.x & 15u;
     const uint64_t row = (uint64_t)blockIdx.x * 16 + g;
-    if (row >= n) return;
-    const uint64_t d0 = rec_off[row], d1 = rec_off[row + 1];
-    if (d1 == d0) return;
-    if (d1 > out_cap) {
-        if (gl == 0) atomicMin((unsigned long long *)err, (unsigned long long)((row << 8) | VCFCD_E_NOSPACE));
-        return;
-    }
-    const uint8_t *src = slots + slot_off[row];
+    const bool live = row < n;
+    uint64_t d0 = 0, d1 = 0;
+    if (live) { d0 = rec_off[row]; d1 = rec_off[row + 1]; }
+    const bool bad = d1 > out_cap;
+    if (bad && gl == 0) atomicMin((unsigned long long *)err, (unsigned long long)((row << 8) | VCFCD_E_NOSPACE));
+    const uint64_t sz = bad ? 0 : d1 - d0;
+    const uint8_t *prim = prims + (live ? (uint64_t)VCFC_PRIM * row : 0);
+    const uint8_t *slot = slots + (live ? slot_off[row] : 0);
     uint8_t *dst = out + d0;
-    const uint64_t sz = d1 - d0;
     uint32_t head = (uint32_t)((16u - (d0 & 15u)) & 15u);
     if (head > sz) head = (uint32_t)sz;
-    if (gl < head) dst[gl] = src[gl];
     const uint64_t body = sz - head;
     const uint64_t nblk = body >> 4;
     const uint32_t tail = (uint32_t)(body & 15u);
-    const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
-    for (uint64_t k = gl; k < nblk; k += 16) {
-        const uint64_t sb = head + 16 * k;
-        const uint4 lo = s4[sb >> 4];
-        const uint4 hi = s4[(sb >> 4) + 1];
-        *reinterpret_cast<uint4 *>(dst + sb) = realign16(lo, hi, head);
+    const uint8_t hb = gl < head ? stage_byte(prim, slot, gl) : (uint8_t)0;
+    const uint8_t tb = gl < tail ? stage_byte(prim, slot, head + 16 * nblk + gl) : (uint8_t)0;
+    // passes run while any group of the wave has blocks left (DPP needs the whole wave)
+    for (uint64_t b0 = 0; vw::ballot(b0 < nblk); b0 += 15) {
+        const uint64_t k = b0 + gl;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (k <= nblk && sz) v = stage_blk(prim, slot, k);   // block nblk: the last output block's upper bytes
+        const uint4 h = make_uint4(vw::row_shl1(v.x), vw::row_shl1(v.y), vw::row_shl1(v.z), vw::row_shl1(v.w));
+        if (gl < 15 && k < nblk) vw::gstore16(dst, head + 16 * k, realign16(v, h, head));
     }
-    if (gl < tail) dst[head + 16 * nblk + gl] = src[head + 16 * nblk + gl];
+    if (gl < head) dst[gl] = hb;
+    if (gl < tail) dst[head + 16 * nblk + gl] = tb;
 }
 
 // ---------------------------------------------------------------------------
@@ -1095,6 +1120,7 @@ VcfcWorkspaceLayout vcfc_encode_workspace_layout(uint64_t n, uint64_t total_line
     L.err = o; o = al(o + 8);
     L.retry = o; o = al(o + 4 * (n + 1));
     L.retry_count = o; o = al(o + 8);
+    L.prim = o; o = al(o + (uint64_t)VCFC_PRIM * n);
     L.slots = o; o = al(o + total_line_bytes + total_line_bytes / 2 + 64 * (n + 1));
     L.total = o;
     return L;
@@ -1120,7 +1146,7 @@ hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t s, hipEvent_t
     e = launch_scan<0>(a.rec_size, a.n, a.partials, a.rec_off, s);
     if (e != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[3], s);
-    hipLaunchKernelGGL(k_compact, dim3((unsigned)((a.n + 15) / 16)), dim3(256), 0, s, a.slots, a.slot_off,
+    hipLaunchKernelGGL(k_compact, dim3((unsigned)((a.n + 15) / 16)), dim3(256), 0, s, a.prim, a.slots, a.slot_off,
                        a.rec_off, a.n, a.out, a.out_cap, a.err);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[4], s);

@@ -402,14 +402,8 @@ inline int compress_stream(Source &src, const Sink &sink, Memory &M, hipStream_t
             VcfcEncodeArgs a;
             a.buf = d_in; a.line_off = x.line_off; a.line_len = x.line_len; a.n = n_data;
             a.out = d_out; a.out_cap = cap; a.rec_off = d_rec_off;
-            a.slot_off = reinterpret_cast<uint64_t *>(ws + W.slot_off);
-            a.rec_size = reinterpret_cast<uint32_t *>(ws + W.rec_size);
-            a.partials = reinterpret_cast<uint64_t *>(ws + W.partials);
+            vcfc_encode_args_workspace(a, ws, W);
             a.err = d_small + 4;
-            a.retry = reinterpret_cast<uint32_t *>(ws + W.retry);
-            a.retry_count = reinterpret_cast<uint32_t *>(ws + W.retry_count);
-            a.slots = ws + W.slots;
-            a.slots_cap = W.total - W.slots;
             oc.rec_off.resize(n_data + 1);
             if (vcfc_encode_device(a, s) != hipSuccess ||
                 hipMemcpyAsync(oc.rec_off.data(), d_rec_off, 8 * (n_data + 1), hipMemcpyDeviceToHost, s) != hipSuccess ||

@@ -40,6 +40,11 @@ __device__ __forceinline__ uint32_t shr1z(uint32_t v) {
 __device__ __forceinline__ uint32_t shl1(uint32_t v, uint32_t fill) {
     return __builtin_amdgcn_update_dpp(fill, v, 0x130, 0xf, 0xf, false);
 }
+// lane i receives lane i+1's value within its row of 16 lanes; the last
+// lane of each row receives 0 (DPP row_shl:1)
+__device__ __forceinline__ uint32_t row_shl1(uint32_t v) {
+    return __builtin_amdgcn_update_dpp(0u, v, 0x101, 0xf, 0xf, false);
+}
 // generic lane gather (ds_bpermute)
 __device__ __forceinline__ uint32_t shfl(uint32_t v, uint32_t src) {
     return __builtin_amdgcn_ds_bpermute(src << 2, v);
