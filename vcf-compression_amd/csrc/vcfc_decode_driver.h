@@ -22,10 +22,13 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <functional>
+#include <thread>
 #include <vector>
 
 #include "vcfc_device.h"
+#include "vcfc_queue.h"
 
 namespace vcfc_dec {
 
@@ -38,7 +41,7 @@ struct Buffers {
     virtual void *get(int slot, uint64_t bytes) = 0;   // nullptr on failure
     // host staging (pinned where the implementation can): HOST_OUT receives
     // decoded lines (D2H), HOST_IN assembles uploads; contents not kept
-    enum { HOST_OUT = 0, HOST_IN, N_HOST };
+    enum { HOST_OUT = 0, HOST_IN, HOST_IN2, N_HOST };
     virtual uint8_t *host(int slot, uint64_t bytes) {
         if (hv[slot].size() < bytes) hv[slot].resize(bytes);
         return hv[slot].data();
@@ -436,6 +439,243 @@ inline int sq_walk(int fd, uint64_t ls, uint64_t want, int64_t max_seek, std::ve
     return ST_OK;
 }
 
+// One batch of the walk: the records, the bytes read with their distances,
+// and the regular records (sane header, whole in the file) staged back to back
+// in a pinned upload buffer.
+struct SqBatch {
+    std::vector<SqRec> recs;
+    std::vector<uint8_t> pre;
+    std::vector<uint64_t> roff, reg;   // staging offsets (+ end) and record index of the regular records
+    uint64_t hbytes = 0;
+    int slot = 0;                      // Buffers::HOST_IN / HOST_IN2
+    int st = ST_OK;                    // walk I/O error
+    bool last = false;                 // the walker stops after this batch
+};
+
+inline int sq_stage(int fd, SqBatch &b, Buffers &B) {
+    b.roff.clear();
+    b.reg.clear();
+    std::vector<uint64_t> rlen;
+    uint64_t hbytes = 0;
+    for (uint64_t i = 0; i < b.recs.size(); i++) {
+        const SqRec &r = b.recs[i];
+        if (r.walk) break;
+        if (r.npre < 24) continue;
+        const uint8_t *h8 = b.pre.data() + r.pre + 16;
+        if ((h8[0] >> 6) != 3u || (h8[4] >> 6) != 3u) continue;
+        const uint64_t L = ((uint64_t)(h8[0] & 0x3Fu) << 24) | ((uint64_t)h8[1] << 16) | ((uint64_t)h8[2] << 8) | h8[3];
+        if (L < 4) continue;
+        b.roff.push_back(hbytes);
+        rlen.push_back(4 + L);
+        b.reg.push_back(i);
+        hbytes += 4 + L;
+    }
+    uint8_t *hbuf = B.host(b.slot == 0 ? Buffers::HOST_IN : Buffers::HOST_IN2, hbytes + 64);
+    if (!hbuf) return ST_E_HIP;
+    uint64_t w = 0, q = 0;
+    for (uint64_t j = 0; j < b.reg.size(); j++) {
+        const SqRec &r = b.recs[b.reg[j]];
+        const uint64_t k = rlen[j];
+        if (16 + k <= r.npre) {
+            memcpy(hbuf + w, b.pre.data() + r.pre + 16, k);
+        } else {
+            const int64_t got = sq_pread(fd, hbuf + w, k, r.ls + 16);
+            if (got < 0) return ST_E_IO;
+            if (got != (int64_t)k) continue;   // short (EOF): the window path decides
+        }
+        b.roff[q] = w;
+        b.reg[q] = b.reg[j];
+        q++;
+        w += k;
+    }
+    b.roff.resize(q);
+    b.reg.resize(q);
+    b.roff.push_back(w);
+    b.hbytes = w;
+    return ST_OK;
+}
+
+// Linear traversal (main.cpp:436-566) from line_start_offset ls as a
+// pipeline: a walker thread reads batches of records ahead (32 records,
+// growing to 4 096) into two pinned staging buffers; this thread decodes each
+// batch on the GPU and applies the reference's verdicts line by line; a
+// writer thread writes the accepted lines (two line buffers).  The walk may
+// run up to two batches past the reference's last record; nothing it reads
+// there is used.
+inline int sq_traverse(int fd, uint64_t fsize, uint64_t ls, uint64_t S, const SparseQuery &q, Buffers &B,
+                       hipStream_t s, const Sink &sink) {
+    const int64_t max_seek = sq_max_seek(fd);
+    constexpr uint64_t SQ_BATCH = 4096;
+    struct Trace {   // stage times (VCFC_SQ_TRACE=1 prints them to stderr)
+        bool on = getenv("VCFC_SQ_TRACE") != nullptr;
+        double walk = 0, dec = 0, eval = 0, wait_w = 0, wait_out = 0, total = 0;
+        uint64_t recs = 0, batches = 0;
+        static double now() {
+            return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+        }
+        ~Trace() {
+            if (on)
+                fprintf(stderr, "sparse_query: %llu records in %llu batches, %.1f ms: walk+stage %.1f ms (walker "
+                                "thread), GPU decode %.1f ms, verdicts %.1f ms, waiting for the walker %.1f ms, "
+                                "for a line buffer %.1f ms\n", (unsigned long long)recs, (unsigned long long)batches,
+                        total * 1e3, walk * 1e3, dec * 1e3, eval * 1e3, wait_w * 1e3, wait_out * 1e3);
+        }
+    } tr;
+    const double t_begin = Trace::now();
+    // ---- writer ------------------------------------------------------------
+    struct WriteJob {
+        int buf = 0;
+        std::vector<std::pair<uint64_t, uint64_t>> spans;
+    };
+    std::vector<uint8_t> lines[2];
+    vcfc_q::Queue<WriteJob> jobs;
+    vcfc_q::Queue<int> free_lines;
+    free_lines.put(0);
+    free_lines.put(1);
+    std::atomic<bool> write_failed{false};
+    std::thread writer([&] {
+        WriteJob j;
+        while (jobs.get(j)) {
+            for (const auto &sp : j.spans)
+                if (!write_failed && !sink(lines[j.buf].data() + sp.first, sp.second - sp.first)) write_failed = true;
+            free_lines.put(j.buf);
+        }
+    });
+    int status = ST_OK;
+    for (bool more = true; more;) {
+        // ---- walker (from ls) --------------------------------------------------
+        vcfc_q::Queue<SqBatch> batches;
+        vcfc_q::Queue<int> free_slots;
+        free_slots.put(0);
+        free_slots.put(1);
+        std::atomic<bool> stop{false};
+        double walk_t = 0;
+        std::thread walker([&, ls] {
+            uint64_t at = ls;
+            for (uint64_t want = 32;; want = std::min<uint64_t>(want * 4, SQ_BATCH)) {
+                int slot;
+                if (stop || !free_slots.get(slot)) break;
+                const double t0 = Trace::now();
+                SqBatch b;
+                b.slot = slot;
+                b.st = sq_walk(fd, at, want, max_seek, b.recs, b.pre);
+                if (!b.st) b.st = sq_stage(fd, b, B);
+                const SqRec *e = b.recs.empty() ? nullptr : &b.recs.back();
+                b.last = b.st || !e || e->walk || e->dnext == 0 || e->sync;
+                if (!b.last) at = e->ls + e->dnext;
+                walk_t += Trace::now() - t0;
+                const bool last = b.last;
+                batches.put(std::move(b));
+                if (last) break;
+            }
+            batches.close();
+        });
+        // ---- GPU decode + verdicts (this thread) ---------------------------------
+        auto finish_walker = [&] {
+            stop = true;
+            free_slots.close();
+            walker.join();
+        };
+        SqBatch b;
+        bool resume = false;   // the walk continues after a sync record's parse end
+        for (;;) {
+            double t0 = Trace::now();
+            if (!batches.get(b)) { more = false; break; }   // (the walker always ends with a last batch)
+            tr.wait_w += Trace::now() - t0;
+            if (b.st) { status = b.st; more = false; break; }
+            const uint64_t nr = b.recs.size();
+            tr.recs += nr;
+            tr.batches++;
+            int lb;
+            t0 = Trace::now();
+            if (!free_lines.get(lb)) { status = ST_E_IO; more = false; break; }
+            tr.wait_out += Trace::now() - t0;
+            std::vector<uint8_t> &L = lines[lb];
+            L.clear();
+            std::vector<uint64_t> lo(nr, ~0ull), le(nr, 0), pend(nr, 0);
+            t0 = Trace::now();
+            const uint64_t nreg = b.reg.size();
+            int st = ST_OK;
+            if (nreg) {
+                uint8_t *hbuf = B.host(b.slot == 0 ? Buffers::HOST_IN : Buffers::HOST_IN2, b.hbytes + 64);
+                const uint8_t *d_in = hbuf ? upload(B, Buffers::IN, hbuf, b.hbytes, s) : nullptr;
+                const uint64_t *d_rec = reinterpret_cast<const uint64_t *>(
+                    upload(B, Buffers::REC, reinterpret_cast<const uint8_t *>(b.roff.data()), 8 * b.roff.size(), s));
+                if (!d_in || !d_rec) st = ST_E_HIP;
+                std::vector<uint64_t> lend;
+                uint64_t j0 = 0;
+                while (!st && j0 < nreg) {
+                    int stop_at = 0;
+                    uint64_t cont = 0;
+                    lend.clear();
+                    const uint64_t base = L.size();
+                    auto lsink = [&](const uint8_t *p, uint64_t k) { L.insert(L.end(), p, p + k); return true; };
+                    st = decode_records(d_in, b.hbytes, S, d_rec + j0, nullptr, nreg - j0, B, s, lsink, 1ull << 30,
+                                        &stop_at, &cont, &lend);
+                    if (st) break;
+                    uint64_t got = lend.size();
+                    if (stop_at == 2) { got--; L.resize(base + (got ? lend[got - 1] : 0)); }   // its line read past the record
+                    for (uint64_t k = 0; k < got; k++) {
+                        const uint64_t i = b.reg[j0 + k];
+                        lo[i] = base + (k ? lend[k - 1] : 0);
+                        le[i] = base + lend[k];
+                        pend[i] = b.recs[i].ls + 16 + (b.roff[j0 + k + 1] - b.roff[j0 + k]);
+                    }
+                    if (stop_at == 0) break;
+                    j0 += got + 1;   // the stopping record: window path below
+                }
+            }
+            free_slots.put(b.slot);   // its bytes are on the device (decode_records synchronised)
+            tr.dec += Trace::now() - t0;
+            if (st) { status = st; free_lines.put(lb); more = false; break; }
+            // verdicts in order; accepted lines that lie back to back in L form one span
+            t0 = Trace::now();
+            WriteJob job;
+            job.buf = lb;
+            bool done = false;
+            for (uint64_t i = 0; i < nr && !done; i++) {
+                const SqRec &r = b.recs[i];
+                if (r.walk) { status = r.walk; done = true; break; }
+                if (lo[i] == ~0ull) {   // window path: its line goes to the end of L
+                    std::vector<uint8_t> one;
+                    if ((st = sq_line_window(fd, fsize, r.ls + 16, S, B, s, one, &pend[i]))) { status = st; done = true; break; }
+                    lo[i] = L.size();
+                    L.insert(L.end(), one.begin(), one.end());
+                    le[i] = L.size();
+                }
+                const uint8_t *x = L.data() + lo[i];
+                const uint64_t n = le[i] - lo[i];
+                // SplitIterator(line, "\t"): CHROM, POS (split_iterator.cpp); strtoul whole (:520-524)
+                uint64_t t1 = 0;
+                while (t1 < n && x[t1] != '\t') t1++;
+                uint64_t t2 = t1 + 1, pos = 0;
+                while (t2 < n && x[t2] != '\t') t2++;
+                if (t1 >= n || !sq_strtoul_whole(x + t1 + 1, t2 - t1 - 1, &pos)) {   // no second term / bad POS: throws
+                    status = ST_E_FORMAT;
+                    done = true;
+                    break;
+                }
+                if (!(t1 == q.ref_len && memcmp(x, q.ref, q.ref_len) == 0 && pos <= q.end)) { done = true; break; }
+                if (!job.spans.empty() && job.spans.back().second == lo[i]) job.spans.back().second = le[i];
+                else job.spans.emplace_back(lo[i], le[i]);
+                if (r.dnext == 0 || pos >= q.end) { done = true; break; }
+                if (r.sync) { ls = pend[i]; resume = true; }   // the failed lseek leaves the parse end
+            }
+            tr.eval += Trace::now() - t0;
+            jobs.put(std::move(job));
+            if (done) { more = false; break; }
+            if (b.last) { more = resume; break; }   // a sync record: walk on from its parse end
+        }
+        finish_walker();
+        tr.walk += walk_t;
+    }
+    jobs.close();
+    writer.join();
+    tr.total = Trace::now() - t_begin;
+    if (status == ST_OK && write_failed) status = ST_E_IO;
+    return status;
+}
+
 inline int sparse_query(int fd, const SparseQuery &q, Buffers &B, hipStream_t s, const Sink &sink) {
     struct stat sb;
     if (fstat(fd, &sb) != 0) return ST_E_IO;
@@ -493,162 +733,7 @@ inline int sparse_query(int fd, const SparseQuery &q, Buffers &B, hipStream_t s,
             break;
         }
     }
-    uint64_t ls = (uint64_t)lseek(fd, 0, SEEK_CUR);
-    // stage times (VCFC_SQ_TRACE=1 prints them to stderr)
-    struct Trace {
-        bool on = getenv("VCFC_SQ_TRACE") != nullptr;
-        double walk = 0, body = 0, dec = 0, eval = 0;
-        uint64_t recs = 0, batches = 0;
-        static double now() {
-            return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
-        }
-        ~Trace() {
-            if (on)
-                fprintf(stderr, "sparse_query: %llu records in %llu batches: walk %.1f ms, record bytes %.1f ms, "
-                                "GPU decode %.1f ms, verdicts+sink %.1f ms\n", (unsigned long long)recs,
-                        (unsigned long long)batches, walk * 1e3, body * 1e3, dec * 1e3, eval * 1e3);
-        }
-    } tr;
-    // linear traversal (:436-566) in batches (growing to SQ_BATCH records:
-    // the walk runs at most one batch past the reference's last record)
-    const int64_t max_seek = sq_max_seek(fd);
-    constexpr uint64_t SQ_BATCH = 4096;
-    std::vector<SqRec> recs;
-    std::vector<uint8_t> pre, lines;
-    std::vector<uint64_t> roff, lend, lineof, pend, rlen;
-    std::vector<int> lst;
-    for (uint64_t want = 32;; want = std::min<uint64_t>(want * 4, SQ_BATCH)) {
-        double t0 = Trace::now();
-        int st = sq_walk(fd, ls, want, max_seek, recs, pre);
-        if (st) return st;
-        const uint64_t nr = recs.size();
-        tr.recs += nr;
-        tr.batches++;
-        double t1 = Trace::now();
-        tr.walk += t1 - t0;
-        // record bytes [ls + 16, + 4 + LEN) of the records with sane headers,
-        // assembled in the upload staging buffer
-        roff.clear(); rlen.clear();
-        std::vector<uint64_t> reg;   // record index of each regular record
-        lst.assign(nr, ST_OK);
-        pend.assign(nr, 0);
-        uint64_t hbytes = 0;
-        for (uint64_t i = 0; i < nr; i++) {
-            if (recs[i].walk) break;
-            const SqRec &r = recs[i];
-            if (r.npre < 24) continue;
-            const uint8_t *h8 = pre.data() + r.pre + 16;
-            if ((h8[0] >> 6) != 3u || (h8[4] >> 6) != 3u) continue;
-            const uint64_t L = ((uint64_t)(h8[0] & 0x3Fu) << 24) | ((uint64_t)h8[1] << 16) | ((uint64_t)h8[2] << 8) | h8[3];
-            if (L < 4) continue;
-            roff.push_back(hbytes);
-            rlen.push_back(4 + L);
-            reg.push_back(i);
-            hbytes += 4 + L;
-        }
-        uint8_t *hbuf = B.host(Buffers::HOST_IN, hbytes + 64);
-        if (!hbuf) return ST_E_HIP;
-        {
-            uint64_t w = 0, q = 0;
-            for (uint64_t j = 0; j < reg.size(); j++) {
-                const SqRec &r = recs[reg[j]];
-                const uint64_t k = rlen[j];
-                if (16 + k <= r.npre) {
-                    memcpy(hbuf + w, pre.data() + r.pre + 16, k);
-                } else if (sq_pread(fd, hbuf + w, k, r.ls + 16) != (int64_t)k) {
-                    continue;   // short (EOF): the window path decides
-                }
-                roff[q] = w;
-                reg[q] = reg[j];
-                q++;
-                w += k;
-            }
-            roff.resize(q);
-            reg.resize(q);
-            hbytes = w;
-        }
-        t0 = Trace::now();
-        tr.body += t0 - t1;
-        // decode the regular records on the GPU; lines[lineof[i], lineof[i + 1]) of record i
-        lines.clear();
-        std::vector<uint64_t> lo(nr, ~0ull), le(nr, 0);
-        const uint64_t nreg = reg.size();
-        if (nreg) {
-            roff.push_back(hbytes);
-            const uint8_t *d_in = upload(B, Buffers::IN, hbuf, hbytes, s);
-            const uint64_t *d_rec = reinterpret_cast<const uint64_t *>(
-                upload(B, Buffers::REC, reinterpret_cast<const uint8_t *>(roff.data()), 8 * roff.size(), s));
-            if (!d_in || !d_rec) return ST_E_HIP;
-            uint64_t j0 = 0;
-            while (j0 < nreg) {
-                int stop = 0;
-                uint64_t cont = 0;
-                lend.clear();
-                const uint64_t base = lines.size();
-                auto lsink = [&](const uint8_t *p, uint64_t k) { lines.insert(lines.end(), p, p + k); return true; };
-                st = decode_records(d_in, hbytes, S, d_rec + j0, nullptr, nreg - j0, B, s, lsink, 1ull << 30,
-                                    &stop, &cont, &lend);
-                if (st) return st;
-                uint64_t got = lend.size();
-                if (stop == 2) { got--; lines.resize(base + (got ? lend[got - 1] : 0)); }   // its line read past the record
-                for (uint64_t k = 0; k < got; k++) {
-                    const uint64_t i = reg[j0 + k];
-                    lo[i] = base + (k ? lend[k - 1] : 0);
-                    le[i] = base + lend[k];
-                    pend[i] = recs[i].ls + 16 + (roff[j0 + k + 1] - roff[j0 + k]);
-                }
-                if (stop == 0) break;
-                j0 += got + 1;   // the stopping record: window path below
-            }
-        }
-        t1 = Trace::now();
-        tr.dec += t1 - t0;
-        struct EvalTime {
-            Trace &t; double t1;
-            ~EvalTime() { t.eval += Trace::now() - t1; }
-        } et{tr, t1};
-        // evaluate in order; accepted lines that lie back to back in `lines`
-        // leave in one write
-        uint64_t ps = 0, pe = 0;   // pending span of `lines`
-        auto flush = [&]() { bool ok = pe == ps || sink(lines.data() + ps, pe - ps); ps = pe = 0; return ok; };
-        for (uint64_t i = 0; i < nr; i++) {
-            const SqRec &r = recs[i];
-            if (r.walk) return flush() ? r.walk : ST_E_IO;
-            const uint8_t *L;
-            uint64_t n;
-            std::vector<uint8_t> one;
-            if (lo[i] != ~0ull) {
-                L = lines.data() + lo[i];
-                n = le[i] - lo[i];
-            } else {
-                if (!flush()) return ST_E_IO;
-                if ((st = sq_line_window(fd, fsize, r.ls + 16, S, B, s, one, &pend[i]))) return st;
-                L = one.data();
-                n = one.size();
-            }
-            // SplitIterator(line, "\t"): CHROM, POS (split_iterator.cpp); strtoul whole (:520-524)
-            uint64_t t1 = 0;
-            while (t1 < n && L[t1] != '\t') t1++;
-            uint64_t t2 = t1 + 1, pos = 0;
-            while (t2 < n && L[t2] != '\t') t2++;
-            if (t1 >= n || !sq_strtoul_whole(L + t1 + 1, t2 - t1 - 1, &pos))   // no second term / bad POS: throws
-                return flush() ? ST_E_FORMAT : ST_E_IO;
-            if (!(t1 == q.ref_len && memcmp(L, q.ref, q.ref_len) == 0 && pos <= q.end)) return flush() ? ST_OK : ST_E_IO;
-            if (lo[i] != ~0ull && pe == lo[i] && pe > ps) {
-                pe = le[i];
-            } else if (lo[i] != ~0ull) {
-                if (!flush()) return ST_E_IO;
-                ps = lo[i];
-                pe = le[i];
-            } else if (!sink(L, n)) {
-                return ST_E_IO;
-            }
-            if (r.dnext == 0 || pos >= q.end) return flush() ? ST_OK : ST_E_IO;
-            if (r.sync) ls = pend[i];   // the failed lseek leaves the parse end
-            else ls = r.ls + r.dnext;
-        }
-        if (!flush()) return ST_E_IO;
-    }
+    return sq_traverse(fd, fsize, (uint64_t)lseek(fd, 0, SEEK_CUR), S, q, B, s, sink);
 }
 
 }  // namespace vcfc_dec

@@ -36,6 +36,7 @@
 #include <vector>
 
 #include "vcfc_device.h"
+#include "vcfc_queue.h"
 
 namespace vcfc_ing {
 
@@ -87,31 +88,7 @@ inline double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-template <class T>
-struct Queue {   // bounded hand-off between the stages
-    std::mutex m;
-    std::condition_variable cv;
-    std::deque<T> q;
-    bool closed = false;
-    void put(T v) {
-        std::lock_guard<std::mutex> g(m);
-        q.push_back(std::move(v));
-        cv.notify_all();
-    }
-    bool get(T &v) {   // false once closed and empty
-        std::unique_lock<std::mutex> g(m);
-        cv.wait(g, [&] { return !q.empty() || closed; });
-        if (q.empty()) return false;
-        v = std::move(q.front());
-        q.pop_front();
-        return true;
-    }
-    void close() {
-        std::lock_guard<std::mutex> g(m);
-        closed = true;
-        cv.notify_all();
-    }
-};
+using vcfc_q::Queue;   // bounded hand-off between the stages
 
 struct InChunk {
     int slot = -1;
