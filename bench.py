@@ -405,7 +405,7 @@ def bench_ingest(args, torch, vcfc, workload):
             elapsed += time.perf_counter() - t0
         identical = open(dst, "rb").read() == want
         ctx.close()
-        res = {"metric": "end-to-end input GT bytes/sec, VCF file -> .vcfc file (row f4)",
+        res = {"metric": "end-to-end input GT bytes/sec, VCF file -> .vcfc file (compress(), BASELINE configs[2]; row f4)",
                "value": round(rows.gt_bytes * args.steps / elapsed / 1e9, 3), "unit": "GB/s", "n_gpus": 1,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
                "higher_is_better": True, "scaling": "replicas", "vs_baseline": None, "dtype": "u8",

@@ -1,0 +1,41 @@
+"""The reference's manual round trip (do-compress.sh: `./main compress`,
+`hexdump -C` of the .vcfc, `./main decompress`) run with this build's CLI in
+the place of the reference's `main`, on BASELINE configs[0] (random_vcf 100 x
+10k): the .vcfc is the reference's byte for byte and the round trip restores
+the input."""
+import gzip
+import hashlib
+import os
+import shutil
+import subprocess
+import tempfile
+
+import pytest
+
+import golden_io as G
+
+pytestmark = pytest.mark.gpu
+
+FLOW = """#!/bin/bash
+fname="$1"
+comp_fname="${fname}.vcfc"
+decomp_fname="${fname}.decompressed"
+./main compress $fname $comp_fname 2>&1 | tee compress.log
+if command -v hexdump > /dev/null; then hexdump $comp_fname -C > "$comp_fname.hexdump"; fi
+./main decompress $comp_fname $decomp_fname 2>&1 | tee decompress.log
+"""
+
+
+def test_do_compress_flow_config0():
+    with tempfile.TemporaryDirectory() as d:
+        os.symlink(os.path.join(G.REPO, "build", "main"), os.path.join(d, "main"))
+        with open(os.path.join(d, "flow.sh"), "w") as f:
+            f.write(FLOW)
+        vcf = G.gz("random_100x10000.vcf.gz")
+        with open(os.path.join(d, "test-100-10000.vcf"), "wb") as f:
+            f.write(vcf)
+        r = subprocess.run(["bash", "flow.sh", "test-100-10000.vcf"], cwd=d, capture_output=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        out = open(os.path.join(d, "test-100-10000.vcf.vcfc"), "rb").read()
+        assert hashlib.sha256(out).hexdigest() == G.manifest()["random_100x10000"]["vcfc_sha256"]
+        assert open(os.path.join(d, "test-100-10000.vcf.decompressed"), "rb").read() == vcf
