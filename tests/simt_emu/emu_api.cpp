@@ -21,6 +21,7 @@ extern "C" int emu_encode_rows(const uint8_t *buf, const uint64_t *line_off, con
     a.buf = buf; a.line_off = line_off; a.line_len = line_len; a.n = n;
     a.out = out; a.out_cap = out_cap; a.rec_off = rec_off;
     vcfc_encode_args_workspace(a, ws, L);
+    a.line_bytes_hint = getenv("EMU_WIDE_COMPACT") ? (~0ull >> 1) : total;   // (tests force the 64-lane compaction)
     a.err = (uint64_t *)(ws + L.err);
     emu::g.switches = 0;
     int st = (int)vcfc_encode_device(a, nullptr);

@@ -3,10 +3,8 @@
 the place of the reference's `main`, on BASELINE configs[0] (random_vcf 100 x
 10k): the .vcfc is the reference's byte for byte and the round trip restores
 the input."""
-import gzip
 import hashlib
 import os
-import shutil
 import subprocess
 import tempfile
 

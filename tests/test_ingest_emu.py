@@ -25,10 +25,21 @@ def check(vcf, chunk, name=""):
         assert el == el_o, (name, chunk, el, el_o)
 
 
-@pytest.mark.parametrize("chunk", [4096, 65536, 1 << 20])
-def test_reference_config1(chunk):
-    st, out, _ = E.emu_compress(G.gz("random_100x10000.vcf.gz"), chunk=chunk)
-    assert st == OK and out == G.gz("random_100x10000.vcfc.gz")
+@pytest.mark.parametrize("chunk,lines", [(4096, 900), (65536, 3000), (1 << 20, None)])
+def test_reference_config1(chunk, lines):
+    """configs[0] through the pipelined driver; with small chunks on a prefix
+    of the file (every line straddling chunks), whole with 1 MiB chunks."""
+    vcf = G.gz("random_100x10000.vcf.gz")
+    if lines is None:   # (three reader threads)
+        st, out, _ = E.emu_compress(vcf, chunk=chunk, read_threads=3)
+        assert st == OK and out == G.gz("random_100x10000.vcfc.gz")
+        return
+    cut = 0
+    while vcf[cut:cut + 1] == b"#":   # header lines
+        cut = vcf.index(b"\n", cut) + 1
+    for _ in range(lines):
+        cut = vcf.index(b"\n", cut) + 1
+    check(vcf[:cut], chunk, "config1 prefix")
 
 
 def test_reference_edge_file_and_bad_header():
@@ -101,8 +112,3 @@ def test_line_longer_than_chunk():
     check(vcf, 1 << 16, "long line, larger chunk")
 
 
-@pytest.mark.parametrize("threads", [1, 3])
-def test_read_threads(threads):
-    vcf = G.gz("random_100x10000.vcf.gz")
-    st, out, _ = E.emu_compress(vcf, chunk=3 << 20, read_threads=threads)
-    assert st == OK and out == G.gz("random_100x10000.vcfc.gz")

@@ -286,6 +286,7 @@ static int encode_rows_device_impl(const uint8_t *d_buf, const uint64_t *d_line_
     a.line_off = d_line_off;
     a.line_len = d_line_len;
     a.n = n;
+    a.line_bytes_hint = total_line_bytes;
     a.out = d_out;
     a.out_cap = out_cap;
     a.rec_off = d_rec_off;

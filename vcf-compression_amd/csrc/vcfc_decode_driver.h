@@ -43,7 +43,7 @@ struct Buffers {
     // decoded lines (D2H), HOST_IN assembles uploads; contents not kept
     enum { HOST_OUT = 0, HOST_IN, HOST_IN2, N_HOST };
     virtual uint8_t *host(int slot, uint64_t bytes) {
-        if (hv[slot].size() < bytes) hv[slot].resize(bytes);
+        if (hv[slot].size() < bytes || hv[slot].empty()) hv[slot].resize(bytes < 64 ? 64 : bytes);
         return hv[slot].data();
     }
     std::vector<uint8_t> hv[N_HOST];
@@ -182,7 +182,7 @@ inline int decode_records(const uint8_t *d_in, uint64_t n, uint64_t S, const uin
             if ((pst = plan())) return pst;
             continue;   // same i0, exact sizes
         }
-        uint8_t *host = B.host(Buffers::HOST_OUT, bytes);
+        uint8_t *host = B.host(Buffers::HOST_OUT, bytes + 64);
         if (!host) return ST_E_HIP;
         if (hipMemcpyAsync(host, d_out, bytes, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
             return ST_E_HIP;

@@ -20,6 +20,7 @@ struct VcfcEncodeArgs {
     const uint64_t *line_off;  // byte offset of line i in buf
     const uint32_t *line_len;  // length of line i, without '\n'
     uint64_t n;                // rows
+    uint64_t line_bytes_hint;  // sum of the line lengths (<= the workspace's total_line_bytes): picks the compaction shape
     // output
     uint8_t *out;              // records, concatenated in row order
     uint64_t out_cap;

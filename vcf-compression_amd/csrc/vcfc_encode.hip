@@ -9,7 +9,8 @@
 //                     1 KiB bursts; rows of another shape are queued
 //   k_encode_general  persistent waves encode the queued rows (any shape)
 //   scan<IDENT>  rec_off[i] = sum_{k<i} rec_size_k             (tiny)
-//   k_compact    16 lanes per row: staging -> final offset, 16-byte stores
+//   k_compact    16 (long rows: 64) lanes per row: staging -> final offset,
+//                16-byte stores
 //
 // Record layout (reference compress.cpp:32-100,188-199):
 //   [LEN:4 BE|0xC0][REQ:4 BE|0xC0][cols 0..7 '\t'-joined]['\t'FORMAT]['\t']
@@ -990,14 +991,21 @@ __device__ __forceinline__ uint4 stage_blk(const uint8_t *prim, const uint8_t *s
 __device__ __forceinline__ uint8_t stage_byte(const uint8_t *prim, const uint8_t *slot, uint64_t x) {
     return x < VCFC_PRIM ? prim[x] : slot[x - VCFC_PRIM];
 }
+// GROUP lanes per row: 16 (one DPP row; four rows per wave) for records of
+// a few KiB, 64 (the whole wave, DPP wave_shl) for long records.
+template <uint32_t GROUP>
+__device__ __forceinline__ uint32_t next_lane(uint32_t v) {
+    return GROUP == 16 ? vw::row_shl1(v) : vw::shl1(v, 0u);
+}
+template <uint32_t GROUP>
 __global__ __launch_bounds__(256) void k_compact(const uint8_t *__restrict__ prims,
                                                  const uint8_t *__restrict__ slots,
                                                  const uint64_t *__restrict__ slot_off,
                                                  const uint64_t *__restrict__ rec_off, uint64_t n,
                                                  uint8_t *__restrict__ out, uint64_t out_cap,
                                                  uint64_t *err) {
-    const uint32_t g = threadIdx.x >> 4, gl = threadIdx.x & 15u;
-    const uint64_t row = (uint64_t)blockIdx.x * 16 + g;
+    const uint32_t g = threadIdx.x / GROUP, gl = threadIdx.x % GROUP;
+    const uint64_t row = (uint64_t)blockIdx.x * (256 / GROUP) + g;
     const bool live = row < n;
     uint64_t d0 = 0, d1 = 0;
     if (live) { d0 = rec_off[row]; d1 = rec_off[row + 1]; }
@@ -1015,12 +1023,13 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t *__restrict__ pri
     const uint8_t hb = gl < head ? stage_byte(prim, slot, gl) : (uint8_t)0;
     const uint8_t tb = gl < tail ? stage_byte(prim, slot, head + 16 * nblk + gl) : (uint8_t)0;
     // passes run while any group of the wave has blocks left (DPP needs the whole wave)
-    for (uint64_t b0 = 0; vw::ballot(b0 < nblk); b0 += 15) {
+    for (uint64_t b0 = 0; vw::ballot(b0 < nblk); b0 += GROUP - 1) {
         const uint64_t k = b0 + gl;
         uint4 v = make_uint4(0, 0, 0, 0);
         if (k <= nblk && sz) v = stage_blk(prim, slot, k);   // block nblk: the last output block's upper bytes
-        const uint4 h = make_uint4(vw::row_shl1(v.x), vw::row_shl1(v.y), vw::row_shl1(v.z), vw::row_shl1(v.w));
-        if (gl < 15 && k < nblk) vw::gstore16(dst, head + 16 * k, realign16(v, h, head));
+        const uint4 h = make_uint4(next_lane<GROUP>(v.x), next_lane<GROUP>(v.y), next_lane<GROUP>(v.z),
+                                   next_lane<GROUP>(v.w));
+        if (gl < GROUP - 1 && k < nblk) vw::gstore16(dst, head + 16 * k, realign16(v, h, head));
     }
     if (gl < head) dst[gl] = hb;
     if (gl < tail) dst[head + 16 * nblk + gl] = tb;
@@ -1146,8 +1155,17 @@ hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t s, hipEvent_t
     e = launch_scan<0>(a.rec_size, a.n, a.partials, a.rec_off, s);
     if (e != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[3], s);
-    hipLaunchKernelGGL(k_compact, dim3((unsigned)((a.n + 15) / 16)), dim3(256), 0, s, a.prim, a.slots, a.slot_off,
-                       a.rec_off, a.n, a.out, a.out_cap, a.err);
+    // records of rows longer than 64 KiB on average (biobank-wide rows) get a
+    // whole wave each
+#ifndef VCFC_WIDE_ROW
+#define VCFC_WIDE_ROW (64ull << 10)
+#endif
+    if (a.line_bytes_hint > VCFC_WIDE_ROW * a.n)
+        hipLaunchKernelGGL(k_compact<64>, dim3((unsigned)((a.n + 3) / 4)), dim3(256), 0, s, a.prim, a.slots,
+                           a.slot_off, a.rec_off, a.n, a.out, a.out_cap, a.err);
+    else
+        hipLaunchKernelGGL(k_compact<16>, dim3((unsigned)((a.n + 15) / 16)), dim3(256), 0, s, a.prim, a.slots,
+                           a.slot_off, a.rec_off, a.n, a.out, a.out_cap, a.err);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[4], s);
     return hipSuccess;

@@ -378,6 +378,7 @@ inline int compress_stream(Source &src, const Sink &sink, Memory &M, hipStream_t
             if (!ws || !d_out) return finish(ST_E_HIP);
             VcfcEncodeArgs a;
             a.buf = d_in; a.line_off = x.line_off; a.line_len = x.line_len; a.n = n_data;
+            a.line_bytes_hint = n;
             a.out = d_out; a.out_cap = cap; a.rec_off = d_rec_off;
             vcfc_encode_args_workspace(a, ws, W);
             a.err = d_small + 4;
