@@ -547,10 +547,18 @@ def main():
     import vcfc
     import workload
 
-    dev = torch.device("cuda:%d" % local)
+    # VCFC_BENCH_REHEARSAL=1 rehearses the N > 1 path on one GPU: every rank on
+    # cuda:0, gloo with host tensors for the collectives (RCCL refuses two
+    # ranks on one device).  Never used for a reported number.
+    rehearsal = os.environ.get("VCFC_BENCH_REHEARSAL") == "1"
+    dev = torch.device("cuda:%d" % (0 if rehearsal else local))
     torch.cuda.set_device(dev)
+    cdev = torch.device("cpu") if rehearsal else dev   # collective tensors
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
     n, S = args.rows, args.samples
     rows = workload.DeviceRows(torch, vcfc, n, S, args.law, seed=1000 + rank, device=dev, row0=rank * n)
     ws_bytes = vcfc.workspace_size(n, rows.line_bytes)
@@ -559,7 +567,7 @@ def main():
     out = torch.empty(cap, dtype=torch.uint8, device=dev)
     rec = torch.empty(n + 1, dtype=torch.int64, device=dev)
     err = torch.empty(1, dtype=torch.int64, device=dev)
-    counts = torch.empty(world, dtype=torch.int64, device=dev)
+    counts = torch.empty(world, dtype=torch.int64, device=cdev)
     timer = vcfc.StageTimer()
     stream = torch.cuda.current_stream(dev).cuda_stream
 
@@ -569,7 +577,7 @@ def main():
           out.data_ptr(), cap, rec.data_ptr(), ws.data_ptr(), ws_bytes, err.data_ptr(), stream)
         if world > 1:
             # stitch: every rank learns every shard's record bytes -> its file offset
-            dist.all_gather_into_tensor(counts, rec[n:n + 1])
+            dist.all_gather_into_tensor(counts, rec[n:n + 1].to(cdev))
 
     for _ in range(args.warmup):
         step(False)
@@ -587,7 +595,7 @@ def main():
     elapsed = time.perf_counter() - t0
     stages, calls = timer.read()
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
