@@ -192,6 +192,23 @@ int vcfc_query_match_device(const uint8_t *d_in, const uint64_t *d_rec_start, ui
  * between records).  The GPU plans offsets and prefixes; the host writes. */
 uint64_t vcfc_sparse_offset(uint64_t pos);
 int vcfc_sparsify_file(vcfc_ctx *ctx, const char *in_vcfc, const char *out_sparse);
+/* Sharded sparsify (multi-GPU, one process per GPU; SURVEY §8 e).  Rank
+ * `rank` of `world` owns records [n*rank/world, n*(rank+1)/world) and plans
+ * them on its GPU with one halo record on each side (the neighbours' offsets
+ * give its first dist_to_prev and last dist_to_next).  info[4] =
+ * {lo, hi, first unparsable record (global index, ~0 = none; bytes after the
+ * last whole record count as record n), 1 if adjacent records of the planned
+ * range overlap or are out of order}.
+ * out_sparse == NULL: plan only.  Otherwise the slice is also written into
+ * out_sparse (opened without truncation): rank 0 writes the header lines, the
+ * owner of record 0 the first-offset slot.  Writing is only valid when every
+ * rank's plan reported no error and no anomaly (records then occupy disjoint
+ * ranges, so concurrent writes equal the reference's sequential ones);
+ * otherwise one rank runs vcfc_sparsify_file, which replays the reference's
+ * write order.  VCFC_E_ARG when asked to write a slice whose own plan is not
+ * clean. */
+int vcfc_sparsify_shard(vcfc_ctx *ctx, const char *in_vcfc, const char *out_sparse, int rank, int world,
+                        uint64_t info[4]);
 /* Sparse-file query: query_sparse_file_fd (reference src/main.cpp:235-582)
  * over a file written by sparsify, stdout-identical to the reference's
  * `main sparse-query`: start == end looks up the one slot of `start` and

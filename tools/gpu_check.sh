@@ -20,6 +20,7 @@ for s in $STEPS; do
     bench0) timeout -k 10 600 python bench.py --law 0 --no-cpu-baseline > "$O/bench_law0.json" 2> "$O/bench_law0.err" || { echo "bench0 failed"; tail -30 "$O/bench_law0.err"; exit 1; } ; cat "$O/bench_law0.json" ;;
     biobank) timeout -k 10 900 python bench.py --mode biobank --steps 5 --warmup 1 > "$O/bench_biobank.json" 2> "$O/bench_biobank.err" || { echo "biobank failed"; tail -30 "$O/bench_biobank.err"; exit 1; } ; cat "$O/bench_biobank.json" ;;
     profbio) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/profbio" -o run -- python3 "$R/bench.py" --mode biobank --steps 3 --warmup 1 --no-cpu-baseline > "$O/profbio.log" 2>&1) || { echo "profbio failed rc=$?"; tail -30 "$O/profbio.log"; exit 1; } ;;
+    dtests) timeout -k 10 600 python -u -m pytest tests/test_gpu_dist_sparsify.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread > "$O/pytest_d.log" 2>&1 || { echo "dtests failed rc=$?"; tail -40 "$O/pytest_d.log"; exit 1; } ;;
     wtests) timeout -k 10 900 python -u -m pytest tests/test_gpu_encode.py -x -v -k synthetic -p no:cacheprovider --timeout 300 --timeout-method thread > "$O/pytest_w.log" 2>&1 || { echo "wtests failed rc=$?"; tail -40 "$O/pytest_w.log"; exit 1; } ;;
     benchdec) timeout -k 10 600 python bench.py --mode decode > "$O/bench_decode.json" 2> "$O/bench_decode.err" || { echo "benchdec failed"; tail -30 "$O/bench_decode.err"; exit 1; } ; cat "$O/bench_decode.json" ;;
     benchsp) timeout -k 10 900 python bench.py --mode sparse --steps 5 --warmup 1 > "$O/bench_sparse.json" 2> "$O/bench_sparse.err" || { echo "benchsp failed"; tail -30 "$O/bench_sparse.err"; exit 1; } ; cat "$O/bench_sparse.json" ;;

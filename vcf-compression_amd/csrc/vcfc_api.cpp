@@ -445,53 +445,56 @@ int vcfc_sparse_plan_device(const uint8_t *d_recs, const uint64_t *d_rec_off, ui
 // one byte per syscall) or, if the plan flags overlapping/out-of-order
 // records, replays the reference's write sequence so later writes win as
 // they do there.
-int vcfc_sparsify_file(vcfc_ctx *c, const char *in_path, const char *out_path) {
-    if (!c || !in_path || !out_path) return VCFC_E_ARG;
-    if (hipSetDevice(c->device) != hipSuccess) return VCFC_E_HIP;
-    MappedFile f;
-    int st = f.open_ro(in_path);
-    if (st) return st;
-    uint64_t data_in = 0;
-    if ((st = parse_vcfc_header(f.p, f.n, &data_in, nullptr))) return st;
-    const uint8_t *recs = f.p + data_in;
-    const uint64_t rbytes = f.n - data_in;
-    std::vector<uint64_t> rec;
-    const int ist = index_records(recs, rbytes, rec);   // error after the good prefix
-    const uint64_t n = rec.size() - 1;
-    const uint64_t data_start = data_in + 8;            // header lines + 8-byte slot
-    std::vector<uint64_t> file_off(n), status(2, 0);
-    std::vector<uint8_t> prefix(16 * n);
-    if (n) {
-        const uint64_t span = rec[n];
-        if (c->in.ensure(span + 64) || c->rec.ensure(8 * (n + 1)) || c->out.ensure(16 * n) ||
-            c->off.ensure(8 * n) || c->err.ensure(16))
-            return VCFC_E_HIP;
-        hipStream_t s = c->stream;
-        if (hipMemcpyAsync(c->in.p, recs, span, hipMemcpyHostToDevice, s) ||
-            hipMemcpyAsync(c->rec.p, rec.data(), 8 * (n + 1), hipMemcpyHostToDevice, s))
-            return VCFC_E_HIP;
-        if (vcfc_sparse_plan_launch(static_cast<uint8_t *>(c->in.p), static_cast<uint64_t *>(c->rec.p), n,
-                                    data_start, static_cast<uint64_t *>(c->off.p), static_cast<uint8_t *>(c->out.p),
-                                    static_cast<uint64_t *>(c->err.p), s) != hipSuccess)
-            return VCFC_E_HIP;
-        if (hipMemcpyAsync(file_off.data(), c->off.p, 8 * n, hipMemcpyDeviceToHost, s) ||
-            hipMemcpyAsync(prefix.data(), c->out.p, 16 * n, hipMemcpyDeviceToHost, s) ||
-            hipMemcpyAsync(status.data(), c->err.p, 16, hipMemcpyDeviceToHost, s) || hipStreamSynchronize(s))
-            return VCFC_E_HIP;
-    }
-    uint64_t upto = n;   // records before the first unparsable one are written
-    if (status[0] != ~0ull && n) upto = status[0] >> 8;
-    int fd = open(out_path, O_CREAT | O_TRUNC | O_RDWR, 0600);
-    if (fd < 0) return VCFC_E_IO;
-    int w = write_all_at(fd, f.p, data_in, 0);
-    const uint8_t zero8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (!w) w = write_all_at(fd, zero8, 8, data_in);
-    const bool replay = status[1] != 0;
-    for (uint64_t i = 0; i < upto && !w; i++) {
+namespace {
+
+// Plan records [a, b) of the index on the GPU (k_sparse_plan): file offsets,
+// 16-byte prefixes; status[0] = ~0 or (first unparsable record, local to a)
+// << 8 | code, status[1] = 1 if adjacent records overlap or are out of order.
+int sparse_plan_range(vcfc_ctx *c, const uint8_t *recs, const std::vector<uint64_t> &rec, uint64_t a, uint64_t b,
+                      uint64_t data_start, std::vector<uint64_t> &file_off, std::vector<uint8_t> &prefix,
+                      uint64_t status[2]) {
+    const uint64_t n = b - a;
+    file_off.assign(n, 0);
+    prefix.assign(16 * n, 0);
+    status[0] = ~0ull;
+    status[1] = 0;
+    if (!n) return VCFC_OK;
+    const uint64_t base = rec[a], span = rec[b] - base;
+    std::vector<uint64_t> ro(n + 1);
+    for (uint64_t i = 0; i <= n; i++) ro[i] = rec[a + i] - base;
+    if (c->in.ensure(span + 64) || c->rec.ensure(8 * (n + 1)) || c->out.ensure(16 * n) || c->off.ensure(8 * n) ||
+        c->err.ensure(16))
+        return VCFC_E_HIP;
+    hipStream_t s = c->stream;
+    if (hipMemcpyAsync(c->in.p, recs + base, span, hipMemcpyHostToDevice, s) ||
+        hipMemcpyAsync(c->rec.p, ro.data(), 8 * (n + 1), hipMemcpyHostToDevice, s))
+        return VCFC_E_HIP;
+    if (vcfc_sparse_plan_launch(static_cast<uint8_t *>(c->in.p), static_cast<uint64_t *>(c->rec.p), n, data_start,
+                                static_cast<uint64_t *>(c->off.p), static_cast<uint8_t *>(c->out.p),
+                                static_cast<uint64_t *>(c->err.p), s) != hipSuccess)
+        return VCFC_E_HIP;
+    if (hipMemcpyAsync(file_off.data(), c->off.p, 8 * n, hipMemcpyDeviceToHost, s) ||
+        hipMemcpyAsync(prefix.data(), c->out.p, 16 * n, hipMemcpyDeviceToHost, s) ||
+        hipMemcpyAsync(status, c->err.p, 16, hipMemcpyDeviceToHost, s) || hipStreamSynchronize(s))
+        return VCFC_E_HIP;
+    return VCFC_OK;
+}
+
+// Write records g0 .. g0 + cnt - 1 (global indices; file_off / prefix point at
+// record g0's plan) with one pwritev each; record 0 also fills the
+// first-offset slot (host byte order, sparse.cpp:495-511).  replay (g0 == 0
+// only): the reference's exact write sequence -- a record's dist_to_next goes
+// out as 0 and the next record's step patches it (sparse.cpp:529-553) -- so
+// later writes win where records overlap.
+int sparse_write_range(int fd, const uint8_t *recs, const std::vector<uint64_t> &rec, uint64_t g0, uint64_t cnt,
+                       const uint64_t *file_off, const uint8_t *prefix, uint64_t data_start, bool replay) {
+    int w = VCFC_OK;
+    for (uint64_t i = 0; i < cnt && !w; i++) {
+        const uint64_t g = g0 + i;
         uint8_t pfx[16];
-        memcpy(pfx, prefix.data() + 16 * i, 16);
-        if (i == 0) {
-            const uint64_t voff = file_off[0] - data_start;   // host byte order (sparse.cpp:511)
+        memcpy(pfx, prefix + 16 * i, 16);
+        if (g == 0) {
+            const uint64_t voff = file_off[i] - data_start;
             w = write_all_at(fd, &voff, 8, data_start - 8);
         } else if (replay) {
             uint8_t d[8];
@@ -499,22 +502,104 @@ int vcfc_sparsify_file(vcfc_ctx *c, const char *in_path, const char *out_path) {
             w = write_all_at(fd, d, 8, file_off[i - 1] + 8);
         }
         if (w) break;
-        if (replay) memset(pfx + 8, 0, 8);   // patched by the next record's step
-        struct iovec iov[2] = {{pfx, 16}, {const_cast<uint8_t *>(recs + rec[i]), (size_t)(rec[i + 1] - rec[i])}};
-        const uint64_t want = 16 + rec[i + 1] - rec[i];
+        if (replay) memset(pfx + 8, 0, 8);
+        struct iovec iov[2] = {{pfx, 16}, {const_cast<uint8_t *>(recs + rec[g]), (size_t)(rec[g + 1] - rec[g])}};
+        const uint64_t want = 16 + rec[g + 1] - rec[g];
         ssize_t k = pwritev(fd, iov, 2, (off_t)file_off[i]);
         if (k != (ssize_t)want) {
             // short write: finish the record plainly
             std::vector<uint8_t> tmp(want);
             memcpy(tmp.data(), pfx, 16);
-            memcpy(tmp.data() + 16, recs + rec[i], want - 16);
+            memcpy(tmp.data() + 16, recs + rec[g], want - 16);
             w = write_all_at(fd, tmp.data(), want, file_off[i]);
         }
     }
+    return w;
+}
+
+// The .vcfc mapped, its header parsed and its records indexed.
+struct SparseInput {
+    MappedFile f;
+    uint64_t data_in = 0, n = 0, data_start = 0;
+    const uint8_t *recs = nullptr;
+    std::vector<uint64_t> rec;
+    int ist = VCFC_OK;   // index_records status (an error after the good prefix)
+    int open(const char *path) {
+        int st = f.open_ro(path);
+        if (st) return st;
+        if ((st = parse_vcfc_header(f.p, f.n, &data_in, nullptr))) return st;
+        recs = f.p + data_in;
+        ist = index_records(recs, f.n - data_in, rec);
+        n = rec.size() - 1;
+        data_start = data_in + 8;   // header lines + 8-byte slot
+        return VCFC_OK;
+    }
+};
+
+}  // namespace
+
+int vcfc_sparsify_file(vcfc_ctx *c, const char *in_path, const char *out_path) {
+    if (!c || !in_path || !out_path) return VCFC_E_ARG;
+    if (hipSetDevice(c->device) != hipSuccess) return VCFC_E_HIP;
+    SparseInput in;
+    int st = in.open(in_path);
+    if (st) return st;
+    const uint64_t n = in.n;
+    std::vector<uint64_t> file_off;
+    std::vector<uint8_t> prefix;
+    uint64_t status[2];
+    if ((st = sparse_plan_range(c, in.recs, in.rec, 0, n, in.data_start, file_off, prefix, status))) return st;
+    uint64_t upto = n;   // records before the first unparsable one are written
+    if (status[0] != ~0ull && n) upto = status[0] >> 8;
+    int fd = open(out_path, O_CREAT | O_TRUNC | O_RDWR, 0600);
+    if (fd < 0) return VCFC_E_IO;
+    int w = write_all_at(fd, in.f.p, in.data_in, 0);
+    const uint8_t zero8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (!w) w = write_all_at(fd, zero8, 8, in.data_in);
+    if (!w)
+        w = sparse_write_range(fd, in.recs, in.rec, 0, upto, file_off.data(), prefix.data(), in.data_start,
+                               status[1] != 0);
     close(fd);
     if (w) return w;
     if (upto < n) return VCFC_E_FORMAT;
-    return ist;
+    return in.ist;
+}
+
+int vcfc_sparsify_shard(vcfc_ctx *c, const char *in_path, const char *out_path, int rank, int world,
+                        uint64_t info[4]) {
+    if (!c || !in_path || !info || world < 1 || rank < 0 || rank >= world) return VCFC_E_ARG;
+    if (hipSetDevice(c->device) != hipSuccess) return VCFC_E_HIP;
+    SparseInput in;
+    int st = in.open(in_path);
+    if (st) return st;
+    const uint64_t n = in.n;
+    const uint64_t lo = (uint64_t)((unsigned __int128)n * (unsigned)rank / (unsigned)world);
+    const uint64_t hi = (uint64_t)((unsigned __int128)n * (unsigned)(rank + 1) / (unsigned)world);
+    const uint64_t a = lo ? lo - 1 : 0, b = hi < n ? hi + 1 : n;   // one halo record each side
+    std::vector<uint64_t> file_off;
+    std::vector<uint8_t> prefix;
+    uint64_t status[2] = {~0ull, 0};
+    if (hi > lo && (st = sparse_plan_range(c, in.recs, in.rec, a, b, in.data_start, file_off, prefix, status)))
+        return st;
+    info[0] = lo;
+    info[1] = hi;
+    info[2] = status[0] != ~0ull ? a + (status[0] >> 8) : (in.ist ? n : ~0ull);
+    info[3] = status[1];
+    if (!out_path) return VCFC_OK;
+    if (info[2] != ~0ull || info[3]) return VCFC_E_ARG;
+    int fd = open(out_path, O_CREAT | O_WRONLY, 0600);
+    if (fd < 0) return VCFC_E_IO;
+    int w = VCFC_OK;
+    if (rank == 0) {
+        w = write_all_at(fd, in.f.p, in.data_in, 0);
+        const uint8_t zero8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (!w && n == 0) w = write_all_at(fd, zero8, 8, in.data_in);   // else record 0's owner fills it
+    }
+    if (!w && hi > lo)
+        w = sparse_write_range(fd, in.recs, in.rec, lo, hi - lo, file_off.data() + (lo - a),
+                               prefix.data() + 16 * (lo - a), in.data_start, false);
+    close(fd);
+    return w;
 }
 
 uint64_t vcfc_compress_bound(uint64_t in_bytes) { return in_bytes + in_bytes / 2 + 64; }

@@ -10,7 +10,10 @@ all-gathers the byte counts (RCCL on GPU ranks, gloo in the CPU tests), and
 pwrites its bytes at the exclusive prefix.
 
 Run: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \\
-         vcf-compression_amd/dist_compress.py in.vcf out.vcfc
+         vcf-compression_amd/dist_compress.py [sparsify] in out
+
+`sparsify` shards sparsify_file the same way (records split evenly, one
+halo record each side, one all-gather of the plans' verdicts).
 """
 import os
 import sys
@@ -84,6 +87,33 @@ def compress_shard(in_path, out_path, rank, world, encode, allgather):
     return status, total, gline
 
 
+def sparsify_shards(rank, world, shard, whole, allgather):
+    """Sharded sparsify_file (reference src/sparse.cpp:290-580; SURVEY §8 e).
+
+    shard(write) -> (status, [lo, hi, first_err or None, anomaly]) plans this
+    rank's records [lo, hi) with one halo record each side and, when write is
+    true, writes them into the (already created) output; whole() -> status of
+    the single-process sparsify, which replays the reference's write order;
+    allgather(list_of_ints) -> per-rank lists.
+
+    Every rank plans; one all-gather of (status, first unparsable record,
+    anomaly) decides.  Clean everywhere: records sit at strictly increasing,
+    disjoint offsets, so the ranks write their slices concurrently and the
+    file equals the reference's sequential one.  Otherwise (out-of-order or
+    overlapping POS, a record the reference throws on) rank 0 alone runs the
+    replay.  Returns the job status (the same on every rank)."""
+    st, info = shard(False)
+    g = allgather([st, -1 if info[2] is None else int(info[2]), int(info[3])])
+    if any(x[0] for x in g):
+        return next(x[0] for x in g if x[0])
+    if all(x[1] == -1 and x[2] == 0 for x in g):
+        st, _ = shard(True)
+    else:
+        st = whole() if rank == 0 else 0
+    g = allgather([st])
+    return next((x[0] for x in g if x[0]), 0)
+
+
 def main():
     import torch  # noqa: F401  (torch first: one HIP runtime)
     import torch.distributed as dist
@@ -92,6 +122,10 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    mode = "compress"
+    if sys.argv[1] == "sparsify":
+        mode = "sparsify"
+        del sys.argv[1]
     in_path, out_path = sys.argv[1], sys.argv[2]
     dev = torch.device("cuda:%d" % local)
     torch.cuda.set_device(dev)
@@ -117,7 +151,13 @@ def main():
         dist.all_gather_into_tensor(out, t)   # RCCL over xGMI
         return out.view(world, len(vals)).cpu().tolist()
 
-    st, total, line = compress_shard(in_path, out_path, rank, world, encode, allgather)
+    if mode == "sparsify":
+        st = sparsify_shards(rank, world,
+                             lambda write: ctx.sparsify_shard(in_path, out_path if write else None, rank, world),
+                             lambda: ctx.sparsify_status(in_path, out_path), allgather)
+        line = -1
+    else:
+        st, total, line = compress_shard(in_path, out_path, rank, world, encode, allgather)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -35,6 +35,7 @@ EXPORTS = [
     "vcfc_decompress_buffer", "vcfc_decompress_file", "vcfc_decode_workspace_size",
     "vcfc_decode_records_device", "vcfc_parse_query", "vcfc_query_buffer", "vcfc_query_file",
     "vcfc_query_match_device", "vcfc_decode_selected_device", "vcfc_sparse_query_file",
+    "vcfc_sparsify_shard",
 ]
 
 
@@ -82,6 +83,8 @@ def lib():
     L.vcfc_sparse_offset.restype = u64
     L.vcfc_sparse_offset.argtypes = [u64]
     L.vcfc_sparsify_file.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p]
+    L.vcfc_sparsify_shard.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
+                                      ctypes.POINTER(u64)]
     L.vcfc_sparse_plan_device.argtypes = [vp, vp, u64, u64, vp, vp, vp, vp]
     L.vcfc_decompress_buffer.argtypes = [vp, vp, u64, vp, u64, ctypes.POINTER(u64)]
     L.vcfc_decompress_file.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p]
@@ -291,6 +294,20 @@ class Context:
     def sparsify_file(self, in_path, out_path):
         """sparsify_file (reference src/sparse.cpp:290-580)."""
         raise_for(lib().vcfc_sparsify_file(self._h, in_path.encode(), out_path.encode()))
+
+    def sparsify_status(self, in_path, out_path):
+        """sparsify_file without raising: the C status (VCFC_E_FORMAT where the
+        reference throws, after writing the records before)."""
+        return lib().vcfc_sparsify_file(self._h, in_path.encode(), out_path.encode())
+
+    def sparsify_shard(self, in_path, out_path, rank, world):
+        """This rank's slice of a sharded sparsify (vcfc_sparsify_shard):
+        out_path None plans only.  Returns (status, [lo, hi, first_err or
+        None, anomaly])."""
+        info = (ctypes.c_uint64 * 4)()
+        st = lib().vcfc_sparsify_shard(self._h, in_path.encode(), out_path.encode() if out_path else None,
+                                       rank, world, info)
+        return st, [info[0], info[1], None if info[2] == NO_ERROR else info[2], info[3]]
 
     def encode_rows(self, buf, line_off, line_len):
         """Host batch: returns (status, records bytes, rec_off, err_row)."""
