@@ -73,6 +73,7 @@ inline uint32_t mulhi(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a *
 inline uint4 gload16(const void *base, uint32_t idx) { return ((const uint4 *)base)[idx]; }
 inline uint32_t gload4(const void *base, uint32_t idx) { return ((const uint32_t *)base)[idx]; }
 inline void gstore16(void *base, uint64_t byte_off, uint4 v) { *(uint4 *)((uint8_t *)base + byte_off) = v; }
+inline void gstore16_nt(void *base, uint64_t byte_off, uint4 v) { gstore16(base, byte_off, v); }
 struct brsrc { const uint8_t *base; uint32_t bytes; };
 inline brsrc make_rsrc(const void *base, uint32_t bytes) { return brsrc{(const uint8_t *)base, bytes}; }
 inline uint32_t bload_dw(brsrc r, uint32_t off) {

@@ -85,9 +85,12 @@ __device__ __forceinline__ void ring_put(Ring &r, uint32_t pos, uint32_t b) {
 // loop of unknown trip count makes hipcc's vmcnt tracking give up on the
 // prefetch).
 // staging address of record byte f (a burst lies wholly in one region)
+// (non-temporal: k_compact reads the staging back only after the whole
+// batch, so keeping it out of L2's way helps the input stream -- about 1 %,
+// profiles/r01/ab/ab_nt_stores.txt)
 __device__ __forceinline__ void ring_stage(Ring &r, uint32_t f, uint4 v) {
-    if (r.fpos < VCFC_PRIM) vw::gstore16(r.prim, f, v);
-    else vw::gstore16(r.slot, f - VCFC_PRIM, v);
+    if (r.fpos < VCFC_PRIM) vw::gstore16_nt(r.prim, f, v);
+    else vw::gstore16_nt(r.slot, f - VCFC_PRIM, v);
 }
 __device__ __forceinline__ void ring_burst(Ring &r, uint32_t l) {
     const uint4 v = *reinterpret_cast<const uint4 *>(r.lds + ((r.fpos + 16u * l) & RMASK));

@@ -128,6 +128,12 @@ __device__ __forceinline__ void gstore16(void *base, uint64_t byte_off, uint4 v)
     t.x = v.x; t.y = v.y; t.z = v.z; t.w = v.w;
     *((g_v4u *)((__attribute__((address_space(1))) uint8_t *)base + byte_off)) = t;
 }
+// non-temporal 16-byte store (streamed data no kernel re-reads soon)
+__device__ __forceinline__ void gstore16_nt(void *base, uint64_t byte_off, uint4 v) {
+    v4u t;
+    t.x = v.x; t.y = v.y; t.z = v.z; t.w = v.w;
+    __builtin_nontemporal_store(t, (g_v4u *)((__attribute__((address_space(1))) uint8_t *)base + byte_off));
+}
 // Raw buffer resource over [base, base + bytes): loads at offsets past
 // `bytes` (checked per dword) return 0 instead of touching memory, so
 // prefetches past a row's end need no clamping.  The chunk offset goes in
