@@ -52,6 +52,12 @@ const char *vcfc_strerror(int status);
 typedef struct vcfc_ctx vcfc_ctx;
 int vcfc_ctx_create(int device, vcfc_ctx **out);
 void vcfc_ctx_destroy(vcfc_ctx *ctx);
+/* Input chunk of the pipelined file compress (vcfc_compress_file/_buffer):
+ * chunk_bytes in [4096, 3 GiB], or 0 for the default (128 MiB).  A line longer
+ * than the chunk grows that chunk (doubling) until it fits; no input is read
+ * twice.  The reference reads line by line (getline, src/compress.cpp:218);
+ * the output does not depend on the chunk size. */
+int vcfc_ctx_set_ingest_chunk(vcfc_ctx *ctx, uint64_t chunk_bytes);
 
 /* ---- one line: replaces compress_data_line (src/compress.hpp:20-23) --------
  * Appends the record for `line` (no trailing '\n'; `len` bytes) to `out`
@@ -117,6 +123,18 @@ int vcfc_compress_file(vcfc_ctx *ctx, const char *in_path, const char *out_path,
 uint64_t vcfc_compress_bound(uint64_t in_bytes);
 int vcfc_compress_buffer(vcfc_ctx *ctx, const uint8_t *in, uint64_t n, uint8_t *out, uint64_t out_cap,
                          uint64_t *out_len, int64_t *err_line);
+
+/* One rank's share of a multi-GPU compress (SURVEY §8 e): compresses the
+ * byte range [off, off + len) of in_path (whole lines: off at a line start,
+ * off + len after a '\n' or at EOF) through the same pipeline and writes the
+ * output to out_fd at out_off onwards (pwrite; nothing else in the file is
+ * touched).  *out_bytes = bytes written (on a failing line: the output of the
+ * lines before it), *err_line = 1-based line within the range, *lines =
+ * lines in the range (for global line numbers).  The concatenation of the
+ * ranks' outputs in range order equals vcfc_compress_file's output (compress()
+ * keeps no state across lines, reference src/compress.cpp:205-257). */
+int vcfc_compress_range(vcfc_ctx *ctx, const char *in_path, uint64_t off, uint64_t len, int out_fd,
+                        uint64_t out_off, uint64_t *out_bytes, int64_t *err_line, uint64_t *lines);
 
 /* ---- decoder: decompress2_fd (reference src/compress.cpp:1214-1257,
  * decompress2_data_line :741-986) ----------------------------------------
@@ -240,6 +258,16 @@ int vcfc_synth_rows_device(uint8_t *d_buf, const uint64_t *d_line_off, uint64_t 
                            const uint8_t *d_prefix, const uint64_t *d_prefix_off,
                            const float *d_row_af, uint32_t samples, int law, uint64_t seed,
                            void *stream);
+
+/* Per-record 64-bit digests of an encoded batch, in place on the GPU:
+ * d_hash[i] = digest of d_recs[d_rec_off[i] .. d_rec_off[i+1]).  Digest:
+ * h = len * 0x9E3779B97F4A7C15 + sum_k mix(w_k ^ (k * 0xD1B54A32D192ED03 +
+ * 0x8CB92BA72F3D8DD7)) mod 2^64, result mix(h); w_k = bytes [8k, 8k+8)
+ * little-endian, zero-padded; mix = splitmix64's finaliser.  Lets a caller
+ * verify multi-GB batches against a CPU encode by comparing 8 B per row (no
+ * reference counterpart).  Enqueued on `stream`. */
+int vcfc_record_hash_device(const uint8_t *d_recs, const uint64_t *d_rec_off, uint64_t n, uint64_t *d_hash,
+                            void *stream);
 
 #ifdef __cplusplus
 }

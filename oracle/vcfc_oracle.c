@@ -656,3 +656,85 @@ done:
     *out_len = o;
     return st;
 }
+
+/* ------------------------------------------------------------------------
+ * Batch checker (not a reference function): the 64-bit record digest that
+ * libvcfc's vcfc_record_hash_device computes on the GPU, and a threaded
+ * encode of many rows that returns only each record's digest and size, so
+ * full 1M-row batches can be compared without shipping the records.
+ *
+ * vcfo_hash64(p, n):  h = n * G + sum_k mix(w_k ^ (k * K1 + K2))  (mod 2^64),
+ * result mix(h), where w_k = bytes [8k, 8k + 8) of p little-endian
+ * (zero-padded) and mix = the splitmix64 finaliser. */
+static uint64_t mix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+uint64_t vcfo_hash64(const uint8_t *p, size_t n) {
+    uint64_t h = (uint64_t)n * 0x9E3779B97F4A7C15ull;
+    for (size_t k = 0; 8 * k < n; k++) {
+        uint64_t w = 0;
+        const size_t m = n - 8 * k < 8 ? n - 8 * k : 8;
+        memcpy(&w, p + 8 * k, m);   /* little-endian host */
+        h += mix64(w ^ ((uint64_t)k * 0xD1B54A32D192ED03ull + 0x8CB92BA72F3D8DD7ull));
+    }
+    return mix64(h);
+}
+
+#include <pthread.h>
+
+typedef struct {
+    const uint8_t *buf;
+    const uint64_t *off;
+    const uint32_t *len;
+    uint64_t lo, hi;
+    uint64_t *hash;
+    uint32_t *size;
+    int32_t *status;
+} rows_job_t;
+
+static void *rows_worker(void *arg) {
+    rows_job_t *j = (rows_job_t *)arg;
+    size_t cap = 0;
+    uint8_t *tmp = NULL;
+    for (uint64_t i = j->lo; i < j->hi; i++) {
+        const size_t want = vcfo_encode_bound(j->len[i]);
+        if (want > cap) {
+            free(tmp);
+            cap = want * 2;
+            tmp = (uint8_t *)malloc(cap);
+        }
+        size_t n = 0;
+        const int st = vcfo_encode_line(j->buf + j->off[i], j->len[i], 1, tmp, cap, &n);
+        j->status[i] = st;
+        j->size[i] = st == VCFO_OK ? (uint32_t)n : 0u;
+        j->hash[i] = st == VCFO_OK ? vcfo_hash64(tmp, n) : 0u;
+    }
+    free(tmp);
+    return NULL;
+}
+
+/* Encode rows buf[off[i] .. + len[i]) (no '\n') with `threads` threads:
+ * per row its status, record size and vcfo_hash64 of the record. */
+int vcfo_encode_rows_hash(const uint8_t *buf, const uint64_t *off, const uint32_t *len, uint64_t n, int threads,
+                          uint64_t *hash, uint32_t *size, int32_t *status) {
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    pthread_t th[256];
+    rows_job_t jobs[256];
+    for (int t = 0; t < threads; t++) {
+        jobs[t].buf = buf; jobs[t].off = off; jobs[t].len = len;
+        jobs[t].lo = n * (uint64_t)t / (uint64_t)threads;
+        jobs[t].hi = n * (uint64_t)(t + 1) / (uint64_t)threads;
+        jobs[t].hash = hash; jobs[t].size = size; jobs[t].status = status;
+        if (pthread_create(&th[t], NULL, rows_worker, &jobs[t]) != 0) {
+            for (int u = 0; u < t; u++) pthread_join(th[u], NULL);
+            return -1;
+        }
+    }
+    for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+    return 0;
+}

@@ -30,6 +30,11 @@ int vcfo_sparsify(const uint8_t *in, size_t n, const char *out_path);
 int vcfo_sparse_query(const char *path, const uint8_t *qref, size_t qref_len, int has_range, uint64_t qstart,
                       uint64_t qend, uint8_t *out, size_t cap, size_t *out_len);
 int vcfo_strtoul_whole(const uint8_t *s, size_t n, uint64_t *out);
+/* batch checker: record digest (= vcfc_record_hash_device) and a threaded
+ * encode returning per-row status / record size / digest */
+uint64_t vcfo_hash64(const uint8_t *p, size_t n);
+int vcfo_encode_rows_hash(const uint8_t *buf, const uint64_t *off, const uint32_t *len, uint64_t n, int threads,
+                          uint64_t *hash, uint32_t *size, int32_t *status);
 #ifdef __cplusplus
 }
 #endif

@@ -32,9 +32,21 @@ def lib():
                                 ctypes.POINTER(u64), u64]
         L.emu_sparse_query.argtypes = [ctypes.c_char_p, ctypes.c_char_p, u64, ctypes.c_int, u64, u64, ctypes.c_int]
         L.emu_compress.argtypes = [ctypes.c_char_p, u64, vp, u64, ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_int64),
-                                   u64, ctypes.c_int]
+                                   u64, ctypes.c_int, u64]
+        L.emu_record_hash.argtypes = [vp, vp, u64, vp]
         _lib = L
     return _lib
+
+
+def emu_record_hash(recs, rec_off):
+    """Per-record digests of `recs` (bytes) at rec_off (n + 1) on the emulator."""
+    n = len(rec_off) - 1
+    out = np.zeros(max(n, 1), dtype=np.uint64)
+    src = np.frombuffer(recs + b"\0" * 16, dtype=np.uint8)
+    ro = np.ascontiguousarray(rec_off, dtype=np.uint64)
+    st = lib().emu_record_hash(src.ctypes.data, ro.ctypes.data, n, out.ctypes.data)
+    assert st == 0
+    return out[:n]
 
 
 def data_lines(vcf):
@@ -119,7 +131,7 @@ def emu_sparse_query(path, ref, has_range, start, end):
         return st, f.read()
 
 
-def emu_compress(vcf, chunk=4096, read_threads=2, cap=None):
+def emu_compress(vcf, chunk=4096, read_threads=2, cap=None, max_chunk=0):
     """compress() through the product ingest pipeline on the emulator:
     (status, bytes, err_line)."""
     cap = cap or 2 * len(vcf) + 4096
@@ -127,5 +139,5 @@ def emu_compress(vcf, chunk=4096, read_threads=2, cap=None):
     n = ctypes.c_uint64(0)
     el = ctypes.c_int64(-1)
     st = lib().emu_compress(vcf, len(vcf), out.ctypes.data, cap, ctypes.byref(n), ctypes.byref(el), chunk,
-                            read_threads)
+                            read_threads, max_chunk)
     return st, out[:n.value].tobytes(), el.value

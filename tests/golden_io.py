@@ -65,6 +65,34 @@ def oracle_encode_line(line, add_newline=True):
     return st, buf.raw[:n.value]
 
 
+def oracle_hash64(rec):
+    """vcfo_hash64: the record digest vcfc_record_hash_device computes."""
+    lib = oracle()
+    lib.vcfo_hash64.restype = ctypes.c_uint64
+    lib.vcfo_hash64.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
+    return lib.vcfo_hash64(rec, len(rec))
+
+
+def oracle_encode_rows_hash(buf, line_off, line_len, threads=8):
+    """Threaded oracle encode of rows buf[line_off[i] .. + line_len[i]):
+    (status int32[n], record size uint32[n], digest uint64[n]).  `buf` is a
+    numpy uint8 array (or bytes)."""
+    import numpy as np
+    lib = oracle()
+    vp = ctypes.c_void_p
+    lib.vcfo_encode_rows_hash.argtypes = [vp, vp, vp, ctypes.c_uint64, ctypes.c_int, vp, vp, vp]
+    b = np.frombuffer(buf, dtype=np.uint8) if isinstance(buf, (bytes, bytearray)) else buf
+    off = np.ascontiguousarray(line_off, dtype=np.uint64)
+    ln = np.ascontiguousarray(line_len, dtype=np.uint32)
+    n = len(off)
+    st = np.zeros(n, dtype=np.int32)
+    size = np.zeros(n, dtype=np.uint32)
+    h = np.zeros(n, dtype=np.uint64)
+    assert lib.vcfo_encode_rows_hash(b.ctypes.data, off.ctypes.data, ln.ctypes.data, n, threads, h.ctypes.data,
+                                     size.ctypes.data, st.ctypes.data) == 0
+    return st, size, h
+
+
 def oracle_compress(data):
     lib = oracle()
     cap = len(data) * 2 + 1024

@@ -139,7 +139,7 @@ struct BufSource : vcfc_ing::Source {
 }  // namespace
 
 extern "C" int emu_compress(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len,
-                            int64_t *err_line, uint64_t chunk, int read_threads) {
+                            int64_t *err_line, uint64_t chunk, int read_threads, uint64_t max_chunk) {
     uint64_t o = 0;
     auto sink = [&](const uint8_t *p, uint64_t k) {
         if (o + k > cap) return false;
@@ -154,7 +154,13 @@ extern "C" int emu_compress(const uint8_t *in, uint64_t n, uint8_t *out, uint64_
     vcfc_ing::Config cfg;
     cfg.chunk = chunk;
     cfg.read_threads = read_threads;
+    if (max_chunk) cfg.max_chunk = max_chunk;
     int st = vcfc_ing::compress_stream(src, sink, M, nullptr, cfg, err_line);
     *out_len = o;
     return st;
+}
+
+// Per-record digests (csrc/vcfc_check.hip) on the emulator.
+extern "C" int emu_record_hash(const uint8_t *recs, const uint64_t *rec_off, uint64_t n, uint64_t *out) {
+    return (int)vcfc_record_hash(recs, rec_off, n, out, nullptr);
 }

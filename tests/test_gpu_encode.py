@@ -193,7 +193,7 @@ def test_logical_shards_stitch_on_one_gpu(vcfc, world):
                     slots[rank] = vals
                     bar.wait()
                     return list(slots)
-                res[rank] = D.compress_shard(ip, op, rank, world, ctx.compress_status, allgather)
+                res[rank] = D.compress_shard(ip, op, rank, world, ctx.compress_range, allgather)
 
         ts = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
         for t in ts:

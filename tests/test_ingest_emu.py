@@ -103,12 +103,41 @@ def test_empty_and_tiny_inputs():
             check(vcf, chunk, repr(vcf))
 
 
-def test_line_longer_than_chunk():
-    """The driver refuses (E_ARG) a line longer than its chunk; the C ABI then
-    reruns with the whole input as one chunk (vcfc_api.cpp)."""
-    vcf = D.header(2000) + b"\t".join([b"1", b"2", b"a", b"b", b"c", b"d", b"e", b"f", b"GT"] + [b"0|1"] * 2000) + b"\n"
-    st, out, _ = E.emu_compress(vcf, chunk=4096)
+def long_line_file(rnd, n_short, long_samples, samples=40):
+    """Short rows with a few rows of `long_samples` tokens mixed in (at the
+    start, the middle, and as an unterminated last line)."""
+    lines = D.header(samples).rstrip(b"\n").split(b"\n")
+    rows = D.rows(rnd, n_short, samples, escapes=0.03)
+    big = [b"\t".join([b"1", b"%d" % (10 + k), b"a", b"b", b"c", b"d", b"e", b"f", b"GT"] +
+                       [rnd.choice([b"0|0", b"0|1", b"1|1", b"0|2"]) for _ in range(n)])
+           for k, n in enumerate(long_samples)]
+    body = [big[0]] + rows[:n_short // 2] + big[1:-1] + rows[n_short // 2:] + [big[-1]]
+    return b"\n".join(lines + body)
+
+
+@pytest.mark.parametrize("chunk", [4096, 8192])
+def test_line_longer_than_chunk(chunk):
+    """A line longer than the chunk grows that chunk (doubling, its bytes
+    kept) until the line fits: one pass, output identical to the reference's
+    (compress() reads line by line, src/compress.cpp:218)."""
+    rnd = random.Random(chunk)
+    vcf = long_line_file(rnd, 50, [2000, 5000, 1100, 9000])   # lines of 4.4 KB .. 36 KB
+    check(vcf, chunk, "long lines")
+    st, out, _ = E.emu_compress(vcf, chunk=chunk)
+    assert st == OK
+    # a single line longer than every chunk, no header
+    vcf = b"\t".join([b"1", b"2", b"a", b"b", b"c", b"d", b"e", b"f", b"GT"] + [b"0|1"] * 3000)
+    check(vcf, chunk, "one long line")
+
+
+def test_line_longer_than_max_chunk():
+    """Growth stops at cfg.max_chunk: E_ARG, and the lines before the long one
+    are written (the C ABI's limit is 3 GiB; a record's LEN is < 2^30)."""
+    rnd = random.Random(9)
+    lines = D.header(40).rstrip(b"\n").split(b"\n") + D.rows(rnd, 20, 40)
+    head = b"\n".join(lines) + b"\n"
+    vcf = head + b"\t".join([b"1", b"2", b"a", b"b", b"c", b"d", b"e", b"f", b"GT"] + [b"0|1"] * 5000) + b"\n"
+    st, out, _ = E.emu_compress(vcf, chunk=4096, max_chunk=16384)
     assert st == E_ARG
-    check(vcf, 1 << 16, "long line, larger chunk")
-
-
+    st_o, want, _ = G.oracle_compress(head)
+    assert st_o == OK and want.startswith(out) and len(out) > 0

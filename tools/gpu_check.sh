@@ -39,6 +39,7 @@ for s in $STEPS; do
            n=$(echo $P | cut -d' ' -f1)
            (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --pmc $P --kernel-trace --output-format csv -d "$O/pmc_$n" -o run -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$O/pmc_$n.log" 2>&1) || { echo "pmc $n failed rc=$?"; tail -30 "$O/pmc_$n.log"; exit 1; }
          done ;;
+    ptest) timeout -k 10 1000 python -u -m pytest ${PT_ARGS} -x -v -p no:cacheprovider --timeout 400 --timeout-method thread > "$O/pytest_sel.log" 2>&1 || { echo "ptest failed rc=$?"; tail -60 "$O/pytest_sel.log"; exit 1; } ; tail -5 "$O/pytest_sel.log" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

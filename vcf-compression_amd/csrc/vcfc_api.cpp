@@ -85,6 +85,7 @@ struct vcfc_ctx {
     DevBuf ing_dev[vcfc_ing::Memory::N_DEV];
     HostBuf ing_host[vcfc_ing::Memory::N_HOST];
     HostBuf dec_host[vcfc_dec::Buffers::N_HOST];
+    uint64_t ingest_chunk = 0;   // 0: default (128 MiB)
 };
 
 namespace {
@@ -181,12 +182,14 @@ struct CtxIngestMemory : vcfc_ing::Memory {
     }
 };
 
+// bytes [base, base + n) of a file
 struct FdSource : vcfc_ing::Source {
     int fd;
-    uint64_t n;
-    FdSource(int f, uint64_t size) : fd(f), n(size) {}
+    uint64_t n, base;
+    FdSource(int f, uint64_t size, uint64_t base_off = 0) : fd(f), n(size), base(base_off) {}
     uint64_t size() const override { return n; }
     bool read(uint8_t *dst, uint64_t off, uint64_t k) override {
+        off += base;
         while (k) {
             const ssize_t r = pread(fd, dst, std::min<uint64_t>(k, 1ull << 30), (off_t)off);
             if (r <= 0) return false;
@@ -207,10 +210,12 @@ struct MemSource : vcfc_ing::Source {
     }
 };
 
-// chunk size: 128 MiB, or the whole input when smaller
-vcfc_ing::Config ingest_config(uint64_t n) {
+// chunk size: the context's (vcfc_ctx_set_ingest_chunk), else 128 MiB; never
+// more than the input (rounded up to 4 KiB)
+vcfc_ing::Config ingest_config(const vcfc_ctx *c, uint64_t n) {
     vcfc_ing::Config cfg;
-    cfg.chunk = std::min<uint64_t>(128ull << 20, std::max<uint64_t>((n + 4095) & ~4095ull, 4096));
+    const uint64_t want = c->ingest_chunk ? c->ingest_chunk : (128ull << 20);
+    cfg.chunk = std::min<uint64_t>(want, std::max<uint64_t>((n + 4095) & ~4095ull, 4096));
     return cfg;
 }
 
@@ -262,6 +267,12 @@ void vcfc_ctx_destroy(vcfc_ctx *c) {
     for (auto &b : c->dec_host) b.release();
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
+}
+
+int vcfc_ctx_set_ingest_chunk(vcfc_ctx *c, uint64_t chunk_bytes) {
+    if (!c || (chunk_bytes && (chunk_bytes < 4096 || chunk_bytes > (3ull << 30)))) return VCFC_E_ARG;
+    c->ingest_chunk = chunk_bytes;
+    return VCFC_OK;
 }
 
 uint64_t vcfc_encode_bound(uint64_t n_rows, uint64_t total_line_bytes) {
@@ -623,13 +634,8 @@ int vcfc_compress_buffer(vcfc_ctx *c, const uint8_t *in, uint64_t n, uint8_t *ou
     };
     MemSource src(in, n);
     CtxIngestMemory M(c);
-    vcfc_ing::Config cfg = ingest_config(n);
-    int st = vcfc_ing::compress_stream(src, sink, M, c->stream, cfg, err_line);
-    if (st == VCFC_E_ARG && !full) {   // a line longer than a chunk: the whole input as one chunk
-        o = 0;
-        cfg.chunk = n + 4096;
-        st = vcfc_ing::compress_stream(src, sink, M, c->stream, cfg, err_line);
-    }
+    const vcfc_ing::Config cfg = ingest_config(c, n);
+    const int st = vcfc_ing::compress_stream(src, sink, M, c->stream, cfg, err_line);
     *out_len = o;
     if (full) return VCFC_E_NOSPACE;
     return st;
@@ -659,15 +665,43 @@ int vcfc_compress_file(vcfc_ctx *c, const char *in_path, const char *out_path, i
     };
     FdSource src(fd, n);
     CtxIngestMemory M(c);
-    vcfc_ing::Config cfg = ingest_config(n);
+    const vcfc_ing::Config cfg = ingest_config(c, n);
     int s = vcfc_ing::compress_stream(src, sink, M, c->stream, cfg, err_line);
-    if (s == VCFC_E_ARG) {   // a line longer than a chunk: start over with the whole input as one chunk
-        if (ftruncate(ofd, 0) != 0 || lseek(ofd, 0, SEEK_SET) != 0) { close(fd); close(ofd); return VCFC_E_IO; }
-        cfg.chunk = n + 4096;
-        s = vcfc_ing::compress_stream(src, sink, M, c->stream, cfg, err_line);
-    }
     close(fd);
     if (close(ofd) != 0 && s == VCFC_OK) s = VCFC_E_IO;
+    return s;
+}
+
+// One rank's share of a sharded compress (SURVEY §8 e): the line-aligned byte
+// range [off, off + len) of in_path through the same pipeline, its output
+// written to out_fd from out_off on (pwrite; the caller places it).
+int vcfc_compress_range(vcfc_ctx *c, const char *in_path, uint64_t off, uint64_t len, int out_fd, uint64_t out_off,
+                        uint64_t *out_bytes, int64_t *err_line, uint64_t *lines) {
+    if (!c || !in_path || out_fd < 0 || !out_bytes) return VCFC_E_ARG;
+    *out_bytes = 0;
+    if (err_line) *err_line = -1;
+    if (lines) *lines = 0;
+    if (hipSetDevice(c->device) != hipSuccess) return VCFC_E_HIP;
+    int fd = open(in_path, O_RDONLY);
+    if (fd < 0) return VCFC_E_IO;
+    struct stat st;
+    if (fstat(fd, &st) != 0 || off > (uint64_t)st.st_size || len > (uint64_t)st.st_size - off) {
+        close(fd);
+        return VCFC_E_ARG;
+    }
+    posix_fadvise(fd, (off_t)off, (off_t)len, POSIX_FADV_SEQUENTIAL);
+    uint64_t o = 0;
+    auto sink = [&](const uint8_t *p, uint64_t k) {
+        if (write_all_at(out_fd, p, k, out_off + o)) return false;
+        o += k;
+        return true;
+    };
+    FdSource src(fd, len, off);
+    CtxIngestMemory M(c);
+    const vcfc_ing::Config cfg = ingest_config(c, len);
+    const int s = vcfc_ing::compress_stream(src, sink, M, c->stream, cfg, err_line, lines);
+    close(fd);
+    *out_bytes = o;
     return s;
 }
 
@@ -848,6 +882,13 @@ int vcfc_query_match_device(const uint8_t *d_in, const uint64_t *d_rec_start, ui
     VcfcQuery q;
     q.ref = d_ref; q.ref_len = (uint32_t)ref_len; q.has_range = has_range ? 1u : 0u; q.start = start; q.end = end;
     return vcfc_query_match(d_in, d_rec_start, n, q, d_flag, d_err, static_cast<hipStream_t>(stream)) == hipSuccess
+               ? VCFC_OK : VCFC_E_HIP;
+}
+
+int vcfc_record_hash_device(const uint8_t *d_recs, const uint64_t *d_rec_off, uint64_t n, uint64_t *d_hash,
+                            void *stream) {
+    if (n && (!d_recs || !d_rec_off || !d_hash)) return VCFC_E_ARG;
+    return vcfc_record_hash(d_recs, d_rec_off, n, d_hash, static_cast<hipStream_t>(stream)) == hipSuccess
                ? VCFC_OK : VCFC_E_HIP;
 }
 

@@ -119,6 +119,8 @@ hipError_t vcfc_decode_write(const VcfcDecodeArgs &a, uint64_t first, uint64_t l
 // error, bytes, lines, parse end}
 hipError_t vcfc_decode_stream(const uint8_t *in, uint64_t n, uint64_t p, uint64_t S, uint64_t max_lines,
                               uint8_t *out, uint64_t *st, hipStream_t s);
+// per-record 64-bit digests of records[rec_off[i], rec_off[i + 1]) (vcfc_check.hip)
+hipError_t vcfc_record_hash(const uint8_t *recs, const uint64_t *rec_off, uint64_t n, uint64_t *out, hipStream_t s);
 // exclusive u32 -> u64 scan with out[n] = total (shared with the encoder)
 hipError_t vcfc_scan_u32(const uint32_t *in, uint64_t n, uint64_t *partials, uint64_t *out, hipStream_t s);
 

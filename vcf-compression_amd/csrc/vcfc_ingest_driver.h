@@ -65,7 +65,9 @@ struct Memory {
 };
 
 struct Config {
-    uint64_t chunk = 256ull << 20;   // input bytes per chunk (lines must be shorter)
+    uint64_t chunk = 256ull << 20;   // input bytes per chunk; a chunk grows to hold a longer line
+    uint64_t max_chunk = 3ull << 30; // growth limit (line offsets in a chunk are 32-bit; a record's
+                                     // LEN header holds < 2^30 anyway, reference src/utils.hpp:160)
     int read_threads = 8;
 };
 
@@ -93,9 +95,12 @@ using vcfc_q::Queue;   // bounded hand-off between the stages
 struct InChunk {
     int slot = -1;
     int dslot = -1;       // device copy (set by the uploader)
+    uint8_t *host = nullptr;       // pinned copy (slot `slot`)
+    const uint8_t *dev = nullptr;  // device copy (slot `dslot`)
     uint64_t bytes = 0;   // whole lines, the last one ending with '\n'
-    bool ok = true;       // false: read error, or a line longer than a chunk
+    bool ok = true;       // false: read or allocation error, or a line longer than cfg.max_chunk
     bool long_line = false;
+    bool alloc_failed = false;
 };
 
 struct PassLine {
@@ -106,6 +111,7 @@ struct PassLine {
 
 struct OutChunk {
     int slot = -1;
+    const uint8_t *data = nullptr;        // pinned records (slot `slot`)
     uint64_t rec_bytes = 0;               // records of the good rows
     std::vector<uint64_t> rec_off;        // only when pass lines are interleaved
     std::vector<PassLine> pass;           // the ones to write
@@ -115,30 +121,34 @@ struct OutChunk {
 }  // namespace detail
 
 // Compress `src` into `sink`.  *err_line = 1-based line of the failing line
-// (-1 if none).  ST_E_ARG: a line longer than cfg.chunk (the lines before it
-// may have been written; the caller restarts with a larger chunk).
+// (-1 if none); *lines_out = lines consumed ('\n'-terminated, an unterminated
+// last line counts as one) when the whole input was compressed.  Chunks hold cfg.chunk bytes of whole lines; a line longer
+// than that grows its chunk (doubling) until the line fits, so no input is
+// read twice.  ST_E_ARG: a line longer than cfg.max_chunk (the lines before
+// it have been written).  Every buffer is sized per chunk: the pinned output
+// slots by the chunk's actual record bytes.
 inline int compress_stream(Source &src, const Sink &sink, Memory &M, hipStream_t s, const Config &cfg,
-                           int64_t *err_line) {
+                           int64_t *err_line, uint64_t *lines_out = nullptr) {
     using namespace detail;
     if (err_line) *err_line = -1;
+    if (lines_out) *lines_out = 0;
     const uint64_t N = src.size();
     const uint64_t C = cfg.chunk;
-    const uint64_t CX = C + 16;   // a chunk may gain the '\n' after an unterminated last line
     if (N == 0) return ST_OK;
+    if (C < 16 || C > cfg.max_chunk) return ST_E_ARG;
     uint8_t *hin[3];
-    for (int k = 0; k < 3; k++)
-        if (!(hin[k] = static_cast<uint8_t *>(M.host(Memory::H_IN0 + k, CX + 64)))) return ST_E_HIP;
-    uint8_t *hout[2];
-    const uint64_t out_cap = vcfc_record_bound(CX / 2 + 1, CX) + 64;
-    for (int k = 0; k < 2; k++)
-        if (!(hout[k] = static_cast<uint8_t *>(M.host(Memory::H_OUT0 + k, out_cap)))) return ST_E_HIP;
+    uint64_t hin_cap[3];
+    for (int k = 0; k < 3; k++) {
+        hin_cap[k] = C + 64;   // + the '\n' after an unterminated last line
+        if (!(hin[k] = static_cast<uint8_t *>(M.host(Memory::H_IN0 + k, hin_cap[k])))) return ST_E_HIP;
+    }
+    uint8_t *hout[2] = {nullptr, nullptr};
+    uint64_t hout_cap[2] = {0, 0};
     uint64_t *hsmall = static_cast<uint64_t *>(M.host(Memory::H_SMALL, 64));
-    uint8_t *d_inb[2] = {static_cast<uint8_t *>(M.dev(Memory::D_IN0, CX + 64)),
-                         static_cast<uint8_t *>(M.dev(Memory::D_IN1, CX + 64))};
-    const VcfcLineIndexLayout L1 = vcfc_line_index_layout(CX, 0);
-    uint8_t *d_ix1 = static_cast<uint8_t *>(M.dev(Memory::D_IX1, L1.total1));
+    uint8_t *d_inb[2] = {nullptr, nullptr};
+    uint64_t d_inb_cap[2] = {0, 0};
     uint64_t *d_small = static_cast<uint64_t *>(M.dev(Memory::D_SMALL, 64));
-    if (!hsmall || !d_inb[0] || !d_inb[1] || !d_ix1 || !d_small) return ST_E_HIP;
+    if (!hsmall || !d_small) return ST_E_HIP;
     hipStream_t s_copy = nullptr;
     hipEvent_t ev_up[2] = {nullptr, nullptr};
     if (hipStreamCreateWithFlags(&s_copy, hipStreamNonBlocking) != hipSuccess) return ST_E_HIP;
@@ -160,16 +170,8 @@ inline int compress_stream(Source &src, const Sink &sink, Memory &M, hipStream_t
     const double t_begin = now_s();
     std::thread reader([&] {
         uint64_t pos = 0;
-        while (pos < N) {
-            int slot;
-            if (!free_in.get(slot)) break;
-            uint8_t *b = hin[slot];
-            InChunk ch;
-            ch.slot = slot;
-            const uint64_t c0 = carry.size();
-            if (c0) memcpy(b, carry.data(), c0);
-            const uint64_t want = std::min<uint64_t>(C - c0, N - pos);
-            // parallel reads of [pos, pos + want)
+        // read [pos, pos + want) into b + at with up to cfg.read_threads threads
+        auto read_into = [&](uint8_t *b, uint64_t at, uint64_t want) {
             const int T = want >= (1u << 20) ? std::max(1, cfg.read_threads) : 1;
             std::vector<std::thread> ts;
             std::vector<char> ok(T, 1);
@@ -177,27 +179,66 @@ inline int compress_stream(Source &src, const Sink &sink, Memory &M, hipStream_t
             for (int t = 0; t < T; t++) {
                 const uint64_t a = t * per, e = std::min(want, a + per);
                 if (a >= e) continue;
-                ts.emplace_back([&, t, a, e] { ok[t] = src.read(b + c0 + a, pos + a, e - a) ? 1 : 0; });
+                ts.emplace_back([&, t, a, e] { ok[t] = src.read(b + at + a, pos + a, e - a) ? 1 : 0; });
             }
             const double r0 = now_s();
             for (auto &t : ts) t.join();
             t_read += now_s() - r0;
-            for (char o : ok) ch.ok = ch.ok && o;
+            bool all = true;
+            for (char o : ok) all = all && o;
             pos += want;
-            uint64_t total = c0 + want;
+            return all;
+        };
+        while (pos < N) {
+            int slot;
+            if (!free_in.get(slot)) break;
+            InChunk ch;
+            ch.slot = slot;
+            uint8_t *b = hin[slot];
+            const uint64_t c0 = carry.size();
+            uint64_t lim = std::max<uint64_t>(C, c0);   // chunk bytes this time
+            if (lim + 64 > hin_cap[slot]) {
+                if (!(b = static_cast<uint8_t *>(M.host(Memory::H_IN0 + slot, lim + 64)))) {
+                    ch.ok = false; ch.alloc_failed = true;
+                    filled.put(ch);
+                    break;
+                }
+                hin[slot] = b;
+                hin_cap[slot] = lim + 64;
+            }
+            if (c0) memcpy(b, carry.data(), c0);
+            uint64_t total = c0;
+            uint64_t scanned = c0;   // bytes [0, scanned) hold no '\n' (carry holds none)
+            const uint8_t *nl = nullptr;
+            for (;;) {
+                const uint64_t want = std::min<uint64_t>(lim - total, N - pos);
+                ch.ok = read_into(b, total, want) && ch.ok;
+                total += want;
+                if (pos >= N || !ch.ok) break;
+                nl = static_cast<const uint8_t *>(memrchr(b + scanned, '\n', total - scanned));
+                if (nl) break;
+                scanned = total;
+                // a line longer than the chunk: double the chunk, keep its bytes
+                if (lim >= cfg.max_chunk) { ch.ok = false; ch.long_line = true; break; }
+                const uint64_t grown = std::min<uint64_t>(2 * lim, cfg.max_chunk);
+                std::vector<uint8_t> keep(b, b + total);
+                if (!(b = static_cast<uint8_t *>(M.host(Memory::H_IN0 + slot, grown + 64)))) {
+                    ch.ok = false; ch.alloc_failed = true;
+                    break;
+                }
+                memcpy(b, keep.data(), total);
+                hin[slot] = b;
+                hin_cap[slot] = grown + 64;
+                lim = grown;
+            }
+            ch.host = b;
             carry.clear();
-            if (pos >= N) {
+            if (ch.ok && pos >= N) {
                 if (total && b[total - 1] != '\n') b[total++] = '\n';   // getline returns an unterminated last line
                 ch.bytes = total;
-            } else {
-                const uint8_t *nl = static_cast<const uint8_t *>(memrchr(b, '\n', total));
-                if (!nl) {   // a line longer than a chunk
-                    ch.ok = false;
-                    ch.long_line = true;
-                } else {
-                    ch.bytes = (uint64_t)(nl - b) + 1;
-                    carry.assign(b + ch.bytes, b + total);
-                }
+            } else if (ch.ok) {
+                ch.bytes = (uint64_t)(nl - b) + 1;
+                carry.assign(b + ch.bytes, b + total);
             }
             filled.put(ch);
             if (!ch.ok) break;
@@ -217,7 +258,12 @@ inline int compress_stream(Source &src, const Sink &sink, Memory &M, hipStream_t
                 int ds;
                 if (!free_dev.get(ds)) break;
                 ch.dslot = ds;
-                if (hipMemcpyAsync(d_inb[ds], hin[ch.slot], ch.bytes, hipMemcpyHostToDevice, s_copy) != hipSuccess ||
+                if (ch.bytes + 64 > d_inb_cap[ds]) {   // first use, or a grown chunk
+                    d_inb[ds] = static_cast<uint8_t *>(M.dev(Memory::D_IN0 + ds, ch.bytes + 64));
+                    d_inb_cap[ds] = d_inb[ds] ? ch.bytes + 64 : 0;
+                }
+                ch.dev = d_inb[ds];
+                if (!ch.dev || hipMemcpyAsync(d_inb[ds], ch.host, ch.bytes, hipMemcpyHostToDevice, s_copy) != hipSuccess ||
                     hipEventRecord(ev_up[ds], s_copy) != hipSuccess)
                     ch.ok = false;
             }
@@ -236,7 +282,7 @@ inline int compress_stream(Source &src, const Sink &sink, Memory &M, hipStream_t
     std::thread writer([&] {
         OutChunk oc;
         while (to_write.get(oc)) {
-            const uint8_t *r = hout[oc.slot];
+            const uint8_t *r = oc.data;
             const double w0 = now_s();
             if (!write_failed) {
                 if (oc.pass.empty()) {
@@ -291,10 +337,13 @@ inline int compress_stream(Source &src, const Sink &sink, Memory &M, hipStream_t
             double &t, g;
             ~Acc() { t += now_s() - g; }
         } acc{t_gpu, g0};
-        if (!ch.ok) return finish(ch.long_line ? ST_E_ARG : ch.dslot >= 0 ? ST_E_HIP : ST_E_IO);
+        if (!ch.ok) return finish(ch.long_line ? ST_E_ARG : (ch.alloc_failed || ch.dslot >= 0) ? ST_E_HIP : ST_E_IO);
         const uint64_t n = ch.bytes;
-        const uint8_t *h = hin[ch.slot];
-        uint8_t *d_in = d_inb[ch.dslot];
+        const uint8_t *h = ch.host;
+        const uint8_t *d_in = ch.dev;
+        const VcfcLineIndexLayout L1 = vcfc_line_index_layout(n, 0);
+        uint8_t *d_ix1 = static_cast<uint8_t *>(M.dev(Memory::D_IX1, L1.total1));
+        if (!d_ix1) return finish(ST_E_HIP);
         VcfcLineIndex x;
         x.counts = d_small;
         // phase 1: '\n' positions
@@ -304,7 +353,7 @@ inline int compress_stream(Source &src, const Sink &sink, Memory &M, hipStream_t
             return finish(ST_E_HIP);
         const uint64_t n_lines = hsmall[0];
         // phase 2: data and '#' lines
-        const VcfcLineIndexLayout L = vcfc_line_index_layout(CX, n_lines);
+        const VcfcLineIndexLayout L = vcfc_line_index_layout(n, n_lines);
         const uint64_t max_data = n_lines;
         uint8_t *d_ix2 = static_cast<uint8_t *>(M.dev(Memory::D_IX2, L.total2));
         uint8_t *d_lines = static_cast<uint8_t *>(M.dev(Memory::D_LINES, 32 * (max_data + 1)));
@@ -409,6 +458,12 @@ inline int compress_stream(Source &src, const Sink &sink, Memory &M, hipStream_t
             while (!pass.empty() && pass.back().before > good) pass.pop_back();   // '#' lines after the failing row
         }
         oc.rec_bytes = oc.rec_off[good];
+        if (oc.rec_bytes + 64 > hout_cap[oslot]) {   // pinned output sized by the records actually made
+            hout[oslot] = static_cast<uint8_t *>(M.host(Memory::H_OUT0 + oslot, oc.rec_bytes + 64));
+            hout_cap[oslot] = hout[oslot] ? oc.rec_bytes + 64 : 0;
+            if (!hout[oslot]) return finish(ST_E_HIP);
+        }
+        oc.data = hout[oslot];
         if (oc.rec_bytes &&
             (hipMemcpyAsync(hout[oslot], d_out, oc.rec_bytes, hipMemcpyDeviceToHost, s) != hipSuccess || !sync()))
             return finish(ST_E_HIP);
@@ -421,6 +476,7 @@ inline int compress_stream(Source &src, const Sink &sink, Memory &M, hipStream_t
             return finish(st);
         }
         line_base += n_lines;
+        if (lines_out) *lines_out = line_base;
     }
     return finish(ST_OK);
 }

@@ -5,9 +5,11 @@ per-shard output sizes to stitch the output.
 compress() (reference src/compress.cpp:205-257) is stateless per line -- the
 schema it tracks is never read by the encoder -- so any split at a line
 boundary can be compressed independently and the outputs concatenated in
-order.  Each rank encodes its slice on its own GPU (vcfc.Context.compress_buffer),
-all-gathers the byte counts (RCCL on GPU ranks, gloo in the CPU tests), and
-pwrites its bytes at the exclusive prefix.
+order.  Each rank streams its slice through the ingest pipeline on its own GPU
+(vcfc.Context.compress_range: reader threads, pinned H2D, GPU line index +
+encode), all-gathers (bytes, status, failing line, lines) -- RCCL on GPU
+ranks, gloo in the CPU tests -- and places its output at the exclusive
+prefix of the byte counts.
 
 Run: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \\
          vcf-compression_amd/dist_compress.py [sparsify] in out
@@ -17,6 +19,9 @@ halo record each side, one all-gather of the plans' verdicts).
 """
 import os
 import sys
+import tempfile
+
+E_IO = 7   # include/vcfc.h VCFC_E_IO
 
 
 def split_points(data_len, world, read_at):
@@ -45,45 +50,94 @@ def exclusive_offsets(counts):
     return offs, acc
 
 
-def compress_shard(in_path, out_path, rank, world, encode, allgather):
-    """encode(bytes) -> (status, out_bytes, err_line_in_slice), where on a
-    failing line out_bytes holds the output of the slice's lines before it;
-    allgather(list_of_ints_local) -> list of per-rank lists.
-    Returns (status, total_bytes, global_err_line).  The output file equals
-    the single-process output: on a failure, everything before the first
-    failing line in file order (the reference stops there)."""
+def copy_to(src_fd, dst_fd, n, dst_off):
+    """Copy bytes [0, n) of src_fd to dst_fd at dst_off: copy_file_range (in
+    the kernel; a reflink where the filesystem has them), else a pread/pwrite
+    loop.  Both loop until every byte is placed (one call moves < 2 GiB)."""
+    done = 0
+    try:
+        while done < n:
+            k = os.copy_file_range(src_fd, dst_fd, n - done, done, dst_off + done)
+            if k <= 0:
+                raise OSError("copy_file_range made no progress")
+            done += k
+        return
+    except (OSError, AttributeError):
+        pass
+    while done < n:
+        b = os.pread(src_fd, min(n - done, 64 << 20), done)
+        if not b:
+            raise OSError("short read of a shard's spill file")
+        mv = memoryview(b)
+        while len(mv):
+            w = os.pwrite(dst_fd, mv, dst_off + done)
+            if w <= 0:
+                raise OSError("pwrite made no progress")
+            mv = mv[w:]
+            done += w
+
+
+def compress_shard(in_path, out_path, rank, world, compress_range, allgather):
+    """One rank of a sharded compress.
+
+    compress_range(in_path, off, length, fd, out_off) -> (status, bytes
+    written, 1-based failing line in the range or -1, lines in the range)
+    streams the rank's line-aligned byte range through the ingest pipeline
+    (vcfc.Context.compress_range) and writes its output to fd from out_off on;
+    allgather(list_of_ints) -> per-rank lists.  Rank 0's output starts the
+    file, so it writes in place; every other rank spills to a temporary file
+    beside the output and, once one all-gather has given it its offset (the
+    exclusive prefix of the byte counts), copies the spill there.  No rank
+    reads outside its own range, and no slice is held in memory.
+
+    Returns (status, total bytes, global failing line or -1) -- the same on
+    every rank.  The output file equals the single-process output: on a
+    failure, everything before the first failing line in file order (the
+    reference stops there, src/compress.cpp:205-257).  Errors that are not
+    about the VCF (HIP, I/O) travel through the same all-gather, so no rank
+    is left waiting in the collective."""
     size = os.path.getsize(in_path)
     with open(in_path, "rb") as f:
         def read_at(off, n):
             f.seek(off)
             return f.read(n)
         pts = split_points(size, world, read_at)
-        f.seek(pts[rank])
-        mine = f.read(pts[rank + 1] - pts[rank])
-        # lines before my slice (for global line numbers of errors)
-        f.seek(0)
-        lines_before = 0
-        left = pts[rank]
-        while left > 0:
-            b = f.read(min(left, 1 << 24))
-            lines_before += b.count(b"\n")
-            left -= len(b)
-    st, out, err_line = encode(mine)
-    g = allgather([len(out), st, (lines_before + err_line) if st else -1])
-    # the first failing rank (shards are in file order) holds the first
-    # failing line: it writes its partial output, later ranks write nothing
-    first_bad = next((r for r, x in enumerate(g) if x[1] != 0), world)
-    counts = [x[0] if r <= first_bad else 0 for r, x in enumerate(g)]
-    offs, total = exclusive_offsets(counts)
-    status, gline = (g[first_bad][1], g[first_bad][2]) if first_bad < world else (0, -1)
+    lo, hi = pts[rank], pts[rank + 1]
     fd = os.open(out_path, os.O_WRONLY | os.O_CREAT, 0o644)
+    pfd, part = -1, None
     try:
-        if out and rank <= first_bad:
-            os.pwrite(fd, out, offs[rank])
+        try:
+            if rank == 0:
+                st, nb, eline, lines = compress_range(in_path, lo, hi - lo, fd, 0)
+            else:
+                pfd, part = tempfile.mkstemp(prefix=".vcfc-part%d-" % rank,
+                                             dir=os.path.dirname(os.path.abspath(out_path)))
+                st, nb, eline, lines = compress_range(in_path, lo, hi - lo, pfd, 0)
+        except Exception as e:   # still take part in the collective
+            print("vcfc rank %d: %s" % (rank, e), file=sys.stderr)
+            st, nb, eline, lines = E_IO, 0, -1, 0
+        g = allgather([int(nb), int(st), int(eline), int(lines)])
+        # the first failing rank (shards are in file order) holds the first
+        # failing line: it places its partial output, later ranks nothing
+        first_bad = next((r for r, x in enumerate(g) if x[1] != 0), world)
+        counts = [x[0] if r <= first_bad else 0 for r, x in enumerate(g)]
+        offs, total = exclusive_offsets(counts)
+        if first_bad < world:
+            status = g[first_bad][1]
+            eb = g[first_bad][2]
+            gline = sum(x[3] for x in g[:first_bad]) + eb if eb >= 0 else -1
+        else:
+            status, gline = 0, -1
+        if rank > 0 and rank <= first_bad and counts[rank]:
+            copy_to(pfd, fd, counts[rank], offs[rank])
         if rank == world - 1:
             os.ftruncate(fd, total)
     finally:
         os.close(fd)
+        if pfd >= 0:
+            os.close(pfd)
+        if part:
+            os.unlink(part)
     return status, total, gline
 
 
@@ -135,13 +189,16 @@ def main():
         open(out_path, "wb").close()
     if world > 1:
         dist.barrier()
-    ctx = vcfc.Context(local)
+    try:
+        ctx = vcfc.Context(local)
+    except RuntimeError as e:   # reported through the all-gather below
+        print("vcfc rank %d: %s" % (rank, e), file=sys.stderr)
+        ctx = None
 
-    def encode(buf):
-        st, out, line = ctx.compress_status(buf)
-        if st not in (vcfc.OK, vcfc.E_LT8COLS, vcfc.E_8COLS, vcfc.E_HEADER):
-            vcfc.raise_for(st)
-        return st, out, line
+    def compress_range(path, off, length, fd, out_off):
+        if ctx is None:
+            return vcfc.E_HIP, 0, -1, 0
+        return ctx.compress_range(path, off, length, fd, out_off)
 
     def allgather(vals):
         if world == 1:
@@ -152,12 +209,14 @@ def main():
         return out.view(world, len(vals)).cpu().tolist()
 
     if mode == "sparsify":
+        if ctx is None:
+            vcfc.raise_for(vcfc.E_HIP)
         st = sparsify_shards(rank, world,
                              lambda write: ctx.sparsify_shard(in_path, out_path if write else None, rank, world),
                              lambda: ctx.sparsify_status(in_path, out_path), allgather)
         line = -1
     else:
-        st, total, line = compress_shard(in_path, out_path, rank, world, encode, allgather)
+        st, total, line = compress_shard(in_path, out_path, rank, world, compress_range, allgather)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -35,7 +35,8 @@ EXPORTS = [
     "vcfc_decompress_buffer", "vcfc_decompress_file", "vcfc_decode_workspace_size",
     "vcfc_decode_records_device", "vcfc_parse_query", "vcfc_query_buffer", "vcfc_query_file",
     "vcfc_query_match_device", "vcfc_decode_selected_device", "vcfc_sparse_query_file",
-    "vcfc_sparsify_shard",
+    "vcfc_sparsify_shard", "vcfc_ctx_set_ingest_chunk", "vcfc_record_hash_device",
+    "vcfc_compress_range",
 ]
 
 
@@ -64,6 +65,10 @@ def lib():
     L.vcfc_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
     L.vcfc_ctx_destroy.argtypes = [vp]
     L.vcfc_ctx_destroy.restype = None
+    L.vcfc_ctx_set_ingest_chunk.argtypes = [vp, u64]
+    L.vcfc_record_hash_device.argtypes = [vp, vp, u64, vp, vp]
+    L.vcfc_compress_range.argtypes = [vp, ctypes.c_char_p, u64, u64, ctypes.c_int, u64, ctypes.POINTER(u64),
+                                      ctypes.POINTER(i64), ctypes.POINTER(u64)]
     L.vcfc_compress_data_line.argtypes = [vp, ctypes.c_char_p, u64, ctypes.c_int, vp, u64, ctypes.POINTER(u64)]
     L.vcfc_encode_bound.restype = u64
     L.vcfc_encode_bound.argtypes = [u64, u64]
@@ -162,6 +167,11 @@ class Context:
         except Exception:
             pass
 
+    def set_ingest_chunk(self, chunk_bytes):
+        """Input chunk of compress_file / compress_buffer (0 = default 128 MiB);
+        the output does not depend on it."""
+        raise_for(lib().vcfc_ctx_set_ingest_chunk(self._h, int(chunk_bytes)))
+
     def __enter__(self):
         return self
 
@@ -207,6 +217,16 @@ class Context:
         line = ctypes.c_int64(-1)
         st = lib().vcfc_compress_file(self._h, in_path.encode(), out_path.encode(), ctypes.byref(line))
         raise_for(st, "line %d" % line.value)
+
+    def compress_range(self, in_path, off, length, out_fd, out_off=0):
+        """One shard of a sharded compress: bytes [off, off + length) of
+        in_path (whole lines) -> out_fd at out_off.  Returns (status,
+        bytes written, 1-based failing line in the range or -1, lines in the
+        range); does not raise (ranks exchange statuses first)."""
+        nb, line, lines = ctypes.c_uint64(0), ctypes.c_int64(-1), ctypes.c_uint64(0)
+        st = lib().vcfc_compress_range(self._h, in_path.encode(), off, length, out_fd, out_off, ctypes.byref(nb),
+                                       ctypes.byref(line), ctypes.byref(lines))
+        return st, nb.value, line.value, lines.value
 
     def decompress_buffer(self, data, cap=None):
         """.vcfc bytes -> VCF bytes, as decompress2_fd (reference
@@ -393,3 +413,8 @@ def synth_rows_device(d_buf, d_line_off, n, d_prefix, d_prefix_off, d_row_af, sa
     st = lib().vcfc_synth_rows_device(d_buf, d_line_off, n, d_prefix, d_prefix_off, d_row_af, samples,
                                       law, seed, stream)
     raise_for(st)
+
+
+def record_hash_device(d_recs, d_rec_off, n, d_hash, stream=0):
+    """Per-record 64-bit digests on the GPU (include/vcfc.h vcfc_record_hash_device)."""
+    raise_for(lib().vcfc_record_hash_device(d_recs, d_rec_off, n, d_hash, stream))
