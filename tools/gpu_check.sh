@@ -34,10 +34,14 @@ for s in $STEPS; do
            n=$(echo $P | cut -d' ' -f1)
            (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --pmc $P --kernel-trace --output-format csv -d "$O/pmcdec_$n" -o run -- python3 "$R/bench.py" --mode decode --steps 3 --warmup 1 --no-cpu-baseline > "$O/pmcdec_$n.log" 2>&1) || { echo "pmcdec $n failed rc=$?"; tail -30 "$O/pmcdec_$n.log"; exit 1; }
          done ;;
-    prof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof" -o run -- python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu-baseline > "$O/prof.log" 2>&1) || { echo "prof failed rc=$?"; tail -30 "$O/prof.log"; exit 1; } ;;
+    prof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof" -o run -- python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu-baseline ${BENCH_ARGS} > "$O/prof.log" 2>&1) || { echo "prof failed rc=$?"; tail -30 "$O/prof.log"; exit 1; } ;;
     pmc) for P in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" "FETCH_SIZE" "WRITE_SIZE" "GRBM_GUI_ACTIVE SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR"; do
            n=$(echo $P | cut -d' ' -f1)
-           (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --pmc $P --kernel-trace --output-format csv -d "$O/pmc_$n" -o run -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$O/pmc_$n.log" 2>&1) || { echo "pmc $n failed rc=$?"; tail -30 "$O/pmc_$n.log"; exit 1; }
+           (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --pmc $P --kernel-trace --output-format csv -d "$O/pmc_$n" -o run -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS} > "$O/pmc_$n.log" 2>&1) || { echo "pmc $n failed rc=$?"; tail -30 "$O/pmc_$n.log"; exit 1; }
+         done ;;
+    pmcx) for P in "SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_VMEM_WR SQ_INSTS_VALU"; do
+           n=$(echo $P | cut -d' ' -f1)
+           (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --pmc $P --kernel-trace --output-format csv -d "$O/pmcx_$n" -o run -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS} > "$O/pmcx_$n.log" 2>&1) || { echo "pmcx $n failed rc=$?"; tail -30 "$O/pmcx_$n.log"; exit 1; }
          done ;;
     ptest) timeout -k 10 1000 python -u -m pytest ${PT_ARGS} -x -v -p no:cacheprovider --timeout 400 --timeout-method thread > "$O/pytest_sel.log" 2>&1 || { echo "ptest failed rc=$?"; tail -60 "$O/pytest_sel.log"; exit 1; } ; tail -5 "$O/pytest_sel.log" ;;
     *) echo "unknown step $s"; exit 2 ;;

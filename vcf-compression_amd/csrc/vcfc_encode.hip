@@ -36,7 +36,11 @@ namespace {
 constexpr int K1_WAVES = 4;            // rows per 256-thread block
 constexpr uint32_t RING = 4096;        // per-wave LDS ring (bytes)
 constexpr uint32_t RMASK = RING - 1;
-constexpr uint32_t RING_STRIDE = RING + 64;   // + one dummy byte per lane (branch-free stores)
+// + a 64-byte tail (a lane's bytes written past the ring end, moved to its
+// start afterwards) + one dummy word per lane (branch-free stores)
+constexpr uint32_t RING_TAIL = 64;
+constexpr uint32_t RING_DUMMY = RING + RING_TAIL;
+constexpr uint32_t RING_STRIDE = RING_DUMMY + 4 * 64;
 constexpr uint32_t BURST = 1024;       // flush granule (64 lanes x 16 B)
 constexpr uint32_t CLS_ESC = 4, CLS_NONE = 5;
 
@@ -309,7 +313,7 @@ __device__ bool gt_general(const Chunk &cur, int32_t tf, FastState &f, Ring &r) 
     for (int j = 0; j < (int)TPL; j++) d[j] = vw::alignbyte(cur.w(j + 1), cur.w(j), phi);
     const int32_t t0 = tf + (int32_t)(TPL * l);
     const uint32_t u0 = (uint32_t)(t0 + 1);
-    const uint32_t dummy = RING + l;
+    const uint32_t dummy = RING_DUMMY + 4 * l;
     bool v[TPL];
 #pragma unroll
     for (int j = 0; j < (int)TPL; j++) v[j] = (uint32_t)(t0 + j) < T;
@@ -608,29 +612,38 @@ __device__ __forceinline__ void esc8(const uint32_t (&d)[TPL8], int32_t t0, int3
     const uint32_t n2 = (uint32_t)__builtin_popcount(sb & (sb - 1u));
     const uint32_t cnt = (full ? 1u : 0u) + (lead1 ? 1u : 0u) + n2 + 4u * (uint32_t)__builtin_popcount(eb);
     const uint32_t incl2 = vw::scan_add(cnt);
-    uint32_t pos = r.wpos + incl2 - cnt;
-    if (full) ring_put(r, pos, m0 | cap);
-    pos += full ? 1u : 0u;
-    bool seen = false;
+    // The lane's bytes go to base + [0, cnt) (cnt <= 41 < RING_TAIL: no
+    // masking per byte; bytes past the ring end are moved below).  Stores are
+    // unconditional: a byte or escape word the lane does not emit goes to its
+    // dummy word, so the slots need no branches; an escape's four bytes
+    // (0xE1 and its token) leave as one unaligned ds_write_b32.
+    const uint32_t base = (r.wpos + incl2 - cnt) & RMASK;
+    uint8_t *const lb = r.lds + base;
+    uint8_t *const dm = r.lds + RING_DUMMY + 4u * vw::lane_id();
+    *(full ? lb : dm) = (uint8_t)(m0 | cap);
+    uint32_t o = full ? 1u : 0u;
     uint32_t jp = 0;
 #pragma unroll
     for (int j = 0; j < (int)TPL8; j++) {
         const bool s = (sb >> (4 * j)) & 1u;
         const bool e = (eb >> (4 * j)) & 1u;
         const uint32_t pc = (cp4 >> (4 * j)) & 7u;
-        const bool lead = s && (seen || lead1);
-        const uint32_t b = !seen ? b1
+        const bool first = (uint32_t)j == j1;
+        const bool lead = s && (!first || lead1);
+        const uint32_t b = first ? b1
                          : (pc == CLS_ESC ? 0x09u : (vw::perm(0x80C0A000u, 0x80C0A000u, pc) | ((uint32_t)j - jp)));
-        if (lead) ring_put(r, pos, b);
-        pos += lead ? 1u : 0u;
-        if (e) {
-            ring_put(r, pos, 0xE1u);
-            ring_put(r, pos + 1u, d[j] & 0xFFu);
-            ring_put(r, pos + 2u, (d[j] >> 8) & 0xFFu);
-            ring_put(r, pos + 3u, (d[j] >> 16) & 0xFFu);
-            pos += 4u;
+        *(lead ? lb + o : dm) = (uint8_t)b;
+        o += lead ? 1u : 0u;
+        const uint32_t pay = (d[j] << 8) | 0xE1u;   // 0xE1, then the token's three bytes
+        __builtin_memcpy(e ? lb + o : dm, &pay, 4);
+        o += e ? 4u : 0u;
+        if (s) jp = (uint32_t)j;
+    }
+    const bool wrap = base + cnt > RING;
+    if (vw::ballot(wrap)) {
+        if (wrap) {
+            for (uint32_t q = RING; q < base + cnt; q++) r.lds[q - RING] = r.lds[q];
         }
-        if (s) { seen = true; jp = (uint32_t)j; }
     }
     r.wpos += vw::readlane(incl2, 63);
     f.pcls = (vw::readlane(cbH, 63) >> 24) & 7u;
@@ -642,6 +655,20 @@ __device__ __forceinline__ void esc8(const uint32_t (&d)[TPL8], int32_t t0, int3
 // TAB needed; slots past it ignored)
 template <bool EDGE>
 __device__ __forceinline__ bool shape3(const uint32_t (&d)[TPL8], int32_t t0, uint32_t T) {
+    if (!EDGE) {
+        // t = d ^ TABs: byte 3 must be 0 (a TAB) in every slot -- OR them all;
+        // bytes 0..2 must not be (haszero on t with byte 3 forced to 0xFF,
+        // exact for "some byte is zero", OR-accumulated over the slots)
+        uint32_t at = 0, az = 0;
+#pragma unroll
+        for (int j = 0; j < (int)TPL8; j++) {
+            const uint32_t t = d[j] ^ 0x09090909u;
+            const uint32_t u = t | 0xFF000000u;
+            at |= t;
+            az |= (u - 0x01010101u) & ~u;
+        }
+        return (at >> 24) != 0 || (az & 0x80808080u) != 0;
+    }
     bool bad = false;
 #pragma unroll
     for (int j = 0; j < (int)TPL8; j++) {
@@ -755,7 +782,27 @@ __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring
     const uint32_t ncG = (T + SLOTS8 - 1) / SLOTS8;
     const uint32_t lo32 = BPL8 * l;
     uint32_t C0 = 0;
+#ifndef VCFC_GT_DEPTH
+#define VCFC_GT_DEPTH 3   // genotype chunks in flight per wave
+#endif
     for (;;) {
+#if VCFC_GT_DEPTH == 2
+        Chunk8 b0 = load_chunk8(rsG, C0, lo32);
+        Chunk8 b1 = load_chunk8(rsG, C0 + 1, lo32);
+        vw::pin_loads();
+        uint32_t C = C0, gen = C0;
+        bool ok = true;
+        for (;;) {
+            if (ok) { ok = vw::readfirst(gt_step8(b0, C, f, r)); gen = C; }
+            b0 = load_chunk8(rsG, C + 2, lo32);
+            vw::pin_loads();
+            if (ok && C + 1 < ncG) { ok = vw::readfirst(gt_step8(b1, C + 1, f, r)); gen = C + 1; }
+            b1 = load_chunk8(rsG, C + 3, lo32);
+            vw::pin_loads();
+            C = vw::readfirst(C + 2);
+            if (!ok || C >= ncG) break;
+        }
+#else
         Chunk8 b0 = load_chunk8(rsG, C0, lo32);
         Chunk8 b1 = load_chunk8(rsG, C0 + 1, lo32);
         Chunk8 b2 = load_chunk8(rsG, C0 + 2, lo32);
@@ -775,6 +822,7 @@ __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring
             C = vw::readfirst(C + 3);
             if (!ok || C >= ncG) break;
         }
+#endif
         if (ok) break;
         // chunk `gen`: the general step over its two 1 KiB halves
         for (uint32_t h = 0; h < 2; h++) {
@@ -928,7 +976,17 @@ __device__ __forceinline__ bool row_setup(const VcfcEncodeArgs &a, uint64_t row,
 
 // Fast kernel: one wave per row; rows without the GT-only shape are queued
 // for k_encode_general.
+// Pinned to 6 waves/SIMD (the SGPR count allows no more): without the pin the
+// branch-free escape emission takes 84 VGPRs and 5 waves, +5 % on the
+// headline rows (profiles/r02/ab/ab_esc8_emit.txt).  A/B builds override it.
+#ifndef VCFC_FAST_WPE
+#define VCFC_FAST_WPE 6
+#endif
+#if VCFC_FAST_WPE
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VCFC_FAST_WPE, VCFC_FAST_WPE))) void k_encode_fast(VcfcEncodeArgs a) {
+#else
 __global__ __launch_bounds__(256) void k_encode_fast(VcfcEncodeArgs a) {
+#endif
     __shared__ __attribute__((aligned(16))) uint8_t lds[K1_WAVES * RING_STRIDE];
     const uint32_t wave = vw::readfirst(threadIdx.x >> 6);   // wave-uniform: scalar row/len/loop control
     const uint64_t row = (uint64_t)blockIdx.x * K1_WAVES + wave;
