@@ -8,8 +8,9 @@ step   : one pass of the hot path (reference compress_data_line,
          slot scan -> k_encode -> size scan -> k_compact, plus -- for N > 1
          -- one RCCL all-gather of the per-shard record byte counts (the
          stitch offsets of the output file).
-scaling: weak.  Every rank encodes its own 1M-row shard (rows are
+scaling: weak (default).  Every rank encodes its own 1M-row shard (rows are
          independent; the shards are contiguous row ranges of one file).
+         --scaling strong: the 1M rows are split over the ranks (1M/N each).
 value  : GT bytes of all ranks / (max over ranks of the timed wall time).
 
 Also printed: `roofline` for the dominant kernel k_encode (algorithmic bytes
@@ -41,7 +42,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--rows", type=int, default=None, help="rows per GPU (default 1M; 100k in --mode biobank)")
     ap.add_argument("--samples", type=int, default=None, help="samples (default 2504; 100k in --mode biobank)")
-    ap.add_argument("--law", type=int, default=1, help="1 = chr22-shaped (headline), 0 = random_vcf law")
+    ap.add_argument("--law", type=int, default=1, choices=[0, 1, 2],
+                    help="1 = chr22-shaped (headline), 0 = random_vcf law, 2 = general shapes (SURVEY D3)")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
+                    help="weak: every rank encodes --rows rows; strong: the --rows rows are split over the ranks")
     ap.add_argument("--cpu-rows", type=int, default=None,
                     help="rows in the CPU-baseline sample (default: about 1.2 GB of lines)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -63,6 +67,10 @@ def parse():
     if a.cpu_rows is None:
         a.cpu_rows = max(1, int(1.2e9 // (4 * a.samples + 180)))   # ~120k rows at 2504 samples
     return a
+
+
+def law_name(law):
+    return {0: "random_vcf-law", 1: "chr22-shaped", 2: "general-shapes (chrX haploid/GT:DP:GQ/missing)"}[law]
 
 
 def cpu_baseline(rows, torch, args):
@@ -267,8 +275,7 @@ def bench_decode(args, torch, vcfc, workload):
            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
            "higher_is_better": True, "scaling": "replicas", "vs_baseline": None, "dtype": "u8",
            "data": "synthetic (generated and encoded in HBM)",
-           "config": {"workload": "%s %d samples x %d variants" % ("chr22-shaped" if args.law == 1 else
-                                                                   "random_vcf-law", S, n),
+           "config": {"workload": "%s %d samples x %d variants" % (law_name(args.law), S, n),
                       "record_bytes": rec_bytes, "line_bytes": total},
            "roofline": {"kernel": "k_dec_plan + k_dec_write", "bound": "hbm",
                         "achieved": round(alg / (ev_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -337,7 +344,7 @@ def bench_query(args, torch, vcfc, workload):
            "higher_is_better": True, "scaling": "replicas", "vs_baseline": None, "dtype": "u8",
            "data": "synthetic (generated and encoded in HBM)",
            "config": {"workload": "%s %d samples x %d variants, query %s (%d rows, %.1f%%)"
-                                  % ("chr22-shaped" if args.law == 1 else "random_vcf-law", S, n, q, b - a + 1,
+                                  % (law_name(args.law), S, n, q, b - a + 1,
                                      100.0 * (b - a + 1) / n),
                       "record_bytes": rec_bytes, "selected_record_bytes": sel_rec, "line_bytes": total},
            "roofline": {"kernel": "k_query_match + k_dec_plan + k_dec_write", "bound": "hbm",
@@ -411,7 +418,7 @@ def bench_ingest(args, torch, vcfc, workload):
                "higher_is_better": True, "scaling": "replicas", "vs_baseline": None, "dtype": "u8",
                "data": "synthetic (generated in HBM, written to a file in the page cache)",
                "config": {"workload": "%s %d samples x %d variants, %.2f GB file"
-                                      % ("chr22-shaped" if args.law == 1 else "random_vcf-law", S, n, in_bytes / 1e9),
+                                      % (law_name(args.law), S, n, in_bytes / 1e9),
                           "input_bytes": in_bytes, "output_bytes": len(want)},
                "roofline": {"kernel": "pipeline (file read + H2D + index + encode + D2H + write)", "bound": "pcie",
                             "achieved": round(in_bytes * args.steps / elapsed / 1e9, 2), "peak": round(h2d, 1),
@@ -559,8 +566,15 @@ def main():
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=dev)
-    n, S = args.rows, args.samples
-    rows = workload.DeviceRows(torch, vcfc, n, S, args.law, seed=1000 + rank, device=dev, row0=rank * n)
+    S = args.samples
+    if args.scaling == "strong":
+        # the --rows rows split over the ranks (each rank generates its own
+        # contiguous slice, same law; the total work is fixed)
+        r0, r1 = args.rows * rank // world, args.rows * (rank + 1) // world
+    else:
+        r0, r1 = rank * args.rows, (rank + 1) * args.rows
+    n = r1 - r0
+    rows = workload.DeviceRows(torch, vcfc, n, S, args.law, seed=1000 + rank, device=dev, row0=r0)
     ws_bytes = vcfc.workspace_size(n, rows.line_bytes)
     cap = vcfc.encode_bound(n, rows.line_bytes)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
@@ -605,11 +619,14 @@ def main():
     copy_gbs = measured_copy_gbs(torch, dev)
     out_bytes = int(rec[n].item())
     ms_step = elapsed * 1e3 / args.steps
-    gt_total = rows.gt_bytes * world
+    gt = torch.tensor([rows.gt_bytes], dtype=torch.int64, device=cdev)
+    if world > 1:
+        dist.all_reduce(gt)   # GT bytes of all ranks (strong: the whole dataset once)
+    gt_total = int(gt.item())
     value = gt_total * args.steps / elapsed / 1e9
     k_ms = stages["k_encode"] / max(calls, 1)
     alg = rows.line_bytes + out_bytes
-    wl = "chr22-shaped" if args.law == 1 else "random_vcf-law"
+    wl = law_name(args.law)
     wkey = "%s/%dx%d" % (wl, S, n)
     if args.mode == "biobank":
         metric = "input GT bytes/sec encoded, 100k-sample x 5M-variant VCF, row-sharded"
@@ -617,7 +634,10 @@ def main():
                  "5M/N-row shard; batches are independent and run back to back)" % (wl, S, n))
     else:
         metric = "input GT bytes/sec encoded, 2504-sample x 1M-variant VCF"
-        wdesc = "%s %d samples x %d variants per GPU (BASELINE configs[1])" % (wl, S, n)
+        if args.scaling == "strong":
+            wdesc = "%s %d samples x %d variants split over %d GPU(s) (BASELINE configs[1])" % (wl, S, args.rows, world)
+        else:
+            wdesc = "%s %d samples x %d variants per GPU (BASELINE configs[1])" % (wl, S, n)
     roof = {"kernel": "k_encode", "bound": "hbm", "achieved": round(alg / (k_ms * 1e-3) / 1e9, 1),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(alg / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "traffic": load_pmc(wkey),
@@ -627,7 +647,7 @@ def main():
     res = {"metric": metric,
            "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
-           "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic (generated in HBM)",
+           "scaling": args.scaling, "vs_baseline": None, "dtype": "u8", "data": "synthetic (generated in HBM)",
            "config": {"workload": wdesc,
                       "samples": S, "rows_per_gpu": n, "gt_bytes_per_gpu": rows.gt_bytes,
                       "line_bytes_per_gpu": rows.line_bytes, "record_bytes_per_gpu": out_bytes,

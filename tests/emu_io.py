@@ -34,6 +34,7 @@ def lib():
         L.emu_compress.argtypes = [ctypes.c_char_p, u64, vp, u64, ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_int64),
                                    u64, ctypes.c_int, u64]
         L.emu_record_hash.argtypes = [vp, vp, u64, vp]
+        L.emu_synth.argtypes = [vp, vp, u64, vp, vp, vp, ctypes.c_uint32, ctypes.c_int, u64]
         _lib = L
     return _lib
 
@@ -141,3 +142,21 @@ def emu_compress(vcf, chunk=4096, read_threads=2, cap=None, max_chunk=0):
     st = lib().emu_compress(vcf, len(vcf), out.ctypes.data, cap, ctypes.byref(n), ctypes.byref(el), chunk,
                             read_threads, max_chunk)
     return st, out[:n.value].tobytes(), el.value
+
+
+def emu_synth_rows(n, samples, law, seed, row0=0):
+    """vcf-compression_amd/workload.py's synthetic rows generated by the
+    product generator kernel on the emulator: (buf, line_off, line_len)."""
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "vcf-compression_amd"))
+    import workload
+    blob, poff, af, _, gt_len = workload.prefixes(n, law, seed, row0, samples)
+    line_off, line_len, total = workload.layout(poff, samples, gt_len)
+    buf = np.zeros(total + 64, dtype=np.uint8)
+    pre = np.frombuffer(blob, dtype=np.uint8).copy()
+    lo = np.ascontiguousarray(line_off, dtype=np.uint64)
+    po = np.ascontiguousarray(poff, dtype=np.uint64)
+    afp = af.ctypes.data if af is not None else None
+    assert lib().emu_synth(buf.ctypes.data, lo.ctypes.data, n, pre.ctypes.data, po.ctypes.data, afp, samples, law,
+                           seed) == 0
+    return buf[:total], lo, np.ascontiguousarray(line_len, dtype=np.uint32)

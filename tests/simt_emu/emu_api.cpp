@@ -164,3 +164,12 @@ extern "C" int emu_compress(const uint8_t *in, uint64_t n, uint8_t *out, uint64_
 extern "C" int emu_record_hash(const uint8_t *recs, const uint64_t *rec_off, uint64_t n, uint64_t *out) {
     return (int)vcfc_record_hash(recs, rec_off, n, out, nullptr);
 }
+
+// Synthetic rows (csrc/vcfc_synth.hip) on the emulator.
+hipError_t vcfc_synth_device(uint8_t *buf, const uint64_t *line_off, uint64_t n, const uint8_t *prefix,
+                             const uint64_t *prefix_off, const float *row_af, uint32_t S, int law,
+                             uint64_t seed, hipStream_t s);
+extern "C" int emu_synth(uint8_t *buf, const uint64_t *line_off, uint64_t n, const uint8_t *prefix,
+                         const uint64_t *prefix_off, const float *row_af, uint32_t S, int law, uint64_t seed) {
+    return (int)vcfc_synth_device(buf, line_off, n, prefix, prefix_off, row_af, S, law, seed, nullptr);
+}

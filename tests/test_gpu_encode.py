@@ -115,6 +115,7 @@ def _device_encode(torch, vcfc, rows):
 
 
 @pytest.mark.parametrize("law,samples,n", [(0, 2504, 3000), (1, 2504, 3000), (0, 100, 20000), (1, 5003, 700),
+                                           (2, 2504, 3000), (2, 100, 20000), (2, 7, 5000),
                                            (1, 100_000, 48), (0, 100_000, 24)])   # last two: configs[3] rows
 def test_synthetic_rows_all_vs_oracle(torch, vcfc, law, samples, n):
     import workload

@@ -1,7 +1,8 @@
 """Full-size GPU parity (BASELINE configs[1]/[2] and [4]: 2504 samples x 1M
 variants): EVERY record of the batch against the oracle, for both synthetic
 laws (law 0 = the reference generator's random_vcf law,
-other/random_vcf.py:66-70; law 1 = chr22-shaped), plus the decode round trip
+other/random_vcf.py:66-70; law 1 = chr22-shaped; law 2 = general shapes,
+SURVEY §8(d) D3: haploid, GT:DP:GQ, missing), plus the decode round trip
 of the same batch (reference compress_data_line src/compress.cpp:5-203 and
 decompress2_data_line :741-986).
 
@@ -39,7 +40,7 @@ def threads():
     return int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
 
 
-@pytest.mark.parametrize("law", [1, 0])
+@pytest.mark.parametrize("law", [1, 0, 2])
 def test_full_batch_every_record_and_round_trip(torch, vcfc, law):
     import workload
     from test_gpu_encode import _device_encode
@@ -70,10 +71,14 @@ def test_full_batch_every_record_and_round_trip(torch, vcfc, law):
     lines = torch.empty(cap, dtype=torch.uint8, device=dev)
     loff = torch.empty(n + 1, dtype=torch.int64, device=dev)
     derr = torch.empty(1, dtype=torch.int64, device=dev)
-    vcfc.decode_records_device(out.data_ptr(), int(rec[n]), rec_t.data_ptr(), n, S, lines.data_ptr(), cap,
-                               loff.data_ptr(), dws.data_ptr(), dws_bytes, derr.data_ptr(),
-                               torch.cuda.current_stream(dev).cuda_stream)
-    torch.cuda.synchronize(dev)
-    assert int(derr.cpu().numpy().view(np.uint64)[0]) == vcfc.NO_ERROR
+    for exact in (False, True):   # the light plan assumes 3-byte tokens; code 4 = plan again exactly
+        vcfc.decode_records_device(out.data_ptr(), int(rec[n]), rec_t.data_ptr(), n, S, lines.data_ptr(), cap,
+                                   loff.data_ptr(), dws.data_ptr(), dws_bytes, derr.data_ptr(),
+                                   torch.cuda.current_stream(dev).cuda_stream, exact=exact)
+        torch.cuda.synchronize(dev)
+        e = int(derr.cpu().numpy().view(np.uint64)[0])
+        if e == vcfc.NO_ERROR or (e & 0xFF) != 4:
+            break
+    assert e == vcfc.NO_ERROR, hex(e)
     assert int(loff[n].item()) == rows.total_bytes
     assert bool(torch.equal(lines[:rows.total_bytes], rows.buf[:rows.total_bytes]))

@@ -1,0 +1,51 @@
+"""The synthetic workloads (vcf-compression_amd/workload.py + the generator
+kernel csrc/vcfc_synth.hip, here on the fiber emulator): every row is a
+well-formed VCF data line of the declared shape, and its length is the one
+the host layout assumed.  Law 2 is SURVEY §8(d)'s D3 (general shapes)."""
+import numpy as np
+import pytest
+
+import emu_io as E
+import golden_io as G
+
+
+@pytest.mark.parametrize("law,samples", [(0, 70), (1, 130), (2, 70), (2, 300)])
+def test_rows_are_well_formed(law, samples):
+    n = 60
+    buf, off, ln = E.emu_synth_rows(n, samples, law, seed=5)
+    kinds = set()
+    for i in range(n):
+        line = bytes(buf[int(off[i]):int(off[i]) + int(ln[i])])
+        assert buf[int(off[i]) + int(ln[i])] == 10   # '\n' after each line
+        f = line.split(b"\t")
+        assert len(f) == 9 + samples and all(f), i
+        toks = f[9:]
+        if law != 2:
+            assert all(len(t) == 3 and t[1:2] == b"|" for t in toks)
+            continue
+        kind = int(f[7].split(b"KIND=")[1])
+        kinds.add(kind)
+        if kind == 1:
+            assert f[8] == b"GT:DP:GQ" and all(len(t) == 9 and t[3:4] == b":" and t[6:7] == b":" for t in toks)
+        elif kind == 3:
+            assert all(len(t) == 3 and t[1:2] == b"/" for t in toks)
+        elif kind in (0, 4):
+            assert {len(t) for t in toks} <= {1, 3} and any(len(t) == 1 for t in toks)
+        else:
+            assert all(len(t) == 3 for t in toks)
+        st, _ = G.oracle_encode_line(line)
+        assert st == 0
+    if law == 2:
+        assert kinds == {0, 1, 2, 3, 4}
+
+
+def test_law2_columns_fixed_across_rows():
+    """Haploid (male) and missing samples are column traits: the same columns
+    in every row of their kind."""
+    buf, off, ln = E.emu_synth_rows(80, 90, 2, seed=9)
+    pat = {}
+    for i in range(80):
+        f = bytes(buf[int(off[i]):int(off[i]) + int(ln[i])]).split(b"\t")
+        kind = int(f[7].split(b"KIND=")[1])
+        shape = tuple(len(t) for t in f[9:])
+        assert pat.setdefault(kind, shape) == shape

@@ -27,7 +27,17 @@ __device__ __forceinline__ uint32_t allele(uint32_t u, int law, float af) {
     return x < a1 ? 1u : (x < a1 + 0.005f ? 2u : 0u);
 }
 
-// one wave per row: prefix copy + S tokens "a|b" separated by TABs + '\n'
+// law 2 ("general shapes"): per-column sample traits, the
+// same for every row (as sex and coverage are in a real VCF)
+__device__ __forceinline__ bool col_male(uint32_t j) { return (mix64(0xC0FFEEull ^ j) & 1ull) != 0; }
+__device__ __forceinline__ bool col_missing(uint32_t j) { return (mix64(0xBADC0DEull ^ j) >> 32) < 858993459ull; }
+// token bytes of sample j in a law-2 row of `kind` (see workload.py)
+__device__ __forceinline__ uint32_t law2_len(uint32_t kind, uint32_t j) {
+    return kind == 0 ? (col_male(j) ? 1u : 3u) : kind == 1 ? 9u : kind == 4 ? (col_missing(j) ? 1u : 3u) : 3u;
+}
+
+// one wave per row: prefix copy + S tokens separated by TABs + '\n'.
+// laws 0/1: every token "a|b"; law 2: row_af[row] = kind + allele frequency
 __global__ __launch_bounds__(256) void k_synth(uint8_t *buf, const uint64_t *line_off, uint64_t n,
                                                const uint8_t *prefix, const uint64_t *prefix_off,
                                                const float *row_af, uint32_t S, int law, uint64_t seed) {
@@ -39,7 +49,39 @@ __global__ __launch_bounds__(256) void k_synth(uint8_t *buf, const uint64_t *lin
     const uint32_t P = (uint32_t)(p1 - p0);
     for (uint32_t i = l; i < P; i += 64) dst[i] = prefix[p0 + i];
     uint8_t *g = dst + P;
-    const float af = row_af ? row_af[row] : 0.0f;
+    float af = row_af ? row_af[row] : 0.0f;
+    if (law == 2) {
+        const uint32_t kind = (uint32_t)af;
+        af -= (float)kind;
+        uint32_t base = 0;   // byte offset of the current 64-sample block's first token
+        for (uint32_t j0 = 0; j0 < S; j0 += 64) {
+            const uint32_t j = j0 + l;
+            const uint32_t len = j < S ? law2_len(kind, j) : 0u;
+            const uint32_t inc = vw::scan_add(j < S ? len + 1u : 0u);
+            if (j < S) {
+                uint8_t *t = g + base + inc - (len + 1u);
+                const uint64_t h = mix64(seed ^ mix64(row * 0x100000001B3ull + j));
+                const uint32_t a1 = allele((uint32_t)h, 1, af), a2 = allele((uint32_t)(h >> 32), 1, af);
+                if (len == 1) {
+                    t[0] = kind == 4 ? (uint8_t)'.' : (uint8_t)('0' + a1);
+                } else if (kind == 2 && ((h >> 40) & 0xFFu) < 77u) {   // ~30 % "./."
+                    t[0] = '.'; t[1] = '/'; t[2] = '.';
+                } else {
+                    t[0] = (uint8_t)('0' + a1);
+                    t[1] = kind == 3 ? (uint8_t)'/' : (uint8_t)'|';
+                    t[2] = (uint8_t)('0' + a2);
+                    if (len == 9) {
+                        const uint32_t dp = 10u + (uint32_t)((h >> 48) % 90u), gq = 10u + (uint32_t)((h >> 56) % 90u);
+                        t[3] = ':'; t[4] = (uint8_t)('0' + dp / 10); t[5] = (uint8_t)('0' + dp % 10);
+                        t[6] = ':'; t[7] = (uint8_t)('0' + gq / 10); t[8] = (uint8_t)('0' + gq % 10);
+                    }
+                }
+                t[len] = (uint8_t)(j + 1 == S ? '\n' : '\t');
+            }
+            base += vw::readlane(inc, 63);
+        }
+        return;
+    }
     for (uint32_t j = l; j < S; j += 64) {
         const uint64_t h = mix64(seed ^ mix64(row * 0x100000001B3ull + j));
         const uint32_t a1 = allele((uint32_t)h, law, af), a2 = allele((uint32_t)(h >> 32), law, af);

@@ -13,12 +13,42 @@ law 1 "chr22": 1000 Genomes chr22-shaped rows (BASELINE configs[1]): CHROM 22,
        spectrum), so most rows are rare variants with long 0|0 runs; 1 % of
        rows carry a second ALT (tokens with allele 2 -> escapes).
 
+law 2 "general shapes" (SURVEY §8(d) D3): chrX-shaped rows of five kinds,
+       drawn per row (30/30/15/10/15 %): 0 = haploid males ("0"/"1") beside
+       diploid females, the sex a fixed per-sample (column) trait; 1 = FORMAT
+       GT:DP:GQ, tokens "a|b:DD:GG"; 2 = ~30 % missing "./."; 3 = unphased
+       "a/b" only (every token an escape); 4 = "." for a fixed 20 % of the
+       samples.  Kinds 0, 1 and 4 have tokens of another length than 3, so the
+       encoder's general path takes them; 2 and 3 its escape path.  Per-row
+       allele frequencies as law 1.
+
 The 9 leading columns are built on the host; the genotype columns (the
 dominant bytes) are generated on the GPU by vcfc_synth_rows_device.
 """
 import numpy as np
 
 BASES = np.array(list("ATGC"))
+LAW2_KINDS = np.array([0.30, 0.30, 0.15, 0.10, 0.15])
+M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def _mix64(z):
+    """splitmix64 finaliser over a uint64 array (= vcfc_synth.hip mix64)."""
+    with np.errstate(over="ignore"):
+        z = z + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def law2_token_lengths(samples):
+    """Token bytes of each sample for law-2 row kinds 0..4 ([5, samples])."""
+    j = np.arange(samples, dtype=np.uint64)
+    male = (_mix64(np.uint64(0xC0FFEE) ^ j) & np.uint64(1)) != 0
+    missing = (_mix64(np.uint64(0xBADC0DE) ^ j) >> np.uint64(32)) < np.uint64(858993459)
+    three = np.full(samples, 3, dtype=np.int64)
+    return np.stack([np.where(male, 1, 3), np.full(samples, 9, dtype=np.int64), three, three,
+                     np.where(missing, 1, 3)])
 
 
 def prefixes(n, law, seed, row0=0, samples=2504):
@@ -28,7 +58,22 @@ def prefixes(n, law, seed, row0=0, samples=2504):
     (at S = 2504 these are the 1000 Genomes values)."""
     rng = np.random.default_rng(seed)
     ref = rng.integers(0, 4, n)
-    if law == 0:
+    gt_len = None
+    if law == 2:
+        kind = rng.choice(5, n, p=LAW2_KINDS)
+        gaps = rng.geometric(1.0 / 32.0, n)
+        pos = 2781479 + row0 * 32 + np.cumsum(gaps) - gaps[0]
+        an = 2 * samples
+        k = np.clip(np.floor(np.exp(rng.random(n) * np.log(float(an)))).astype(np.int64), 1, an - 1)
+        afv = k / float(an)
+        alt = (ref + rng.integers(1, 4, n)) % 4
+        fmt = np.where(kind == 1, "GT:DP:GQ", "GT")
+        rows = ["X\t%d\t.\t%s\t%s\t50\tPASS\tAC=%d;AN=%d;KIND=%d\t%s\t"
+                % (pos[i], BASES[ref[i]], BASES[alt[i]], k[i], an, kind[i], fmt[i]) for i in range(n)]
+        # (af just below 1 so kind + af keeps its integer part in float32)
+        af = (kind + np.minimum(afv, 0.999)).astype(np.float32)
+        gt_len = law2_token_lengths(samples).sum(axis=1)[kind] + samples   # tokens + TABs + '\n'
+    elif law == 0:
         alt1 = (ref + rng.integers(1, 4, n)) % 4
         alt2 = (alt1 + 1) % 4
         alt2 = np.where(alt2 == ref, (alt2 + 1) % 4, alt2)
@@ -60,13 +105,15 @@ def prefixes(n, law, seed, row0=0, samples=2504):
     plen = np.fromiter((len(r) for r in rows), dtype=np.int64, count=n)
     poff = np.zeros(n + 1, dtype=np.int64)
     np.cumsum(plen, out=poff[1:])
-    return blob, poff, af, np.asarray(pos, dtype=np.int64)
+    return blob, poff, af, np.asarray(pos, dtype=np.int64), gt_len
 
 
-def layout(prefix_off, samples):
-    """Line offsets/lengths for rows = prefix + `samples` tokens, '\\n'-terminated."""
+def layout(prefix_off, samples, gt_len=None):
+    """Line offsets/lengths for rows = prefix + genotype bytes ('\\n'
+    included: 4 * samples for 3-byte tokens, gt_len[i] for law 2)."""
     plen = np.diff(prefix_off)
-    line_len = (plen + 4 * samples - 1).astype(np.int64)
+    gl = 4 * samples if gt_len is None else np.asarray(gt_len, dtype=np.int64)
+    line_len = (plen + gl - 1).astype(np.int64)
     line_off = np.zeros(len(plen), dtype=np.int64)
     np.cumsum(line_len[:-1] + 1, out=line_off[1:])
     total = int(line_off[-1] + line_len[-1] + 1) if len(plen) else 0
@@ -77,14 +124,15 @@ class DeviceRows:
     """A synthetic batch resident in HBM (torch tensors)."""
 
     def __init__(self, torch, vcfc, n, samples, law, seed, device, row0=0):
-        blob, poff, af, self.pos = prefixes(n, law, seed, row0, samples)
-        self.chrom = "1" if law == 0 else "22"
-        line_off, line_len, total = layout(poff, samples)
+        blob, poff, af, self.pos, gt_len = prefixes(n, law, seed, row0, samples)
+        self.chrom = {0: "1", 1: "22", 2: "X"}[law]
+        line_off, line_len, total = layout(poff, samples, gt_len)
         dev = torch.device(device)
         self.n, self.samples, self.law = n, samples, law
         self.total_bytes = total
         self.line_bytes = int(line_len.astype(np.int64).sum())
-        self.gt_bytes = 4 * samples * n   # bytes after the TAB following FORMAT, incl. '\n'
+        # bytes after the TAB following FORMAT, incl. '\n'
+        self.gt_bytes = 4 * samples * n if gt_len is None else int(np.asarray(gt_len).sum())
         self.buf = torch.empty(total + 64, dtype=torch.uint8, device=dev)
         self.line_off = torch.from_numpy(line_off).to(dev)
         self.line_len = torch.from_numpy(line_len).to(dev)
