@@ -49,3 +49,20 @@ def test_law2_columns_fixed_across_rows():
         kind = int(f[7].split(b"KIND=")[1])
         shape = tuple(len(t) for t in f[9:])
         assert pat.setdefault(kind, shape) == shape
+
+
+@pytest.mark.parametrize("samples,seed", [(300, 1), (2504, 2)])
+def test_law2_rows_encode_like_the_oracle(samples, seed):
+    """Law-2 rows (most of them through the general kernel: tokens of 1 and 9
+    bytes) encoded by the product kernels on the emulator, byte-exact vs the
+    oracle, at several row alignments."""
+    n = 30 if samples > 1000 else 60
+    buf, off, ln = E.emu_synth_rows(n, samples, 2, seed=seed)
+    for shift in (0, 3):
+        b = np.concatenate([np.zeros(shift, dtype=np.uint8), buf]).tobytes()
+        st, out, rec, err = E.emu_encode(b, off + np.uint64(shift), ln)
+        assert err == (1 << 64) - 1
+        for i in range(n):
+            line = b[int(off[i]) + shift:int(off[i]) + shift + int(ln[i])]
+            sto, want = G.oracle_encode_line(line)
+            assert sto == 0 and out[int(rec[i]):int(rec[i + 1])] == want, (shift, i)

@@ -851,104 +851,208 @@ __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring
 }
 
 
-// General path: any line.  64-byte windows, one byte per lane (plus a 3-byte
-// look-ahead for the token-length test), ballot/scan bookkeeping.  Handles
-// empty fields anywhere, 9-column rows, tokens of any length, CR, and the
-// reference's error cases (< 8 fields: VcfValidationError; 8: abort).
+// General path: any line (empty fields anywhere, 9-column rows, tokens of any
+// length, CR, the reference's error cases: < 8 fields VcfValidationError, 8
+// fields abort).  1 KiB chunks, 16 bytes per lane (+ a 4-byte look-ahead),
+// SWAR masks per lane:
+//   T   TAB or outside the line;  fs = field starts (non-T after T);
+//   the wave add-scan of |fs| numbers the fields; fields 0..8 are the prefix
+//   (copied, one TAB before each of fields 1..9), fields >= 9 are tokens.
+// Tokens are classed one per loop step (<= 8 per lane: each needs a T before
+// it) into a 4-bit-stride class word, then run starts, the entering run
+// (max-scan) and its offset mod cap follow esc8's rules.  Every input byte
+// emits [lead][mid][raw]: lead = TAB before fields 1..9 or a token's run-end
+// byte / TAB after an escape; mid = 0xE1 (escape) or a full-run byte; raw =
+// a prefix byte or any byte of an escape token.  The lane's bytes leave as
+// one unaligned ds_write_b32 per input byte, in order: a write's unused high
+// bytes are overwritten by the next one, and the last one's (which reach
+// into the next lanes' first bytes) are repaired from each lane's first
+// four bytes, kept in a register.
+__device__ __forceinline__ uint32_t mask_range16(int32_t lo, int32_t hi) {   // bits [lo, hi) of 0..19
+    lo = lo < 0 ? 0 : lo > 20 ? 20 : lo;
+    hi = hi < 0 ? 0 : hi > 20 ? 20 : hi;
+    return hi > lo ? ((1u << hi) - 1u) ^ ((1u << lo) - 1u) : 0u;
+}
+
 __device__ uint32_t encode_general(const uint8_t *__restrict__ line, uint32_t len, Ring &r,
                                    uint32_t *rec_bytes) {
     const uint32_t l = vw::lane_id();
-    const uint64_t lt = vw::lanemask_lt();
-    uint32_t nf = 0;          // fields started so far
-    uint32_t carry_tab = 1;   // byte before the window is TAB / line start
-    uint32_t ccls = CLS_NONE; // class of the last token started (current token)
-    uint32_t crs = 0;         // run start (+1) of the last token started
+    const uint32_t lead = (uint32_t)(reinterpret_cast<uintptr_t>(line) & 15);
+    const uint8_t *A = line - lead;
+    const uint32_t span = lead + len;
+    const uint32_t nch = (span + CHUNK - 1) / CHUNK;
+    const vw::brsrc rs = vw::make_rsrc(A, (span + 3u) & ~3u);
+    const uint32_t lo16 = BPL * l;
+    uint32_t nf = 0;             // fields started so far
+    uint32_t ntok = 0;           // tokens started so far
+    uint32_t carryT = 1;         // byte before the chunk is T
+    uint32_t pcls = CLS_NONE;    // class of the last token so far
+    uint32_t prs = 1;            // run start (+1) of the last token (token 0: a virtual run begun at it, see esc8)
     uint32_t req = 0;
     r.wpos = 8;
     r.fpos = 0;
-    const uint32_t nwin = (len + 63) / 64;
-    for (uint32_t w = 0; w < nwin; w++) {
-        const uint32_t x = w * 64 + l;
-        auto at = [&](uint32_t y) -> uint32_t { return y < len ? (uint32_t)line[y] : 0x09u; };
-        const uint32_t b0 = at(x), b1 = at(x + 1), b2 = at(x + 2), b3 = at(x + 3);
-        const uint32_t tab = b0 == 0x09u ? 1u : 0u;
-        const uint32_t ptab = vw::shr1(tab, carry_tab);
-        const bool start = !tab && ptab;
-        const uint64_t sm = vw::ballot(start);
-        // field index of a non-TAB byte = index of the last start at or before it
-        const uint32_t kcur = nf + (uint32_t)vw::popc64(sm & (lt | (1ull << l))) - 1u;
-        // token class at a start (3-byte test needs 3 bytes of look-ahead)
-        const bool len3 = b1 != 0x09u && b2 != 0x09u && b3 == 0x09u;
-        const uint32_t mycls = start ? (len3 ? cls_of(b0 | (b1 << 8) | (b2 << 16)) : CLS_ESC) : CLS_NONE;
-        const bool tok_start = start && kcur >= 9;
-        const uint32_t t = kcur - 9;   // token index (valid when kcur >= 9)
-        // previous token class for a start lane / current token class for any byte
-        const uint64_t tsm = vw::ballot(tok_start);
-        const uint64_t before = tsm & lt;
-        const uint32_t cls_from = vw::shfl(mycls, before ? (uint32_t)vw::hibit64(before) : 0u);
-        const uint32_t pcls = before ? cls_from : ccls;        // class of the previous token
-        const uint64_t upto = tsm & (lt | (1ull << l));
-        const uint32_t cls_cur_from = vw::shfl(mycls, upto ? (uint32_t)vw::hibit64(upto) : 0u);
-        const uint32_t curcls = upto ? cls_cur_from : ccls;    // class of the token holding this byte
-        const bool s = tok_start && (mycls == CLS_ESC || pcls == CLS_ESC || mycls != pcls);
-        const uint32_t rs_inc = vw::scan_max(s ? t + 1 : 0u);
-        const uint32_t rj = vw::umax(rs_inc, crs);                       // run start (+1) of this token
-        const uint32_t rp = vw::umax(vw::shr1(rs_inc, 0u), crs);         // run start (+1) of the previous
-        // counts
-        uint32_t n = 0;
-        const bool pre_byte = !tab && kcur <= 8;
-        const bool pre_tab = start && kcur >= 1 && kcur <= 9;
-        n += pre_byte ? 1u : 0u;
-        n += pre_tab ? 1u : 0u;
-        uint32_t pe = 0, pc = 0, fu = 0;
-        if (tok_start) {
-            if (s && pcls < CLS_ESC) {
-                const uint32_t off = (t - rp) % cls_cap(pcls);
-                pe = off != cls_cap(pcls) - 1 ? 1u : 0u;
-                pc = off + 1;
-            }
-            if (mycls < CLS_ESC) fu = ((t + 1 - rj) % cls_cap(mycls)) == cls_cap(mycls) - 1 ? 1u : 0u;
-            n += (pcls == CLS_ESC ? 1u : 0u) + pe + (mycls == CLS_ESC ? 2u : fu);
-        } else if (!tab && kcur >= 9 && curcls == CLS_ESC) {
-            n += 1;   // raw byte inside an escaped token
+    Chunk nxt = load_chunk(rs, 0, lo16);
+    for (uint32_t c = 0; c < nch; c = vw::readfirst(c + 1)) {
+        const Chunk cur = look_ahead(nxt);
+        if (c + 1 < nch) nxt = load_chunk(rs, c + 1, lo16);
+        const int32_t x0 = (int32_t)(c * CHUNK + lo16) - (int32_t)lead;   // line offset of lane byte 0
+        // ---- T mask over the lane's 16 bytes + 4 look-ahead bytes ----
+        uint32_t tab = 0;
+#pragma unroll
+        for (int k = 0; k <= (int)TPL; k++) tab |= zero_bytes4(cur.w(k) ^ 0x09090909u) << (4 * k);
+        const uint32_t inl = mask_range16(-x0, (int32_t)len - x0);
+        const uint32_t T20 = (tab & inl) | (~inl & 0xFFFFFu);
+        const uint32_t Tm = T20 & 0xFFFFu;
+        const uint32_t pin = vw::shr1(Tm >> 15, carryT);
+        const uint32_t fs = ~Tm & ((Tm << 1) | pin) & 0xFFFFu;
+        const uint32_t nfs = (uint32_t)__builtin_popcount(fs);
+        const uint32_t finc = vw::scan_add(nfs);
+        const uint32_t fb = nf + finc - nfs;   // field index of the lane's first start
+        // ---- prefix / token split ----
+        uint32_t ts = fs, pmask = 0, leadp = 0;
+        if (nf < 10) {   // (wave-uniform) the prefix may end in this chunk
+            for (uint32_t k = fb; k < 9 && ts; k++) ts &= ts - 1u;
+            const uint32_t tok0 = fb <= 9 ? (ts & (0u - ts)) : 0u;   // start of field 9 (token 0)
+            pmask = tok0 ? tok0 - 1u : (fb <= 9 ? 0xFFFFu : 0u);
+            const uint32_t f0 = fb == 0 ? (fs & (0u - fs)) : 0u;     // field 0: no TAB before it
+            leadp = (fs & pmask & ~f0) | tok0;
+            const uint32_t nreq = (uint32_t)__builtin_popcount(pmask & ~Tm) + (uint32_t)__builtin_popcount(leadp);
+            req += vw::readlane(vw::scan_add(nreq), 63);
         }
-        const uint32_t inc = vw::scan_add(n);
-        uint32_t pos = r.wpos + inc - n;
-        if (pre_tab) ring_put(r, pos++, 0x09u);
-        if (pre_byte) ring_put(r, pos++, b0);
-        if (tok_start) {
-            if (pcls == CLS_ESC) ring_put(r, pos++, 0x09u);
-            if (pe) ring_put(r, pos++, cls_mask(pcls) | pc);
-            if (mycls == CLS_ESC) {
-                ring_put(r, pos++, 0xE1u);
-                ring_put(r, pos++, b0);
-            } else if (fu) {
-                ring_put(r, pos++, cls_mask(mycls) | cls_cap(mycls));
+        // ---- classify the lane's tokens (in order) ----
+        const uint32_t nt = (uint32_t)__builtin_popcount(ts);
+        const uint32_t tinc = vw::scan_add(nt);
+        const uint32_t t0 = ntok + tinc - nt;   // token index of the lane's first token
+        uint32_t cl4 = 0, pos4 = 0, rem = ts;
+        for (uint32_t k = 0; vw::ballot(rem != 0); k++) {
+            if (rem) {
+                const uint32_t i = vw::ffbl(rem);
+                const uint32_t q = i >> 2;
+                const uint32_t lo = q == 0 ? cur.a.x : q == 1 ? cur.a.y : q == 2 ? cur.a.z : cur.a.w;
+                const uint32_t hi = q == 0 ? cur.a.y : q == 1 ? cur.a.z : q == 2 ? cur.a.w : cur.y;
+                const uint32_t d = vw::alignbyte(hi, lo, i & 3u);
+                const bool len3 = ((T20 >> (i + 1)) & 7u) == 4u;   // bytes i+1, i+2 not T; i+3 T
+                const uint32_t cls = len3 ? cls_f(d) : CLS_ESC;
+                cl4 |= cls << (4 * k);
+                pos4 |= i << (4 * k);
+                rem &= rem - 1u;
             }
-        } else if (!tab && kcur >= 9 && curcls == CLS_ESC) {
-            ring_put(r, pos++, b0);
         }
-        // REQ counts the prefix part only
-        const uint32_t npre = (pre_byte ? 1u : 0u) + (pre_tab ? 1u : 0u);
-        req += vw::readlane(vw::scan_add(npre), 63);
-        r.wpos += vw::readlane(inc, 63);
+        const uint32_t vbits = nt >= 8 ? 0x11111111u : (0x11111111u & ((1u << (4 * nt)) - 1u));
+        // the token before the lane: previous lanes' last token, else the chunk carry
+        const uint32_t lastc = nt ? (cl4 >> (4 * (nt - 1))) & 7u : 0u;
+        const uint32_t pk = nt ? ((t0 + nt) << 3) | lastc : 0u;
+        const uint32_t skc = vw::scan_max(pk);
+        const uint32_t pe = vw::shr1z(skc);
+        const uint32_t cin = pe ? (pe & 7u) : pcls;                  // class of the token before the lane
+        const uint32_t p0 = cin == CLS_NONE ? (cl4 & 3u) : cin;      // token 0: virtual run of its own class
+        const uint32_t cp4 = (cl4 << 4) | p0;                         // class of token k-1 at bits 4k
+        const uint32_t xc = cl4 ^ cp4;
+        const uint32_t sb = (xc | (xc >> 1) | (xc >> 2) | (cl4 >> 2)) & vbits;   // run starts (escapes always)
+        const uint32_t eb = (cl4 >> 2) & vbits;                                  // escapes
+        const uint32_t lane_rs = sb ? (t0 + 8u) - ((uint32_t)__builtin_clz(sb) >> 2) : 0u;
+        const uint32_t incl = vw::scan_max(lane_rs);
+        const uint32_t rin = vw::umax(vw::shr1z(incl), prs);
+        const bool is00 = p0 == 0;
+        const uint32_t cap = is00 ? 127u : 31u;
+        const uint32_t mp = mod_cap(t0 + MOD_BIAS - rin, is00);   // run offset of token t0 - 1, mod cap
+        const uint32_t fb1 = sb ? (uint32_t)__builtin_ctz(sb) : 32u;
+        const uint32_t j1 = fb1 >> 2;                                // first start (8: none)
+        const uint32_t m0 = vw::perm(0x80C0A000u, 0x80C0A000u, p0 & 3u);
+        const uint32_t jf = cap - 2u - mp;                           // token completing a chunk of cap
+        const bool full = p0 < CLS_ESC && jf < j1 && jf < nt;
+        uint32_t rr = mp + j1;
+        rr = umin32(rr, rr - cap);
+        const bool pesc = p0 == CLS_ESC;
+        const bool lead1 = j1 < nt && (pesc || rr != cap - 1u);
+        const uint32_t b1 = pesc ? 0x09u : (m0 | (rr + 1u));
+        // per token: lead byte value (LV, 8 bytes) and the byte masks
+        uint32_t LV0 = 0, LV1 = 0, leadt = 0, midt = 0, escm = 0;
+        {
+            uint32_t kp = 0;
+            bool seen = false;
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const bool s = (sb >> (4 * k)) & 1u;
+                const bool e = (eb >> (4 * k)) & 1u;
+                const uint32_t pc = (cp4 >> (4 * k)) & 7u;
+                const uint32_t bit = 1u << ((pos4 >> (4 * k)) & 15u);
+                const bool ld = s && (seen || lead1);
+                const uint32_t b = !seen ? b1
+                                 : (pc == CLS_ESC ? 0x09u : (vw::perm(0x80C0A000u, 0x80C0A000u, pc & 3u) | ((uint32_t)k - kp)));
+                if (k < 4) LV0 |= b << (8 * k); else LV1 |= b << (8 * (k - 4));
+                leadt |= ld ? bit : 0u;
+                midt |= (e || (full && (uint32_t)k == jf)) ? bit : 0u;
+                escm |= e ? bit : 0u;
+                if (s) { seen = true; kp = (uint32_t)k; }
+            }
+        }
+        const uint32_t fullbit = full ? 1u << ((pos4 >> (4 * jf)) & 15u) : 0u;
+        const uint32_t fullb = m0 | cap;
+        // bytes of escape tokens: fill each token start's escape flag up to the next start
+        uint32_t ev = escm, em = ts;
+#pragma unroll
+        for (int d = 1; d < 16; d <<= 1) {
+            ev |= (ev << d) & ~em;
+            em |= em << d;
+        }
+        ev = (ev | (cin == CLS_ESC ? ~em : 0u)) & 0xFFFFu;
+        const uint32_t RAW = ((pmask | (ev & ~pmask)) & ~Tm) & 0xFFFFu;
+        const uint32_t LEAD = leadp | leadt, MID = midt;
+        const uint32_t cnt = (uint32_t)__builtin_popcount(RAW) + (uint32_t)__builtin_popcount(LEAD) +
+                             (uint32_t)__builtin_popcount(MID);
+        const uint32_t inc2 = vw::scan_add(cnt);
+        const uint32_t base = (r.wpos + inc2 - cnt) & RMASK;
+        uint8_t *const lb = r.lds + base;
+        uint32_t o = 0, head = 0;
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const uint32_t li = (LEAD >> i) & 1u, mi = (MID >> i) & 1u, ri = (RAW >> i) & 1u;
+            const uint32_t k = (uint32_t)__builtin_popcount(ts & ((1u << i) - 1u));   // token ordinal at a token start
+            const uint32_t lvw = k < 4 ? LV0 : LV1;
+            const uint32_t lv = ((leadt >> i) & 1u) ? ((lvw >> (8u * (k & 3u))) & 0xFFu) : 0x09u;
+            const uint32_t mv = ((fullbit >> i) & 1u) ? fullb : 0xE1u;
+            const uint32_t rv = byte_of(cur.a, (uint32_t)i);
+            const uint32_t a = mi ? (mv | (rv << 8)) : rv;
+            const uint32_t v = li ? (lv | (a << 8)) : a;
+            __builtin_memcpy(lb + o, &v, 4);
+            const uint32_t cb = li + mi + ri;   // bytes this input byte emits (<= 3)
+            head |= o < 4 ? (v & ((1u << (8u * cb)) - 1u)) << (8u * o) : 0u;
+            o += cb;
+        }
+        // repair the first bytes the previous lanes' last writes ran over
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++) {
+            uint8_t *const dm = r.lds + RING_DUMMY + 4u * l;
+            *(q < o ? lb + q : dm) = (uint8_t)(head >> (8 * q));
+        }
+        const bool wrap = base + o > RING;
+        if (vw::ballot(wrap)) {
+            if (wrap) {
+                for (uint32_t q = RING; q < base + o; q++) r.lds[q - RING] = r.lds[q];
+            }
+        }
+        r.wpos += vw::readlane(inc2, 63);
         // carries
-        nf += (uint32_t)vw::popc64(sm);
-        carry_tab = vw::readlane(tab, 63);
-        if (tsm) {
-            const uint32_t last = (uint32_t)vw::hibit64(tsm);
-            ccls = vw::readlane(mycls, last);
-            crs = vw::readlane(rj, last);
-        }
+        nf += vw::readlane(finc, 63);
+        ntok += vw::readlane(tinc, 63);
+        carryT = vw::readlane(Tm >> 15, 63);
+        const uint32_t last = vw::readlane(skc, 63);
+        if (last) pcls = last & 7u;
+        prs = vw::umax(vw::readlane(incl, 63), prs);
         ring_flush(r, false);
     }
     if (nf < 8) return VCFCD_E_LT8COLS;
     if (nf == 8) return VCFCD_E_8COLS;
-    const uint32_t T = nf - 9;
-    uint32_t extra = 0;
-    if (T > 0 && ccls < CLS_ESC && ((T - crs) % cls_cap(ccls)) != cls_cap(ccls) - 1) extra = 1;
+    // row end: pending chunk of the last run, then '\n'
+    const uint32_t T = ntok;
+    uint32_t extra = 0, pb = 0;
+    if (T > 0 && pcls < CLS_ESC) {
+        const uint32_t off = mod_cap(T - prs, pcls == 0);
+        if (off != (pcls == 0 ? 126u : 30u)) { extra = 1; pb = cls_mask_f(pcls) | (off + 1); }
+    }
     if (l == 0) {
-        if (extra) ring_put(r, r.wpos, cls_mask(ccls) | (((T - crs) % cls_cap(ccls)) + 1));
+        if (extra) ring_put(r, r.wpos, pb);
         ring_put(r, r.wpos + extra, 0x0Au);
     }
     r.wpos += extra + 1;
