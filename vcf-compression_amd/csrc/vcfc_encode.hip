@@ -7,7 +7,7 @@
 //   k_encode_fast     one wave64 per row: tokenise, RLE-encode, stage the
 //                     record in an LDS ring, stream it to the row's staging in
 //                     1 KiB bursts; rows of another shape are queued
-//   k_encode_general  persistent waves encode the queued rows (any shape)
+//   k_encode_general  one wave per queued row (any shape)
 //   scan<IDENT>  rec_off[i] = sum_{k<i} rec_size_k             (tiny)
 //   k_compact    16 (long rows: 64) lanes per row: staging -> final offset,
 //                16-byte stores
@@ -863,11 +863,11 @@ __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring
 // (max-scan) and its offset mod cap follow esc8's rules.  Every input byte
 // emits [lead][mid][raw]: lead = TAB before fields 1..9 or a token's run-end
 // byte / TAB after an escape; mid = 0xE1 (escape) or a full-run byte; raw =
-// a prefix byte or any byte of an escape token.  The lane's bytes leave as
-// one unaligned ds_write_b32 per input byte, in order: a write's unused high
-// bytes are overwritten by the next one, and the last one's (which reach
-// into the next lanes' first bytes) are repaired from each lane's first
-// four bytes, kept in a register.
+// a prefix byte or any byte of an escape token.  The raw bytes go to the
+// ring in one pass over the lane's 16 bytes (one ds_write_b8 each, a dummy
+// byte when there is none), the lead / mid bytes in a second pass over the
+// insertion points only (<= 8 per lane; the pass ends with the lane that
+// has the most).
 __device__ __forceinline__ uint32_t mask_range16(int32_t lo, int32_t hi) {   // bits [lo, hi) of 0..19
     lo = lo < 0 ? 0 : lo > 20 ? 20 : lo;
     hi = hi < 0 ? 0 : hi > 20 ? 20 : hi;
@@ -908,6 +908,48 @@ __device__ uint32_t encode_general(const uint8_t *__restrict__ line, uint32_t le
         const uint32_t nfs = (uint32_t)__builtin_popcount(fs);
         const uint32_t finc = vw::scan_add(nfs);
         const uint32_t fb = nf + finc - nfs;   // field index of the lane's first start
+        // ---- escape-copy chunk: every token an escape of another length than
+        // 3 (e.g. "a|b:DP:GQ", haploid "0"), single TABs, entered inside an
+        // escape token: every token start emits TAB (its predecessor is an
+        // escape) and 0xE1, every other non-TAB byte itself.
+        if (nf >= 10 && pcls == CLS_ESC) {
+            const uint32_t tabs = tab & inl & 0xFFFFu;
+            const bool odd = (tabs & ((T20 >> 1) | (Tm << 1) | pin)) != 0 ||          // empty field / trailing TAB
+                             (fs & ~(T20 >> 1) & ~(T20 >> 2) & (T20 >> 3) & 0xFFFFu) != 0;   // a 3-byte token
+            if (!vw::ballot(odd)) {
+                const uint32_t in16 = ~Tm & 0xFFFFu;   // in-line non-TAB bytes
+                const uint32_t cnt = (uint32_t)__builtin_popcount(in16) + 2u * nfs;
+                const uint32_t inc2 = vw::scan_add(cnt);
+                const uint32_t base = (r.wpos + inc2 - cnt) & RMASK;
+                uint8_t *const lb = r.lds + base;
+                uint8_t *const dm = r.lds + RING_DUMMY + 4u * l;
+                uint32_t o = 0;
+#pragma unroll
+                for (int i = 0; i < 16; i++) {
+                    const bool st = (fs >> i) & 1u;
+                    const uint16_t te = 0xE109u;   // TAB, 0xE1
+                    __builtin_memcpy(st ? lb + o : dm, &te, 2);
+                    o += st ? 2u : 0u;
+                    const bool in = (in16 >> i) & 1u;
+                    *(in ? lb + o : dm) = (uint8_t)byte_of(cur.a, (uint32_t)i);
+                    o += in ? 1u : 0u;
+                }
+                const bool wrap = base + o > RING;
+                if (vw::ballot(wrap)) {
+                    if (wrap) {
+                        for (uint32_t q = RING; q < base + o; q++) r.lds[q - RING] = r.lds[q];
+                    }
+                }
+                r.wpos += vw::readlane(inc2, 63);
+                const uint32_t nst = vw::readlane(finc, 63);
+                nf += nst;
+                ntok += nst;
+                if (nst) prs = ntok;   // every escape starts a run
+                carryT = vw::readlane(Tm >> 15, 63);
+                ring_flush(r, false);
+                continue;
+            }
+        }
         // ---- prefix / token split ----
         uint32_t ts = fs, pmask = 0, leadp = 0;
         if (nf < 10) {   // (wave-uniform) the prefix may end in this chunk
@@ -923,7 +965,7 @@ __device__ uint32_t encode_general(const uint8_t *__restrict__ line, uint32_t le
         const uint32_t nt = (uint32_t)__builtin_popcount(ts);
         const uint32_t tinc = vw::scan_add(nt);
         const uint32_t t0 = ntok + tinc - nt;   // token index of the lane's first token
-        uint32_t cl4 = 0, pos4 = 0, rem = ts;
+        uint32_t cl4 = 0, rem = ts;
         for (uint32_t k = 0; vw::ballot(rem != 0); k++) {
             if (rem) {
                 const uint32_t i = vw::ffbl(rem);
@@ -934,7 +976,6 @@ __device__ uint32_t encode_general(const uint8_t *__restrict__ line, uint32_t le
                 const bool len3 = ((T20 >> (i + 1)) & 7u) == 4u;   // bytes i+1, i+2 not T; i+3 T
                 const uint32_t cls = len3 ? cls_f(d) : CLS_ESC;
                 cl4 |= cls << (4 * k);
-                pos4 |= i << (4 * k);
                 rem &= rem - 1u;
             }
         }
@@ -966,29 +1007,21 @@ __device__ uint32_t encode_general(const uint8_t *__restrict__ line, uint32_t le
         const bool pesc = p0 == CLS_ESC;
         const bool lead1 = j1 < nt && (pesc || rr != cap - 1u);
         const uint32_t b1 = pesc ? 0x09u : (m0 | (rr + 1u));
-        // per token: lead byte value (LV, 8 bytes) and the byte masks
-        uint32_t LV0 = 0, LV1 = 0, leadt = 0, midt = 0, escm = 0;
-        {
-            uint32_t kp = 0;
-            bool seen = false;
-#pragma unroll
-            for (int k = 0; k < 8; k++) {
-                const bool s = (sb >> (4 * k)) & 1u;
-                const bool e = (eb >> (4 * k)) & 1u;
-                const uint32_t pc = (cp4 >> (4 * k)) & 7u;
-                const uint32_t bit = 1u << ((pos4 >> (4 * k)) & 15u);
-                const bool ld = s && (seen || lead1);
-                const uint32_t b = !seen ? b1
-                                 : (pc == CLS_ESC ? 0x09u : (vw::perm(0x80C0A000u, 0x80C0A000u, pc & 3u) | ((uint32_t)k - kp)));
-                if (k < 4) LV0 |= b << (8 * k); else LV1 |= b << (8 * (k - 4));
-                leadt |= ld ? bit : 0u;
-                midt |= (e || (full && (uint32_t)k == jf)) ? bit : 0u;
+        // per-byte masks: LEAD (a byte before the input byte: TAB before
+        // fields 1..9, a token's run-end byte or TAB after an escape), MID
+        // (0xE1 of an escape, a full-run byte), RAW (the input byte itself:
+        // prefix bytes, bytes of escape tokens)
+        uint32_t leadt = 0, midt = 0, escm = 0;
+        for (uint32_t k = 0, rm = ts; vw::ballot(rm != 0); k++) {
+            if (rm) {
+                const uint32_t bit = rm & (0u - rm);
+                const bool s = (sb >> (4 * k)) & 1u, e = (eb >> (4 * k)) & 1u;
+                leadt |= (s && (k != j1 || lead1)) ? bit : 0u;
+                midt |= (e || (full && k == jf)) ? bit : 0u;
                 escm |= e ? bit : 0u;
-                if (s) { seen = true; kp = (uint32_t)k; }
+                rm &= rm - 1u;
             }
         }
-        const uint32_t fullbit = full ? 1u << ((pos4 >> (4 * jf)) & 15u) : 0u;
-        const uint32_t fullb = m0 | cap;
         // bytes of escape tokens: fill each token start's escape flag up to the next start
         uint32_t ev = escm, em = ts;
 #pragma unroll
@@ -997,34 +1030,46 @@ __device__ uint32_t encode_general(const uint8_t *__restrict__ line, uint32_t le
             em |= em << d;
         }
         ev = (ev | (cin == CLS_ESC ? ~em : 0u)) & 0xFFFFu;
-        const uint32_t RAW = ((pmask | (ev & ~pmask)) & ~Tm) & 0xFFFFu;
+        const uint32_t RAW = (pmask | ev) & ~Tm & 0xFFFFu;
         const uint32_t LEAD = leadp | leadt, MID = midt;
         const uint32_t cnt = (uint32_t)__builtin_popcount(RAW) + (uint32_t)__builtin_popcount(LEAD) +
                              (uint32_t)__builtin_popcount(MID);
         const uint32_t inc2 = vw::scan_add(cnt);
         const uint32_t base = (r.wpos + inc2 - cnt) & RMASK;
         uint8_t *const lb = r.lds + base;
-        uint32_t o = 0, head = 0;
+        uint8_t *const dm = r.lds + RING_DUMMY + 4u * l;
+        // pass 1: the raw bytes, each at its place after the bytes inserted before it
+        uint32_t o = 0;
 #pragma unroll
         for (int i = 0; i < 16; i++) {
-            const uint32_t li = (LEAD >> i) & 1u, mi = (MID >> i) & 1u, ri = (RAW >> i) & 1u;
-            const uint32_t k = (uint32_t)__builtin_popcount(ts & ((1u << i) - 1u));   // token ordinal at a token start
-            const uint32_t lvw = k < 4 ? LV0 : LV1;
-            const uint32_t lv = ((leadt >> i) & 1u) ? ((lvw >> (8u * (k & 3u))) & 0xFFu) : 0x09u;
-            const uint32_t mv = ((fullbit >> i) & 1u) ? fullb : 0xE1u;
-            const uint32_t rv = byte_of(cur.a, (uint32_t)i);
-            const uint32_t a = mi ? (mv | (rv << 8)) : rv;
-            const uint32_t v = li ? (lv | (a << 8)) : a;
-            __builtin_memcpy(lb + o, &v, 4);
-            const uint32_t cb = li + mi + ri;   // bytes this input byte emits (<= 3)
-            head |= o < 4 ? (v & ((1u << (8u * cb)) - 1u)) << (8u * o) : 0u;
-            o += cb;
+            o += ((LEAD >> i) & 1u) + ((MID >> i) & 1u);
+            const bool ri = (RAW >> i) & 1u;
+            *(ri ? lb + o : dm) = (uint8_t)byte_of(cur.a, (uint32_t)i);
+            o += ri ? 1u : 0u;
         }
-        // repair the first bytes the previous lanes' last writes ran over
-#pragma unroll
-        for (uint32_t q = 0; q < 4; q++) {
-            uint8_t *const dm = r.lds + RING_DUMMY + 4u * l;
-            *(q < o ? lb + q : dm) = (uint8_t)(head >> (8 * q));
+        // pass 2: the inserted bytes, one insertion point (a field or token
+        // start) per step
+        for (uint32_t rm = LEAD | MID; vw::ballot(rm != 0);) {
+            if (rm) {
+                const uint32_t i = vw::ffbl(rm);
+                const uint32_t below = (1u << i) - 1u;
+                const uint32_t oi = (uint32_t)__builtin_popcount(RAW & below) + (uint32_t)__builtin_popcount(LEAD & below) +
+                                    (uint32_t)__builtin_popcount(MID & below);
+                const bool li = (LEAD >> i) & 1u, mi = (MID >> i) & 1u;
+                uint32_t lv = 0x09u, mv = 0xE1u;
+                if ((ts >> i) & 1u) {   // a token start: its run-end byte (not token 0's TAB), its escape / full byte
+                    const uint32_t k = (uint32_t)__builtin_popcount(ts & below);
+                    const uint32_t pc = (cp4 >> (4 * k)) & 7u;
+                    const uint32_t sbk = sb & ((1u << (4 * k)) - 1u);   // starts before token k
+                    const uint32_t kp = sbk ? (31u - (uint32_t)__builtin_clz(sbk)) >> 2 : 0u;
+                    if ((leadt >> i) & 1u)
+                        lv = k == j1 ? b1 : (pc == CLS_ESC ? 0x09u : (vw::perm(0x80C0A000u, 0x80C0A000u, pc & 3u) | (k - kp)));
+                    mv = (eb >> (4 * k)) & 1u ? 0xE1u : (m0 | cap);
+                }
+                *(li ? lb + oi : dm) = (uint8_t)lv;
+                *(mi ? lb + oi + (li ? 1u : 0u) : dm) = (uint8_t)mv;
+                rm &= rm - 1u;
+            }
         }
         const bool wrap = base + o > RING;
         if (vw::ballot(wrap)) {
@@ -1109,21 +1154,27 @@ __global__ __launch_bounds__(256) void k_encode_fast(VcfcEncodeArgs a) {
     }
 }
 
-// General kernel: persistent waves drain the retry list.
+// General kernel: one wave per row of the retry list.
+#ifndef VCFC_GEN_WPE
+#define VCFC_GEN_WPE 0
+#endif
+#if VCFC_GEN_WPE
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VCFC_GEN_WPE, VCFC_GEN_WPE))) void k_encode_general(VcfcEncodeArgs a) {
+#else
 __global__ __launch_bounds__(256) void k_encode_general(VcfcEncodeArgs a) {
+#endif
     __shared__ __attribute__((aligned(16))) uint8_t lds[K1_WAVES * RING_STRIDE];
     const uint32_t wave = vw::readfirst(threadIdx.x >> 6);
-    const uint32_t cnt = *a.retry_count;
-    for (uint64_t i = (uint64_t)blockIdx.x * K1_WAVES + wave; i < cnt; i += (uint64_t)gridDim.x * K1_WAVES) {
-        const uint64_t row = a.retry[i];
-        Ring r;
-        if (!row_setup(a, row, lds + wave * RING_STRIDE, r)) continue;
-        uint32_t bytes = 0;
-        const uint32_t st = encode_general(a.buf + a.line_off[row], a.line_len[row], r, &bytes);
-        if (vw::lane_id() == 0) {
-            a.rec_size[row] = st == VCFCD_OK ? bytes : 0u;
-            if (st != VCFCD_OK) atomicMin((unsigned long long *)a.err, (unsigned long long)((row << 8) | st));
-        }
+    const uint64_t i = (uint64_t)blockIdx.x * K1_WAVES + wave;
+    if (i >= *a.retry_count) return;
+    const uint64_t row = a.retry[i];
+    Ring r;
+    if (!row_setup(a, row, lds + wave * RING_STRIDE, r)) return;
+    uint32_t bytes = 0;
+    const uint32_t st = encode_general(a.buf + a.line_off[row], a.line_len[row], r, &bytes);
+    if (vw::lane_id() == 0) {
+        a.rec_size[row] = st == VCFCD_OK ? bytes : 0u;
+        if (st != VCFCD_OK) atomicMin((unsigned long long *)a.err, (unsigned long long)((row << 8) | st));
     }
 }
 
@@ -1313,7 +1364,10 @@ hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t s, hipEvent_t
     if ((e = hipGetLastError()) != hipSuccess) return e;
     {
         const uint64_t want = (a.n + K1_WAVES - 1) / K1_WAVES;
-        hipLaunchKernelGGL(k_encode_general, dim3((unsigned)(want < 2048 ? want : 2048)), dim3(64 * K1_WAVES), 0, s, a);
+        // one wave per queued row: a grid for every row, the waves past the
+        // queue's length exit at once (the hardware dispatcher balances rows
+        // of very different lengths better than a persistent grid)
+        hipLaunchKernelGGL(k_encode_general, dim3((unsigned)want), dim3(64 * K1_WAVES), 0, s, a);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (ev) (void)hipEventRecord(ev[2], s);
