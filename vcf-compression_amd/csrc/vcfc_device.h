@@ -13,6 +13,8 @@
 
 // error word: min over failing rows of (row << 8 | code); ~0 = no error
 #define VCFCD_NO_ERROR (~0ull)
+// rec_size value of a row the fast kernel leaves to the general kernel
+#define VCFCD_RETRY 0xFFFFFFFFu
 
 struct VcfcEncodeArgs {
     // input: concatenated VCF data lines (device memory)
@@ -30,8 +32,7 @@ struct VcfcEncodeArgs {
     uint32_t *rec_size;        // n
     uint64_t *partials;        // scan partials
     uint64_t *err;             // 1 word
-    uint32_t *retry;           // rows the fast kernel hands to the general one
-    uint32_t *retry_count;
+    uint32_t *retry_count;     // rows that took the general kernel (test builds only, VCFC_COUNT_RETRIES)
     uint8_t *prim;             // per-row primary staging: record bytes [0, VCFC_PRIM) at prim + VCFC_PRIM * row
     uint8_t *slots;            // per-row overflow slots: record bytes [VCFC_PRIM, ...) at slots + slot_off[row]
     uint64_t slots_cap;
@@ -44,7 +45,7 @@ struct VcfcEncodeArgs {
 #define VCFC_PRIM 1024u
 
 struct VcfcWorkspaceLayout {
-    uint64_t slot_off, rec_size, partials, err, retry, retry_count, prim, slots, total;
+    uint64_t slot_off, rec_size, partials, err, retry_count, prim, slots, total;
 };
 
 // Bytes of per-row staging for a line of `len` bytes: covers the worst-case
@@ -67,7 +68,6 @@ inline void vcfc_encode_args_workspace(VcfcEncodeArgs &a, uint8_t *ws, const Vcf
     a.slot_off = reinterpret_cast<uint64_t *>(ws + L.slot_off);
     a.rec_size = reinterpret_cast<uint32_t *>(ws + L.rec_size);
     a.partials = reinterpret_cast<uint64_t *>(ws + L.partials);
-    a.retry = reinterpret_cast<uint32_t *>(ws + L.retry);
     a.retry_count = reinterpret_cast<uint32_t *>(ws + L.retry_count);
     a.prim = ws + L.prim;
     a.slots = ws + L.slots;

@@ -1145,16 +1145,15 @@ __global__ __launch_bounds__(256) void k_encode_fast(VcfcEncodeArgs a) {
     uint32_t bytes = 0;
     const bool ok = encode_fast(a.buf + a.line_off[row], a.line_len[row], r, &bytes);
     if (vw::lane_id() == 0) {
-        if (ok) {
-            a.rec_size[row] = bytes;
-        } else {
-            const uint32_t k = atomicAdd(a.retry_count, 1u);
-            a.retry[k] = (uint32_t)row;
-        }
+        // not the fast shape: the general kernel's wave for this row takes
+        // it (a flag per row, no shared queue: 750k rows appending to one
+        // counter serialise at the memory side, ~8 ms on the law-2 rows)
+        a.rec_size[row] = ok ? bytes : VCFCD_RETRY;
     }
 }
 
-// General kernel: one wave per row of the retry list.
+// General kernel: one wave per row; only the rows the fast kernel flagged
+// (VCFCD_RETRY) do work, the other waves exit at once.
 #ifndef VCFC_GEN_WPE
 #define VCFC_GEN_WPE 0
 #endif
@@ -1165,9 +1164,11 @@ __global__ __launch_bounds__(256) void k_encode_general(VcfcEncodeArgs a) {
 #endif
     __shared__ __attribute__((aligned(16))) uint8_t lds[K1_WAVES * RING_STRIDE];
     const uint32_t wave = vw::readfirst(threadIdx.x >> 6);
-    const uint64_t i = (uint64_t)blockIdx.x * K1_WAVES + wave;
-    if (i >= *a.retry_count) return;
-    const uint64_t row = a.retry[i];
+    const uint64_t row = (uint64_t)blockIdx.x * K1_WAVES + wave;
+    if (row >= a.n || a.rec_size[row] != VCFCD_RETRY) return;
+#ifdef VCFC_COUNT_RETRIES   // test builds (tests/simt_emu): rows that took the general kernel
+    if (vw::lane_id() == 0) atomicAdd(a.retry_count, 1u);
+#endif
     Ring r;
     if (!row_setup(a, row, lds + wave * RING_STRIDE, r)) return;
     uint32_t bytes = 0;
@@ -1343,7 +1344,6 @@ VcfcWorkspaceLayout vcfc_encode_workspace_layout(uint64_t n, uint64_t total_line
     L.rec_size = o; o = al(o + 4 * (n + 1));
     L.partials = o; o = al(o + 8 * ((n + SCAN_TILE - 1) / SCAN_TILE + 1));
     L.err = o; o = al(o + 8);
-    L.retry = o; o = al(o + 4 * (n + 1));
     L.retry_count = o; o = al(o + 8);
     L.prim = o; o = al(o + (uint64_t)VCFC_PRIM * n);
     L.slots = o; o = al(o + total_line_bytes + total_line_bytes / 2 + 64 * (n + 1));
@@ -1364,9 +1364,9 @@ hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t s, hipEvent_t
     if ((e = hipGetLastError()) != hipSuccess) return e;
     {
         const uint64_t want = (a.n + K1_WAVES - 1) / K1_WAVES;
-        // one wave per queued row: a grid for every row, the waves past the
-        // queue's length exit at once (the hardware dispatcher balances rows
-        // of very different lengths better than a persistent grid)
+        // one wave per row, as the fast kernel (the hardware dispatcher
+        // balances rows of very different lengths better than a persistent
+        // grid); only flagged rows do work
         hipLaunchKernelGGL(k_encode_general, dim3((unsigned)want), dim3(64 * K1_WAVES), 0, s, a);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
