@@ -1152,8 +1152,12 @@ __global__ __launch_bounds__(256) void k_encode_fast(VcfcEncodeArgs a) {
     }
 }
 
-// General kernel: one wave per row; only the rows the fast kernel flagged
-// (VCFCD_RETRY) do work, the other waves exit at once.
+// General kernel: each wave reads the flags of GEN_ROWS consecutive rows
+// with one load and encodes the ones the fast kernel flagged (VCFCD_RETRY),
+// one after the other.  A small grid (n / 128 blocks) costs the headline
+// rows, which flag none, next to nothing; 32 rows per wave keep the waves of
+// the law-2 rows (75 % flagged) balanced.
+constexpr uint32_t GEN_ROWS = 32;   // rows per wave of the general kernel
 #ifndef VCFC_GEN_WPE
 #define VCFC_GEN_WPE 0
 #endif
@@ -1164,18 +1168,24 @@ __global__ __launch_bounds__(256) void k_encode_general(VcfcEncodeArgs a) {
 #endif
     __shared__ __attribute__((aligned(16))) uint8_t lds[K1_WAVES * RING_STRIDE];
     const uint32_t wave = vw::readfirst(threadIdx.x >> 6);
-    const uint64_t row = (uint64_t)blockIdx.x * K1_WAVES + wave;
-    if (row >= a.n || a.rec_size[row] != VCFCD_RETRY) return;
+    const uint64_t row0 = ((uint64_t)blockIdx.x * K1_WAVES + wave) * GEN_ROWS;
+    const uint32_t l = vw::lane_id();
+    const bool flagged = l < GEN_ROWS && row0 + l < a.n && a.rec_size[row0 + l] == VCFCD_RETRY;
+    uint64_t todo = vw::ballot(flagged);
+    while (todo) {
+        const uint64_t row = row0 + (uint64_t)__builtin_ctzll(todo);
+        todo &= todo - 1;
 #ifdef VCFC_COUNT_RETRIES   // test builds (tests/simt_emu): rows that took the general kernel
-    if (vw::lane_id() == 0) atomicAdd(a.retry_count, 1u);
+        if (l == 0) atomicAdd(a.retry_count, 1u);
 #endif
-    Ring r;
-    if (!row_setup(a, row, lds + wave * RING_STRIDE, r)) return;
-    uint32_t bytes = 0;
-    const uint32_t st = encode_general(a.buf + a.line_off[row], a.line_len[row], r, &bytes);
-    if (vw::lane_id() == 0) {
-        a.rec_size[row] = st == VCFCD_OK ? bytes : 0u;
-        if (st != VCFCD_OK) atomicMin((unsigned long long *)a.err, (unsigned long long)((row << 8) | st));
+        Ring r;
+        if (!row_setup(a, row, lds + wave * RING_STRIDE, r)) continue;
+        uint32_t bytes = 0;
+        const uint32_t st = encode_general(a.buf + a.line_off[row], a.line_len[row], r, &bytes);
+        if (l == 0) {
+            a.rec_size[row] = st == VCFCD_OK ? bytes : 0u;
+            if (st != VCFCD_OK) atomicMin((unsigned long long *)a.err, (unsigned long long)((row << 8) | st));
+        }
     }
 }
 
@@ -1363,11 +1373,10 @@ hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t s, hipEvent_t
     hipLaunchKernelGGL(k_encode_fast, dim3((unsigned)((a.n + K1_WAVES - 1) / K1_WAVES)), dim3(64 * K1_WAVES), 0, s, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     {
-        const uint64_t want = (a.n + K1_WAVES - 1) / K1_WAVES;
-        // one wave per row, as the fast kernel (the hardware dispatcher
-        // balances rows of very different lengths better than a persistent
-        // grid); only flagged rows do work
-        hipLaunchKernelGGL(k_encode_general, dim3((unsigned)want), dim3(64 * K1_WAVES), 0, s, a);
+        // GEN_ROWS rows per wave (see k_encode_general)
+        const uint64_t per_block = (uint64_t)K1_WAVES * GEN_ROWS;
+        hipLaunchKernelGGL(k_encode_general, dim3((unsigned)((a.n + per_block - 1) / per_block)), dim3(64 * K1_WAVES), 0,
+                           s, a);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (ev) (void)hipEventRecord(ev[2], s);
