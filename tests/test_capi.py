@@ -4,6 +4,7 @@ import ctypes
 import os
 import re
 import subprocess
+import sys
 
 import pytest
 
@@ -60,3 +61,18 @@ def test_no_gpu_fails_loudly(lib):
     h = ctypes.c_void_p()
     lib.vcfc_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
     assert lib.vcfc_ctx_create(0, ctypes.byref(h)) == 6  # VCFC_E_HIP
+
+
+def test_links_the_real_hip_runtime_with_no_undefined_symbols(lib):
+    """The library is linked against ROCm's libamdhip64 with -z defs (every
+    symbol resolved at build time) and records it by soname, so a PyTorch
+    process maps ONE HIP runtime (torch's copy has the same soname)."""
+    d = subprocess.run(["/opt/rocm/llvm/bin/llvm-readelf", "-d", LIB], capture_output=True, text=True).stdout
+    assert "[libamdhip64.so.7]" in d
+    r = subprocess.run(["ldd", "-r", LIB], capture_output=True, text=True)
+    assert "undefined symbol" not in r.stdout + r.stderr
+    code = ("import sys; sys.path.insert(0, %r); import torch, vcfc; vcfc.lib(); "
+            "print(sorted({l.split()[-1] for l in open('/proc/self/maps') if 'libamdhip64' in l}))"
+            % os.path.join(REPO, "vcf-compression_amd"))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300).stdout
+    assert out.count("libamdhip64") == 1, out
