@@ -55,6 +55,10 @@ def parse():
                          "(100k samples, one 100k-row batch of a 5M-row shard per GPU); decode = row f1; "
                          "query = row f2; ingest = row f4 (end-to-end file compress, configs[2]); "
                          "sparse = rows a7-a9 + f3 (sparsify, sparse-file query)")
+    ap.add_argument("--rows-total", type=int, default=None,
+                    help="--mode biobank: encode the rank's whole share of this many rows (5M = configs[3]) "
+                         "as back-to-back --rows batches, every record digested and sampled rows re-encoded "
+                         "by the CPU checker; a step is the whole shard")
     ap.add_argument("--sparse-rows", type=int, default=200_000, help="rows of the --mode sparse file")
     ap.add_argument("--ingest-rows", type=int, default=200_000, help="rows of the --mode ingest file")
     ap.add_argument("--query-frac", type=float, default=0.125, help="rows selected by the --mode query range")
@@ -537,8 +541,132 @@ def bench_sparse(args, torch, vcfc, workload):
         os.rmdir(tmp)
 
 
+def bench_biobank_shard(args):
+    """configs[3] as a whole shard: rank r of N encodes rows [R*r/N, R*(r+1)/N)
+    of the R = --rows-total row dataset (100k samples) as back-to-back
+    batches of --rows rows.  Every batch is generated in HBM (same prefixes,
+    a new genotype seed per batch; generation is outside the timed encode),
+    encoded, its records digested on the GPU (vcfc_record_hash_device) and
+    folded into a shard checksum, and two rows per batch are re-encoded by the
+    CPU checker (oracle) and compared byte for byte (SURVEY §7 hard part 7).
+    One step = the whole shard; `ms_per_step` and `value` use the summed
+    encode time of its batches (HIP events on the encode stream), max over
+    ranks; the wall time including generation and checks is reported too."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import vcfc
+    import workload
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    rehearsal = os.environ.get("VCFC_BENCH_REHEARSAL") == "1"
+    dev = torch.device("cuda:%d" % (0 if rehearsal else local))
+    torch.cuda.set_device(dev)
+    cdev = torch.device("cpu") if rehearsal else dev
+    if world > 1:
+        dist.init_process_group("gloo" if rehearsal else "nccl", **({} if rehearsal else {"device_id": dev}))
+    R, B, S = args.rows_total, args.rows, args.samples
+    lo, hi = R * rank // world, R * (rank + 1) // world
+    nb = (hi - lo + B - 1) // B
+    rows = workload.DeviceRows(torch, vcfc, B, S, args.law, seed=5000, device=dev, row0=lo)
+    ll = rows.line_len_host.astype(np.int64)
+    lb_prefix = np.concatenate([[0], np.cumsum(ll)])          # line bytes of the first k rows
+    gt_prefix = np.concatenate([[0], np.cumsum(rows.gt_row)])  # GT bytes of the first k rows
+    ws_bytes = vcfc.workspace_size(B, rows.line_bytes)
+    cap = vcfc.encode_bound(B, rows.line_bytes)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    out = torch.empty(cap, dtype=torch.uint8, device=dev)
+    rec = torch.empty(B + 1, dtype=torch.int64, device=dev)
+    err = torch.empty(1, dtype=torch.int64, device=dev)
+    dig = torch.empty(B, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import golden_io as G   # the CPU checker (oracle), verification only
+    rng = np.random.default_rng(rank)
+
+    def shard_pass(check):
+        enc_ms, gt, recb, checked = 0.0, 0, 0, 0
+        csum, cxor = 0, 0
+        for b in range(nb):
+            n = min(B, hi - lo - b * B)
+            rows.resynth(seed=7000 + (lo // B) + b)       # the batch's genotypes (input production, untimed)
+            torch.cuda.synchronize(dev)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            vcfc.encode_rows_device(rows.buf.data_ptr(), rows.line_off.data_ptr(), rows.line_len.data_ptr(), n,
+                                    int(lb_prefix[n]), out.data_ptr(), cap, rec.data_ptr(), ws.data_ptr(), ws_bytes,
+                                    err.data_ptr(), stream)
+            e1.record()
+            torch.cuda.synchronize(dev)
+            enc_ms += e0.elapsed_time(e1)
+            e = int(err.cpu().numpy().view(np.uint64)[0])
+            if e != vcfc.NO_ERROR:
+                raise RuntimeError("batch %d: row error %x" % (b, e))
+            gt += int(gt_prefix[n])
+            recb += int(rec[n].item())
+            if not check:
+                continue
+            vcfc.record_hash_device(out.data_ptr(), rec.data_ptr(), n, dig.data_ptr(), stream)
+            d = dig[:n].cpu().numpy().view(np.uint64)
+            csum = (csum + int(d.sum(dtype=np.uint64))) & ((1 << 64) - 1)
+            cxor ^= int(np.bitwise_xor.reduce(d))
+            for i in rng.integers(0, n, 2):
+                line = rows.host_lines([int(i)])[0]
+                got = out[int(rec[i].item()):int(rec[i + 1].item())].cpu().numpy().tobytes()
+                st, want = G.oracle_encode_line(line)
+                if st != 0 or got != want or G.oracle_hash64(want) != int(d[i]):
+                    raise RuntimeError("batch %d row %d differs from the CPU checker" % (b, int(i)))
+                checked += 1
+        return enc_ms, gt, recb, checked, (csum, cxor)
+
+    for _ in range(args.warmup):
+        shard_pass(False)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    enc_ms, gt, recb, checked, ck = 0.0, 0, 0, 0, None
+    for _ in range(args.steps):
+        m, gt, recb, c, k = shard_pass(True)
+        enc_ms += m
+        checked += c
+        if ck is not None and k != ck:
+            raise RuntimeError("shard checksum changed between passes")
+        ck = k
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    t = torch.tensor([enc_ms / args.steps, wall / args.steps], dtype=torch.float64, device=cdev)
+    g = torch.tensor([gt], dtype=torch.int64, device=cdev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(g)
+    ms, wall_s = float(t[0].item()), float(t[1].item())
+    gt_all = int(g.item())
+    res = {"metric": "input GT bytes/sec encoded, 100k-sample x 5M-variant VCF, row-sharded",
+           "value": round(gt_all / (ms * 1e-3) / 1e9, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "strong",
+           "vs_baseline": None, "dtype": "u8", "data": "synthetic (generated in HBM, batch by batch)",
+           "config": {"workload": "%s %d samples x %d variants, whole shard per GPU: %d-row batches back to back "
+                                  "(BASELINE configs[3])" % (law_name(args.law), S, R, B),
+                      "rows_total": R, "rows_per_gpu": hi - lo, "batches_per_gpu": nb, "gt_bytes_total": gt_all,
+                      "record_bytes_rank0": recb, "parallelism": "row shards x%d" % world},
+           "timing": "ms_per_step = summed HIP-event encode time of the shard's batches (generation and checks "
+                     "excluded), max over ranks; wall_s_per_step includes them",
+           "wall_s_per_step": round(wall_s, 3),
+           "verification": {"records_digested_per_pass": hi - lo, "rows_reencoded_by_cpu_checker": checked,
+                            "shard_checksum_rank0": "%016x:%016x" % ck}}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.mode == "biobank" and args.rows_total:
+        return bench_biobank_shard(args)
     if args.mode not in ("encode", "biobank"):
         import torch
         import vcfc

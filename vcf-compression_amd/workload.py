@@ -132,19 +132,28 @@ class DeviceRows:
         self.total_bytes = total
         self.line_bytes = int(line_len.astype(np.int64).sum())
         # bytes after the TAB following FORMAT, incl. '\n'
-        self.gt_bytes = 4 * samples * n if gt_len is None else int(np.asarray(gt_len).sum())
+        self.gt_row = np.full(n, 4 * samples, dtype=np.int64) if gt_len is None else np.asarray(gt_len, dtype=np.int64)
+        self.gt_bytes = int(self.gt_row.sum())
         self.buf = torch.empty(total + 64, dtype=torch.uint8, device=dev)
         self.line_off = torch.from_numpy(line_off).to(dev)
         self.line_len = torch.from_numpy(line_len).to(dev)
         d_prefix = torch.from_numpy(np.frombuffer(blob, dtype=np.uint8).copy()).to(dev)
         d_poff = torch.from_numpy(poff).to(dev)
         d_af = torch.from_numpy(af).to(dev) if af is not None else None
-        s = torch.cuda.current_stream(dev)
-        vcfc.synth_rows_device(self.buf.data_ptr(), self.line_off.data_ptr(), n, d_prefix.data_ptr(),
-                               d_poff.data_ptr(), d_af.data_ptr() if d_af is not None else None,
-                               samples, law, seed, s.cuda_stream)
+        self._torch, self._vcfc, self._dev = torch, vcfc, dev
+        self._pre = (d_prefix, d_poff, d_af)
+        self.resynth(seed)
         torch.cuda.synchronize(dev)
-        del d_prefix, d_poff, d_af
+        self.line_len_host = line_len
+
+    def resynth(self, seed, stream=None):
+        """Regenerate the genotype columns with another seed (same prefixes
+        and line layout): a new batch of the same shape, made in HBM."""
+        d_prefix, d_poff, d_af = self._pre
+        s = stream if stream is not None else self._torch.cuda.current_stream(self._dev).cuda_stream
+        self._vcfc.synth_rows_device(self.buf.data_ptr(), self.line_off.data_ptr(), self.n, d_prefix.data_ptr(),
+                                     d_poff.data_ptr(), d_af.data_ptr() if d_af is not None else None,
+                                     self.samples, self.law, seed, s)
 
     def host_lines(self, rows):
         """bytes of the given rows (for oracle checks)."""
