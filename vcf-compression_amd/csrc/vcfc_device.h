@@ -36,6 +36,7 @@ struct VcfcEncodeArgs {
     uint8_t *prim;             // per-row primary staging: record bytes [0, VCFC_PRIM) at prim + VCFC_PRIM * row
     uint8_t *slots;            // per-row overflow slots: record bytes [VCFC_PRIM, ...) at slots + slot_off[row]
     uint64_t slots_cap;
+    uint64_t *dbg;             // diagnostic builds only (VCFC_ROW_TIMES): per-row {start, end} wall clock; else null
 };
 
 // Record staging: the first VCFC_PRIM bytes of every record go to a dense
@@ -45,7 +46,7 @@ struct VcfcEncodeArgs {
 #define VCFC_PRIM 1024u
 
 struct VcfcWorkspaceLayout {
-    uint64_t slot_off, rec_size, partials, err, retry_count, prim, slots, total;
+    uint64_t slot_off, rec_size, partials, err, retry_count, prim, slots, dbg, total;
 };
 
 // Bytes of per-row staging for a line of `len` bytes: covers the worst-case
@@ -71,7 +72,8 @@ inline void vcfc_encode_args_workspace(VcfcEncodeArgs &a, uint8_t *ws, const Vcf
     a.retry_count = reinterpret_cast<uint32_t *>(ws + L.retry_count);
     a.prim = ws + L.prim;
     a.slots = ws + L.slots;
-    a.slots_cap = L.total - L.slots;
+    a.slots_cap = L.dbg - L.slots;
+    a.dbg = L.dbg < L.total ? reinterpret_cast<uint64_t *>(ws + L.dbg) : nullptr;
 }
 
 // Enqueue the whole encode on `stream` (no host synchronisation, capturable).

@@ -1140,10 +1140,16 @@ __global__ __launch_bounds__(256) void k_encode_fast(VcfcEncodeArgs a) {
     const uint32_t wave = vw::readfirst(threadIdx.x >> 6);   // wave-uniform: scalar row/len/loop control
     const uint64_t row = (uint64_t)blockIdx.x * K1_WAVES + wave;
     if (row >= a.n) return;
+#ifdef VCFC_ROW_TIMES
+    const uint64_t t_start = wall_clock64();
+#endif
     Ring r;
     if (!row_setup(a, row, lds + wave * RING_STRIDE, r)) return;
     uint32_t bytes = 0;
     const bool ok = encode_fast(a.buf + a.line_off[row], a.line_len[row], r, &bytes);
+#ifdef VCFC_ROW_TIMES
+    if (vw::lane_id() == 0) { a.dbg[2 * row] = t_start; a.dbg[2 * row + 1] = wall_clock64(); }
+#endif
     if (vw::lane_id() == 0) {
         // not the fast shape: the general kernel's wave for this row takes
         // it (a flag per row, no shared queue: 750k rows appending to one
@@ -1357,6 +1363,10 @@ VcfcWorkspaceLayout vcfc_encode_workspace_layout(uint64_t n, uint64_t total_line
     L.retry_count = o; o = al(o + 8);
     L.prim = o; o = al(o + (uint64_t)VCFC_PRIM * n);
     L.slots = o; o = al(o + total_line_bytes + total_line_bytes / 2 + 64 * (n + 1));
+    L.dbg = o;
+#ifdef VCFC_ROW_TIMES
+    o += 16 * n;
+#endif
     L.total = o;
     return L;
 }
