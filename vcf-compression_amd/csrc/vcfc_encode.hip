@@ -216,6 +216,7 @@ struct FastState {
     int32_t gt0;        // line offset of the first sample token (-1: not found yet)
     uint32_t T, phi;    // token count, gt0's byte phase mod 4
     uint32_t pcls, prs; // class / run start(+1) of the previous token
+    uint32_t esc;       // the last genotype chunk held an escape: test the escape shape first
 };
 
 // Prefix phase for chunk c: 0 = no sample yet, 1 = first sample starts in
@@ -537,6 +538,21 @@ __device__ __forceinline__ void clean8(const uint32_t (&d)[TPL8], int32_t t0, in
     ring_flush(r, false);
 }
 
+// classes of four 3-byte tokens (byte j = 0x90 + 2a + b, or 0x94 for an
+// escape) and their escape mask (byte j = 0xFF for an escape)
+__device__ __forceinline__ void esc_classes(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3, uint32_t &cb,
+                                            uint32_t &em) {
+    const uint32_t g0 = vw::perm(d1, d0, 0x06040200u), g1 = vw::perm(d3, d2, 0x06040200u);
+    const uint32_t A = vw::perm(g1, g0, 0x06040200u), B = vw::perm(g1, g0, 0x07050301u);
+    const uint32_t S = vw::perm(vw::perm(d3, d2, 0x05010C0Cu), vw::perm(d1, d0, 0x0C0C0501u), 0x07060100u);
+    // bytes: nonzero iff the token is not plain
+    const uint32_t y = (((A ^ 0x30303030u) | (B ^ 0x30303030u)) & 0xFEFEFEFEu) | (S ^ 0x7C7C7C7Cu);
+    const uint32_t n = (((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y) & 0x80808080u;   // 0x80 per nonzero byte
+    em = (n << 1) - (n >> 7);
+    const uint32_t c = (((A & 0x01010101u) << 1) + (B & 0x01010101u)) | 0x90909090u;
+    cb = (c & ~em) | (0x94949494u & em);
+}
+
 // Escape chunk: every slot in [0, T) is a 3-byte token followed by one TAB
 // (the last token by the line end) -- the shape of multi-allelic ("0|2"),
 // missing ("./.") and unphased ("0/1") genotypes.  Escapes get class 4 (class
@@ -550,20 +566,14 @@ __device__ __forceinline__ void clean8(const uint32_t (&d)[TPL8], int32_t t0, in
 // masked out of the starts and escapes.
 template <bool EDGE>
 __device__ __forceinline__ void esc8(const uint32_t (&d)[TPL8], int32_t t0, int32_t tf, FastState &f, Ring &r) {
-    constexpr uint32_t Z = 0x09307C30u;
-    uint32_t eL = 0, eH = 0;   // 0xFF in the byte of each escape slot
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        eL |= ((d[j] ^ Z) & 0x00FEFFFEu) ? (0xFFu << (8 * j)) : 0u;
-        eH |= ((d[j + 4] ^ Z) & 0x00FEFFFEu) ? (0xFFu << (8 * j)) : 0u;
-    }
-    // class bytes from the low bits of bytes 0 and 2 only (an escape's bytes
-    // must not carry into its neighbours), escapes then set to 0x94
-    uint32_t q[TPL8];
-#pragma unroll
-    for (int j = 0; j < (int)TPL8; j++) q[j] = (d[j] & 0x00010001u) | 0x00300030u;
-    uint32_t cbL = (class_bytes(q[0], q[1], q[2], q[3]) & ~eL) | (0x94949494u & eL);
-    uint32_t cbH = (class_bytes(q[4], q[5], q[6], q[7]) & ~eH) | (0x94949494u & eH);
+    // per 4 slots: gather bytes 0 (allele a), 2 (allele b) and 1 (separator)
+    // of the tokens into one word each; a token is plain ("a|b", a, b in
+    // {0,1}) iff a and b are '0'/'1' and the separator is '|'.  Class byte =
+    // 0x90 + 2a + b, escapes 0x94; an escape's bytes never reach a neighbour.
+    uint32_t cbL, cbH, eL, eH;   // eL/eH: 0xFF in the byte of each escape slot
+    esc_classes(d[0], d[1], d[2], d[3], cbL, eL);
+    esc_classes(d[4], d[5], d[6], d[7], cbH, eH);
+    f.esc = vw::ballot((eL | eH) != 0) != 0;
     if (f.pcls == CLS_NONE) {   // first chunk: see clean8 (an escape token 0 -> class 0: no lead byte)
         f.pcls = vw::readlane(cbL, 0) & 3u;
         f.prs = 1;
@@ -701,7 +711,16 @@ __device__ __forceinline__ bool gt_step8(const Chunk8 &cur, uint32_t C, FastStat
     const int32_t t0 = tf + (int32_t)(TPL8 * l);
     const bool pclean = f.pcls < CLS_ESC || f.pcls == CLS_NONE;
     if (tf + (int32_t)SLOTS8 < (int32_t)T) {
-        // interior chunk: every slot a token, none of them the last
+        // interior chunk: every slot a token, none of them the last.  After
+        // a chunk with escapes the next one most likely has some too (the
+        // random_vcf law: ~20 per chunk): test the escape shape alone.
+        if (f.esc) {
+            if (vw::ballot(shape3<false>(d, t0, T)) == 0) {
+                esc8<false>(d, t0, tf, f, r);
+                return true;
+            }
+            return false;
+        }
         const uint32_t o = ((d[0] ^ Z) | (d[1] ^ Z)) | ((d[2] ^ Z) | (d[3] ^ Z)) |
                            ((d[4] ^ Z) | (d[5] ^ Z)) | ((d[6] ^ Z) | (d[7] ^ Z));
         if (f.pcls == 0 && vw::ballot(o != 0) == 0) {
@@ -753,7 +772,7 @@ __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring
     const uint32_t nch = (span + CHUNK - 1) / CHUNK;
     const uint32_t lo16 = BPL * l;
     FastState f;
-    f.nf = 0; f.carryT = 1; f.gt0 = -1; f.T = 0; f.phi = 0; f.pcls = CLS_NONE; f.prs = 0;
+    f.nf = 0; f.carryT = 1; f.gt0 = -1; f.T = 0; f.phi = 0; f.pcls = CLS_NONE; f.prs = 0; f.esc = 0;
     r.wpos = 8;
     r.fpos = 0;
 
