@@ -341,6 +341,41 @@ __global__ __launch_bounds__(256) void k_dec_plan(VcfcDecodeArgs a) {
         plan_one<FULL>(a, g + (uint64_t)__builtin_ctzll(m) * G, sb);
 }
 
+// Light plan, one lane per record: only the header bits, the REQ length and
+// the final LF are read.  A record that passes is assumed simple with
+// REQ' = REQ (no NUL inside it) and exactly 9 TABs in it; k_dec_write checks
+// both while it copies REQ (and the sample section while it decodes it) and
+// reports code 4 where the assumption was wrong, so the batch is planned
+// again exactly (plan_one<true>).
+template <bool SEL>
+__global__ __launch_bounds__(256) void k_dec_plan_light(VcfcDecodeArgs a) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.n) return;
+    if (SEL && !a.select[i]) {
+        a.st[i] = DS_SKIP;
+        a.line_size[i] = 0;
+        return;
+    }
+    const uint64_t rs = a.rec_start[i], re = a.rec_start[i + 1];
+    bool simple = false;
+    uint64_t size = 0;
+    if (re - rs >= 10 && re - rs < (1ull << 31) && a.S > 0 && a.S < (1ull << 31)) {
+        const uint8_t *h = a.in + rs;
+        const uint32_t req = be30(h + 4);
+        if ((h[0] >> 6) == 3u && (h[4] >> 6) == 3u && req > 0 && 9 + (uint64_t)req < re - rs && a.in[re - 1] == '\n') {
+            simple = true;
+            size = req + 4 * a.S;
+        }
+    }
+    a.st[i] = simple ? DS_SIMPLE : DS_SEQ;
+    a.line_size[i] = simple && size <= 0xFFFFFFFFull ? (uint32_t)size : 0u;
+    if (!simple || size > 0xFFFFFFFFull) {
+        if (simple) a.st[i] = DS_SEQ;
+        const uint32_t q = atomicAdd(a.seq_count, 1u);
+        a.seq_list[q] = (uint32_t)i;
+    }
+}
+
 // Queued records, one lane each (grid-stride).
 __global__ __launch_bounds__(256) void k_dec_seq(VcfcDecodeArgs a) {
     const uint32_t cnt = *a.seq_count;
@@ -384,10 +419,19 @@ __device__ __forceinline__ void write_one(const VcfcDecodeArgs &a, uint64_t i, u
     sg.load(rs);
     const uint32_t req = ((sg.at(rs + 4) & 0x3Fu) << 24) | (sg.at(rs + 5) << 16) | (sg.at(rs + 6) << 8) | sg.at(rs + 7);
     const uint32_t slen = (uint32_t)(a.line_off[i + 1] - L0 - 4ull * S);   // REQ' = line - 4S
-    for (uint32_t b0 = 0; b0 < slen; b0 += 64) {
+    // copy REQ', and check what a light plan assumed: 9 TABs in REQ, REQ'
+    // ends at REQ's first NUL (an exact plan made both true)
+    uint32_t tabs = 0, z = req;
+    for (uint32_t b0 = 0; b0 < req; b0 += 64) {
         sg.need(rs + 8 + b0);
-        if (b0 + l < slen) line[b0 + l] = (uint8_t)sg.at(rs + 8 + b0 + l);
+        const uint32_t k = b0 + l;
+        const uint32_t b = k < req ? sg.at(rs + 8 + k) : 0xFFu;
+        if (k < slen) line[k] = (uint8_t)b;
+        tabs += (uint32_t)vw::popc64(vw::ballot(b == '\t'));
+        const uint64_t zm = vw::ballot(b == 0);
+        if (zm && z == req) z = b0 + (uint32_t)__builtin_ctzll(zm);
     }
+    const bool req_bad = tabs != 9 || z != slen;
     uint8_t *tok = line + slen;
     // Token tiles of TB four-byte words "a|b\t".  Each item writes only its
     // word at its first token's slot in the LDS tile (W); a tile then fills
@@ -458,7 +502,7 @@ __device__ __forceinline__ void write_one(const VcfcDecodeArgs &a, uint64_t i, u
     if (j0 < S) tile_out(S - j0);
     // a light plan assumed this record simple: check it (tokens past S were
     // never stored; the line's bytes are rewritten by the exact rerun)
-    if ((st.bad || st.got != S) && l == 0)
+    if ((st.bad || st.got != S || req_bad) && l == 0)
         atomicMin((unsigned long long *)a.err, (unsigned long long)((i << 8) | 4u));
 }
 
@@ -667,12 +711,13 @@ hipError_t vcfc_decode_plan(const VcfcDecodeArgs &a, bool exact, hipStream_t s) 
     if (a.n == 0) return hipMemsetAsync(a.line_off, 0, 8, s);
     const uint64_t per_wave = a.select ? SEL_R : 1;
     const dim3 grid((unsigned)((a.n + DEC_WAVES * per_wave - 1) / (DEC_WAVES * per_wave))), block(64 * DEC_WAVES);
+    const dim3 lgrid((unsigned)((a.n + 255) / 256));
     if (a.select) {
         if (exact) hipLaunchKernelGGL((k_dec_plan<true, true>), grid, block, 0, s, a);
-        else hipLaunchKernelGGL((k_dec_plan<false, true>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL(k_dec_plan_light<true>, lgrid, dim3(256), 0, s, a);
     } else {
         if (exact) hipLaunchKernelGGL((k_dec_plan<true, false>), grid, block, 0, s, a);
-        else hipLaunchKernelGGL((k_dec_plan<false, false>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL(k_dec_plan_light<false>, lgrid, dim3(256), 0, s, a);
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const uint64_t want = (a.n + 255) / 256;
