@@ -506,8 +506,15 @@ __device__ __forceinline__ void write_one(const VcfcDecodeArgs &a, uint64_t i, u
         atomicMin((unsigned long long *)a.err, (unsigned long long)((i << 8) | 4u));
 }
 
+#ifndef VCFC_DEC_WPE
+#define VCFC_DEC_WPE 0
+#endif
 template <bool SEL>
+#if VCFC_DEC_WPE
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VCFC_DEC_WPE, VCFC_DEC_WPE))) void k_dec_write(VcfcDecodeArgs a, uint64_t first, uint64_t last) {
+#else
 __global__ __launch_bounds__(256) void k_dec_write(VcfcDecodeArgs a, uint64_t first, uint64_t last) {
+#endif
     __shared__ __attribute__((aligned(16))) uint8_t sbuf[DEC_WAVES * SBUF];
     __shared__ __attribute__((aligned(16))) uint32_t tbuf[DEC_WAVES * TB];
     const uint32_t wave = vw::readfirst(threadIdx.x >> 6);
