@@ -50,10 +50,12 @@ def parse():
                     help="rows in the CPU-baseline sample (default: about 1.2 GB of lines)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify-rows", type=int, default=64, help="rows checked against the CPU path")
-    ap.add_argument("--mode", choices=["encode", "biobank", "decode", "query", "ingest", "sparse"], default="encode",
+    ap.add_argument("--mode", choices=["encode", "biobank", "decode", "query", "ingest", "devfile", "sparse"],
+                    default="encode",
                     help="encode = the headline (BASELINE metric, configs[1]); biobank = configs[3] "
                          "(100k samples, one 100k-row batch of a 5M-row shard per GPU); decode = row f1; "
                          "query = row f2; ingest = row f4 (end-to-end file compress, configs[2]); "
+                         "devfile = compress() of the configs[1] file already in HBM (line index + encode); "
                          "sparse = rows a7-a9 + f3 (sparsify, sparse-file query)")
     ap.add_argument("--rows-total", type=int, default=None,
                     help="--mode biobank: encode the rank's whole share of this many rows (5M = configs[3]) "
@@ -453,6 +455,56 @@ def bench_ingest(args, torch, vcfc, workload):
         os.rmdir(tmp)
 
 
+def bench_devfile(args, torch, vcfc, workload):
+    """compress() of the configs[1] file with its bytes already in HBM
+    (vcfc_compress_device): the GPU line index ('\n' scan, data / '#' line
+    tables) and the encoder over the whole file, in chunks of whole lines, the
+    .vcfc bytes left in HBM -- "device-resident file bytes -> records", the
+    headline step plus finding the lines.  The output is checked byte for byte
+    on the GPU against header + the encoder's records of the same rows."""
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    n, S = args.rows, args.samples
+    rows, recs, rec, rec_bytes = encoded_shard(args, torch, vcfc, workload, dev)
+    header = sample_header(S)
+    H = len(header)
+    N = H + rows.total_bytes
+    d_file = torch.empty(N, dtype=torch.uint8, device=dev)
+    d_file[:H] = torch.frombuffer(bytearray(header), dtype=torch.uint8).to(dev)
+    d_file[H:] = rows.buf[:rows.total_bytes]
+    want_len = H + rec_bytes
+    cap = int(vcfc.lib().vcfc_compress_bound(N))
+    d_out = torch.empty(cap, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize(dev)   # the call runs on the context's own stream
+    ctx = vcfc.Context(0)
+    for _ in range(args.warmup):
+        st, k, _ = ctx.compress_device(d_file.data_ptr(), N, d_out.data_ptr(), cap)
+        assert st == 0 and k == want_len, (st, k, want_len)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ctx.compress_device(d_file.data_ptr(), N, d_out.data_ptr(), cap)
+    elapsed = time.perf_counter() - t0   # (the call is synchronous)
+    identical = bool(torch.equal(d_out[:H], d_file[:H])) and bool(torch.equal(d_out[H:want_len], recs[:rec_bytes]))
+    ctx.close()
+    ms = elapsed * 1e3 / args.steps
+    res = {"metric": "input GT bytes/sec, device-resident VCF file bytes -> .vcfc bytes (line index + encode)",
+           "value": round(rows.gt_bytes / (ms * 1e-3) / 1e9, 2), "unit": "GB/s", "n_gpus": 1,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+           "scaling": "replicas", "vs_baseline": None, "dtype": "u8",
+           "data": "synthetic (generated in HBM; header + data lines as one device buffer)",
+           "config": {"workload": "%s %d samples x %d variants, %.2f GB file in HBM (BASELINE configs[1])"
+                                  % (law_name(args.law), S, n, N / 1e9),
+                      "file_bytes": N, "output_bytes": want_len, "chunk": "3 GiB of whole lines"},
+           "roofline": {"kernel": "line index + encoder (whole step)", "bound": "hbm",
+                        "achieved": round((2 * N + want_len) / (ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round((2 * N + want_len) / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                        "traffic": None,
+                        "algorithmic_bytes_per_step": 2 * N + want_len,
+                        "note": "file bytes read twice (index scan, encoder) + output written"},
+           "output_identical_to_header_plus_records": identical}
+    print(json.dumps(res), flush=True)
+
+
 def bench_sparse(args, torch, vcfc, workload):
     """Rows a7-a9 + f3: `sparsify` of a .vcfc file (GPU plan + one pwritev
     per record) and `sparse-query` of the middle --query-frac of its rows
@@ -671,7 +723,8 @@ def main():
         import torch
         import vcfc
         import workload
-        fn = {"decode": bench_decode, "query": bench_query, "ingest": bench_ingest, "sparse": bench_sparse}[args.mode]
+        fn = {"decode": bench_decode, "query": bench_query, "ingest": bench_ingest, "sparse": bench_sparse,
+              "devfile": bench_devfile}[args.mode]
         return fn(args, torch, vcfc, workload)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

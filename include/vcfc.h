@@ -124,6 +124,20 @@ uint64_t vcfc_compress_bound(uint64_t in_bytes);
 int vcfc_compress_buffer(vcfc_ctx *ctx, const uint8_t *in, uint64_t n, uint8_t *out, uint64_t out_cap,
                          uint64_t *out_len, int64_t *err_line);
 
+/* compress() over VCF file bytes already resident in device memory (a
+ * pipeline stage that produced or received the file on the GPU): d_in[0, n)
+ * holds the file's bytes as read, with n > 0 and d_in[n - 1] == '\n' (append
+ * one to an unterminated last line: getline returns it, reference
+ * src/compress.cpp:218); else VCFC_E_ARG.  The line index and the encoder run
+ * on the context's GPU; the bytes compress() writes -- '#' lines verbatim in
+ * place, records of the data lines -- land at d_out[0, *out_len) (out_cap >=
+ * vcfc_compress_bound(n)).  Runs on the context's stream: complete the
+ * writes of d_in first.  Synchronous (the host reads the index counts and
+ * the '#' lines).  Statuses and *err_line as vcfc_compress_buffer; on a
+ * failing line d_out holds the output of the lines before it. */
+int vcfc_compress_device(vcfc_ctx *ctx, const uint8_t *d_in, uint64_t n, uint8_t *d_out, uint64_t out_cap,
+                         uint64_t *out_len, int64_t *err_line);
+
 /* One rank's share of a multi-GPU compress (SURVEY §8 e): compresses the
  * byte range [off, off + len) of in_path (whole lines: off at a line start,
  * off + len after a '\n' or at EOF) through the same pipeline and writes the

@@ -34,6 +34,8 @@ def lib():
         L.emu_compress.argtypes = [ctypes.c_char_p, u64, vp, u64, ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_int64),
                                    u64, ctypes.c_int, u64]
         L.emu_record_hash.argtypes = [vp, vp, u64, vp]
+        L.emu_compress_device.argtypes = [ctypes.c_char_p, u64, vp, u64, ctypes.POINTER(u64),
+                                          ctypes.POINTER(ctypes.c_int64), u64, u64]
         L.emu_synth.argtypes = [vp, vp, u64, vp, vp, vp, ctypes.c_uint32, ctypes.c_int, u64]
         _lib = L
     return _lib
@@ -141,6 +143,18 @@ def emu_compress(vcf, chunk=4096, read_threads=2, cap=None, max_chunk=0):
     el = ctypes.c_int64(-1)
     st = lib().emu_compress(vcf, len(vcf), out.ctypes.data, cap, ctypes.byref(n), ctypes.byref(el), chunk,
                             read_threads, max_chunk)
+    return st, out[:n.value].tobytes(), el.value
+
+
+def emu_compress_device(vcf, chunk=4096, cap=None, max_chunk=0):
+    """compress() of device-resident bytes (vcfc_ing::compress_device) on the
+    emulator: (status, bytes, err_line)."""
+    cap = cap or 2 * len(vcf) + 4096
+    out = np.zeros(cap, dtype=np.uint8)
+    n = ctypes.c_uint64(0)
+    el = ctypes.c_int64(-1)
+    st = lib().emu_compress_device(vcf, len(vcf), out.ctypes.data, cap, ctypes.byref(n), ctypes.byref(el), chunk,
+                                   max_chunk)
     return st, out[:n.value].tobytes(), el.value
 
 

@@ -160,6 +160,17 @@ extern "C" int emu_compress(const uint8_t *in, uint64_t n, uint8_t *out, uint64_
     return st;
 }
 
+// compress() of "device-resident" bytes (host memory on the emulator)
+// through vcfc_ing::compress_device, with small chunks.
+extern "C" int emu_compress_device(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len,
+                                   int64_t *err_line, uint64_t chunk, uint64_t max_chunk) {
+    HostIngestMemory M;
+    vcfc_ing::Config cfg;
+    cfg.chunk = chunk;
+    if (max_chunk) cfg.max_chunk = max_chunk;
+    return vcfc_ing::compress_device(in, n, out, cap, out_len, M, nullptr, cfg, err_line);
+}
+
 // Per-record digests (csrc/vcfc_check.hip) on the emulator.
 extern "C" int emu_record_hash(const uint8_t *recs, const uint64_t *rec_off, uint64_t n, uint64_t *out) {
     return (int)vcfc_record_hash(recs, rec_off, n, out, nullptr);

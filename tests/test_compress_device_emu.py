@@ -1,0 +1,108 @@
+"""Device-resident compress() (vcfc_compress_device, csrc/vcfc_ingest_driver.h
+compress_device: line index + encoder over file bytes already in device
+memory, output left there) on the CPU emulator, with chunks of a few KiB so
+chunk ends fall between lines everywhere, '#' lines interleave with records
+and long lines grow their chunk.  Checked against the reference's own
+compress outputs (tests/golden) and the oracle: bytes, statuses, error lines
+(reference src/compress.cpp:205-257)."""
+import random
+
+import pytest
+
+import emu_io as E
+import golden_io as G
+import test_ingest_emu as T
+
+OK, E_ARG = 0, 5
+
+
+def nl(vcf):
+    """The device entry takes whole lines: getline returns an unterminated
+    last line as if it ended with '\\n'."""
+    return vcf if not vcf or vcf.endswith(b"\n") else vcf + b"\n"
+
+
+def check(vcf, chunk, name=""):
+    vcf = nl(vcf)
+    st_o, want, el_o = G.oracle_compress(vcf)
+    st, got, el = E.emu_compress_device(vcf, chunk=chunk)
+    assert st == st_o, (name, chunk, st, st_o)
+    assert got == want, (name, chunk, len(got), len(want))
+    if st_o != OK:
+        assert el == el_o, (name, chunk, el, el_o)
+
+
+def test_reference_config1():
+    vcf = G.gz("random_100x10000.vcf.gz")
+    st, out, _ = E.emu_compress_device(vcf, chunk=1 << 20)
+    assert st == OK and out == G.gz("random_100x10000.vcfc.gz")
+    cut = 0
+    while vcf[cut:cut + 1] == b"#":
+        cut = vcf.index(b"\n", cut) + 1
+    for _ in range(600):
+        cut = vcf.index(b"\n", cut) + 1
+    check(vcf[:cut], 4096, "config1 prefix, 4 KiB chunks")
+
+
+def test_reference_edge_file_and_bad_header():
+    ec = G.edge_cases()
+    st, out, _ = E.emu_compress_device(nl(bytes.fromhex(ec["file"]["input"])), chunk=4096)
+    assert st == OK and out.hex() == ec["file"]["output"]
+    check(bytes.fromhex(ec["bad_header_file"]["input"]), 4096, "bad_header_file")
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_mixed_files_match_oracle(seed):
+    """'#' lines between data rows (the scratch-buffer placement), empty lines."""
+    rnd = random.Random(seed)
+    for samples in (1, 40, 300):
+        vcf = T.mixed_file(rnd, 60, samples)
+        for chunk in (1 << 12, 1 << 20):
+            check(vcf, chunk, "mixed S=%d" % samples)
+
+
+def test_errors_match_oracle():
+    rnd = random.Random(4)
+    base = T.mixed_file(rnd, 80, 50).split(b"\n")
+    for b in (b"1\t2\t3", b"1\t2\t3\t4\t5\t6\t7\t8", b"#CHROM\tPOS", b"#"):
+        for at in (2, 40, len(base) - 1):
+            lines = list(base)
+            lines.insert(at, b)
+            for chunk in (1 << 12, 1 << 16):
+                check(b"\n".join(lines), chunk, "bad %r at %d" % (b, at))
+
+
+def test_tiny_inputs_and_unterminated():
+    for vcf in (b"", b"\n", b"\n\n\n", b"##x\n", b"#\n", b"1\t2\t3\t4\t5\t6\t7\t8\t9\n", b"\r\n"):
+        check(vcf, 4096, repr(vcf))
+    st, out, _ = E.emu_compress_device(b"##x", chunk=4096)   # last byte not '\n'
+    assert st == E_ARG and out == b""
+
+
+@pytest.mark.parametrize("chunk", [4096, 8192])
+def test_line_longer_than_chunk(chunk):
+    rnd = random.Random(chunk)
+    check(T.long_line_file(rnd, 50, [2000, 5000, 1100, 9000]), chunk, "long lines")
+
+
+def test_line_longer_than_max_chunk():
+    rnd = random.Random(9)
+    lines = T.D.header(40).rstrip(b"\n").split(b"\n") + T.D.rows(rnd, 20, 40)
+    head = b"\n".join(lines) + b"\n"
+    vcf = head + b"\t".join([b"1", b"2", b"a", b"b", b"c", b"d", b"e", b"f", b"GT"] + [b"0|1"] * 5000) + b"\n"
+    st, out, _ = E.emu_compress_device(vcf, chunk=4096, max_chunk=16384)
+    assert st == E_ARG
+    st_o, want, _ = G.oracle_compress(head)
+    assert st_o == OK and out == want
+
+
+def test_short_lines_overflow_the_segment_slot():
+    """More than 256 lines in a 16 KiB segment (short '##' lines, runs of
+    empty lines): k_nl_place scans those segments again."""
+    rnd = random.Random(11)
+    head = b"".join(b"##k%d=%d\n" % (i, rnd.randrange(10)) for i in range(4000))
+    rows = T.D.rows(rnd, 30, 20)
+    body = b"\n".join(rows[:10]) + b"\n" + b"\n" * 6000 + b"\n".join(rows[10:]) + b"\n"
+    vcf = head + T.D.header(20) + body
+    for chunk in (1 << 14, 1 << 20):
+        check(vcf, chunk, "short lines")

@@ -5,7 +5,8 @@ The multi-chunk path runs on real HIP streams here: the input chunk is forced
 down to 4 KiB / 1 MiB / 16 MiB (vcfc_ctx_set_ingest_chunk), so reader
 threads, three pinned input slots, two device slots, the uploader stream and
 its events, partial lines carried across chunks and chunks grown around long
-lines all run on the GPU.  Outputs are checked byte for byte against the
+lines all run on the GPU.  Every case also runs through vcfc_compress_device
+(the same file bytes resident in device memory, chunked the same way).  Outputs are checked byte for byte against the
 reference's own compress outputs (tests/golden) and against the oracle; the
 300 MiB case against the device encoder's records of the same rows."""
 import os
@@ -45,9 +46,27 @@ def ctx(vcfc):
     c.close()
 
 
+def device_path(ctx, data):
+    """(status, bytes, err_line) from vcfc_compress_device: the file bytes
+    already in device memory (an unterminated last line gets its '\n', as
+    getline returns it), line index + encode on the GPU, output in HBM."""
+    import torch as T
+    import vcfc as V
+    if data and not data.endswith(b"\n"):
+        data = data + b"\n"
+    d_in = T.from_numpy(np.frombuffer(data, dtype=np.uint8).copy()).to("cuda:0") if data else \
+        T.empty(16, dtype=T.uint8, device="cuda:0")
+    cap = int(V.lib().vcfc_compress_bound(len(data)))
+    d_out = T.empty(cap, dtype=T.uint8, device="cuda:0")
+    T.cuda.synchronize()   # the call runs on the context's own stream
+    st, k, el = ctx.compress_device(d_in.data_ptr(), len(data), d_out.data_ptr(), cap)
+    return st, d_out[:k].cpu().numpy().tobytes(), el
+
+
 def both_paths(ctx, data, chunk):
-    """(status, bytes, err_line) from compress_buffer (memory source) and from
-    compress_file (fd source, pread by reader threads); they must agree."""
+    """(status, bytes, err_line) from compress_buffer (memory source), from
+    compress_file (fd source, pread by reader threads) and from
+    compress_device (device-resident bytes); they must agree."""
     ctx.set_ingest_chunk(chunk)
     try:
         st, out, el = ctx.compress_status(data)
@@ -61,6 +80,8 @@ def both_paths(ctx, data, chunk):
             st2 = lib().vcfc_compress_file(ctx._h, ip.encode(), op.encode(), ctypes.byref(line))
             out2 = open(op, "rb").read()
         assert (st2, out2, line.value) == (st, out, el), (chunk, st, st2, len(out), len(out2))
+        st3, out3, el3 = device_path(ctx, data)
+        assert (st3, out3, el3) == (st, out, el), (chunk, st, st3, len(out), len(out3))
         return st, out, el
     finally:
         ctx.set_ingest_chunk(0)

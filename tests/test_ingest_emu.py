@@ -141,3 +141,15 @@ def test_line_longer_than_max_chunk():
     assert st == E_ARG
     st_o, want, _ = G.oracle_compress(head)
     assert st_o == OK and want.startswith(out) and len(out) > 0
+
+
+def test_short_lines_overflow_the_segment_slot():
+    """More than 256 lines in a 16 KiB segment of the line index (short '##'
+    lines, runs of empty lines): those segments are scanned again."""
+    rnd = random.Random(11)
+    head = b"".join(b"##k%d=%d\n" % (i, rnd.randrange(10)) for i in range(4000))
+    rows = D.rows(rnd, 30, 20)
+    body = b"\n".join(rows[:10]) + b"\n" + b"\n" * 6000 + b"\n".join(rows[10:]) + b"\n"
+    vcf = head + D.header(20) + body
+    for chunk in (1 << 14, 1 << 20):
+        check(vcf, chunk, "short lines")

@@ -160,7 +160,7 @@ struct VcfcLineIndex {
     uint64_t *counts;       // {lines, data lines, pass lines}
 };
 struct VcfcLineIndexLayout {
-    uint64_t seg_cnt, seg_base, nl, partials1, total1;               // phase 1 workspace
+    uint64_t seg_cnt, seg_base, nl, slot, partials1, total1;         // phase 1 workspace
     uint64_t is_data, is_pass, data_rank, pass_rank, partials2, total2;   // phase 2 workspace
 };
 VcfcLineIndexLayout vcfc_line_index_layout(uint64_t chunk_bytes, uint64_t n_lines);

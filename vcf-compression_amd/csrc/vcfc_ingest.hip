@@ -11,10 +11,14 @@
 //                of data lines before it (where it sits in the output);
 // empty lines are skipped (compress.cpp:219-221) but still counted.
 //
-//   k_nl_count    one wave per 16 KiB segment: '\n' count
+//   k_nl_scan     one wave per 16 KiB segment, the only pass over the bytes:
+//                 '\n' count, and the first NL_SLOT positions in order into
+//                 the segment's slot (per-lane masks, a wave prefix sum of
+//                 their popcounts)
 //   scan          segment bases (the encoder's exclusive scan)
-//   k_nl_emit     one wave per segment: '\n' positions in order (ballot-free:
-//                 per-lane masks, a wave prefix sum of their popcounts)
+//   k_nl_place    one wave per segment: its positions from the slot to their
+//                 place; a segment with more than NL_SLOT lines (average
+//                 line < 64 bytes: header lines) scans its bytes again
 //   k_line_kind   one lane per line: data / pass flags
 //   scan x2       data and pass ranks
 //   k_line_place  one lane per line: scatter into the output arrays
@@ -27,6 +31,7 @@ namespace {
 constexpr uint32_t SEG = 16384;          // bytes per wave
 constexpr uint32_t WIN = 1024;           // bytes per wave step (16 per lane)
 constexpr uint32_t IX_WAVES = 4;
+constexpr uint32_t NL_SLOT = 256;        // '\n' positions kept per segment by k_nl_scan
 
 // bit j: byte j of x is '\n' (exact per byte)
 __device__ __forceinline__ uint32_t nl_bits(uint32_t x) {
@@ -46,34 +51,46 @@ __device__ __forceinline__ uint32_t nl_mask16(const uint8_t *buf, uint64_t n, ui
     return m;
 }
 
-__global__ __launch_bounds__(256) void k_nl_count(const uint8_t *buf, uint64_t n, uint64_t n_seg, uint32_t *seg_cnt) {
-    const uint64_t seg = (uint64_t)blockIdx.x * IX_WAVES + vw::readfirst(threadIdx.x >> 6);
-    if (seg >= n_seg) return;
-    const uint32_t l = vw::lane_id();
-    uint32_t c = 0;
-    for (uint32_t w = 0; w < SEG; w += WIN) c += __builtin_popcount(nl_mask16(buf, n, seg * SEG + w + 16 * l));
-    c = vw::scan_add(c);
-    if (l == 63) seg_cnt[seg] = c;
+// positions of the '\n' bytes of one 1 KiB window (lane l: bytes [p, p + 16))
+// at out[o0 + rank] for ranks below `lim`; returns the window's count
+__device__ __forceinline__ uint32_t nl_window(const uint8_t *buf, uint64_t n, uint64_t p, uint32_t *out, uint64_t o0,
+                                              uint64_t lim) {
+    uint32_t m = nl_mask16(buf, n, p);
+    const uint32_t c = __builtin_popcount(m);
+    const uint32_t inc = vw::scan_add(c);
+    uint64_t o = o0 + inc - c;
+    while (m && o < lim) {
+        out[o++] = (uint32_t)(p + __builtin_ctz(m));
+        m &= m - 1;
+    }
+    return vw::readlane(inc, 63);
 }
 
-__global__ __launch_bounds__(256) void k_nl_emit(const uint8_t *buf, uint64_t n, uint64_t n_seg, const uint64_t *seg_base,
-                                                 uint32_t *nl) {
+__global__ __launch_bounds__(256) void k_nl_scan(const uint8_t *buf, uint64_t n, uint64_t n_seg, uint32_t *seg_cnt,
+                                                 uint32_t *slot) {
     const uint64_t seg = (uint64_t)blockIdx.x * IX_WAVES + vw::readfirst(threadIdx.x >> 6);
     if (seg >= n_seg) return;
     const uint32_t l = vw::lane_id();
-    uint64_t base = seg_base[seg];
-    for (uint32_t w = 0; w < SEG; w += WIN) {
-        const uint64_t p = seg * SEG + w + 16 * l;
-        uint32_t m = nl_mask16(buf, n, p);
-        const uint32_t c = __builtin_popcount(m);
-        const uint32_t inc = vw::scan_add(c);
-        uint64_t o = base + inc - c;
-        while (m) {
-            nl[o++] = (uint32_t)(p + __builtin_ctz(m));
-            m &= m - 1;
-        }
-        base += vw::readlane(inc, 63);
+    uint32_t *sl = slot + seg * NL_SLOT;
+    uint32_t c = 0;
+    for (uint32_t w = 0; w < SEG; w += WIN) c += nl_window(buf, n, seg * SEG + w + 16 * l, sl, c, NL_SLOT);
+    if (l == 0) seg_cnt[seg] = c;
+}
+
+__global__ __launch_bounds__(256) void k_nl_place(const uint8_t *buf, uint64_t n, uint64_t n_seg, const uint32_t *seg_cnt,
+                                                  const uint32_t *slot, const uint64_t *seg_base, uint32_t *nl) {
+    const uint64_t seg = (uint64_t)blockIdx.x * IX_WAVES + vw::readfirst(threadIdx.x >> 6);
+    if (seg >= n_seg) return;
+    const uint32_t l = vw::lane_id();
+    const uint32_t c = seg_cnt[seg];
+    uint32_t *dst = nl + seg_base[seg];
+    if (c <= NL_SLOT) {
+        const uint32_t *sl = slot + seg * NL_SLOT;
+        for (uint32_t k = l; k < c; k += 64) dst[k] = sl[k];
+        return;
     }
+    uint32_t o = 0;   // more lines than the slot holds: scan the segment again
+    for (uint32_t w = 0; w < SEG; w += WIN) o += nl_window(buf, n, seg * SEG + w + 16 * l, dst, o, ~0ull);
 }
 
 __global__ __launch_bounds__(256) void k_line_kind(const uint8_t *buf, const uint32_t *nl, uint64_t n_lines,
@@ -120,6 +137,7 @@ VcfcLineIndexLayout vcfc_line_index_layout(uint64_t chunk_bytes, uint64_t n_line
     L.seg_cnt = o; o = al(o + 4 * seg);
     L.seg_base = o; o = al(o + 8 * (seg + 1));
     L.nl = o; o = al(o + 4 * lines);
+    L.slot = o; o = al(o + 4ull * NL_SLOT * seg);
     L.partials1 = o; o = al(o + 8 * ((seg + 4095) / 4096 + 1));
     L.total1 = o;
     o = 0;
@@ -143,15 +161,16 @@ hipError_t vcfc_line_index(const uint8_t *buf, uint64_t n, uint8_t *ws, const Vc
     uint32_t *seg_cnt = reinterpret_cast<uint32_t *>(ws + L.seg_cnt);
     uint64_t *seg_base = reinterpret_cast<uint64_t *>(ws + L.seg_base);
     uint32_t *nl = reinterpret_cast<uint32_t *>(ws + L.nl);
+    uint32_t *slot = reinterpret_cast<uint32_t *>(ws + L.slot);
     uint64_t *partials = reinterpret_cast<uint64_t *>(ws + L.partials1);
     hipError_t e;
     if (n == 0) return hipMemsetAsync(x.counts, 0, 24, s);
     const uint64_t n_seg = (n + SEG - 1) / SEG;
     const dim3 sg((unsigned)((n_seg + IX_WAVES - 1) / IX_WAVES)), blk(64 * IX_WAVES);
-    hipLaunchKernelGGL(k_nl_count, sg, blk, 0, s, buf, n, n_seg, seg_cnt);
+    hipLaunchKernelGGL(k_nl_scan, sg, blk, 0, s, buf, n, n_seg, seg_cnt, slot);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = vcfc_scan_u32(seg_cnt, n_seg, partials, seg_base, s)) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_nl_emit, sg, blk, 0, s, buf, n, n_seg, seg_base, nl);
+    hipLaunchKernelGGL(k_nl_place, sg, blk, 0, s, buf, n, n_seg, seg_cnt, slot, seg_base, nl);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     return hipMemcpyAsync(x.counts, seg_base + n_seg, 8, hipMemcpyDeviceToDevice, s);
 }

@@ -481,4 +481,217 @@ inline int compress_stream(Source &src, const Sink &sink, Memory &M, hipStream_t
     return finish(ST_OK);
 }
 
+// compress() over VCF file bytes already resident in device memory: d_in[0, N)
+// holds the file's bytes as read (N > 0, d_in[N - 1] == '\n'), the .vcfc bytes
+// go to d_out[0, *out_len).  The GPU stage of compress_stream without the
+// transfer stages: chunks of whole lines (up to cfg.chunk bytes, grown to
+// hold a longer line, up to cfg.max_chunk: the index's positions are 32-bit)
+// are line-indexed and encoded in place; a chunk whose '#' lines all precede
+// its data lines (every real VCF) is encoded straight behind them into
+// d_out, one with interleaved '#' lines through a scratch buffer.  The host
+// only reads the index counts, the '#' lines (checked: >= 8 terms, as the
+// writer path) and a window before each chunk end.
+inline int compress_device(const uint8_t *d_in, uint64_t N, uint8_t *d_out, uint64_t out_cap, uint64_t *out_len,
+                           Memory &M, hipStream_t s, const Config &cfg, int64_t *err_line) {
+    using namespace detail;
+    if (err_line) *err_line = -1;
+    *out_len = 0;
+    if (N == 0) return ST_OK;
+    const bool trace = getenv("VCFC_DEV_TRACE") != nullptr;
+    if (trace) fprintf(stderr, "compress_device: N=%llu chunk=%llu max=%llu\n", (unsigned long long)N,
+                       (unsigned long long)cfg.chunk, (unsigned long long)cfg.max_chunk);
+    if (cfg.chunk < 16 || cfg.chunk > cfg.max_chunk) return ST_E_ARG;
+    uint64_t *hsmall = static_cast<uint64_t *>(M.host(Memory::H_SMALL, 64));
+    uint64_t *d_small = static_cast<uint64_t *>(M.dev(Memory::D_SMALL, 64));
+    if (!hsmall || !d_small) return ST_E_HIP;
+    auto sync = [&]() { return hipStreamSynchronize(s) == hipSuccess; };
+    auto d2h = [&](void *dst, const void *src, uint64_t k) {
+        return hipMemcpyAsync(dst, src, k, hipMemcpyDeviceToHost, s) == hipSuccess;
+    };
+    {
+        uint8_t last = 0;
+        if (!d2h(&last, d_in + N - 1, 1) || !sync()) return ST_E_HIP;
+        if (last != '\n') {
+            if (trace) fprintf(stderr, "compress_device: last byte %u\n", last);
+            return ST_E_ARG;
+        }
+    }
+    uint64_t pos = 0, o = 0, line_base = 0;
+    constexpr uint64_t WIN = 1ull << 16;
+    std::vector<uint8_t> win;
+    while (pos < N) {
+        // ---- the chunk: whole lines [pos, pos + n) ----
+        uint64_t lim = cfg.chunk, n = 0;
+        for (;;) {
+            if (N - pos <= lim) { n = N - pos; break; }
+            // the last '\n' of [pos, pos + lim), scanning windows backwards
+            uint64_t hi = lim;
+            while (hi > 0 && !n) {
+                const uint64_t lo = hi > WIN ? hi - WIN : 0;
+                win.resize(hi - lo);
+                if (!d2h(win.data(), d_in + pos + lo, hi - lo) || !sync()) return ST_E_HIP;
+                const void *nl = memrchr(win.data(), '\n', hi - lo);
+                if (nl) n = lo + (uint64_t)(static_cast<const uint8_t *>(nl) - win.data()) + 1;
+                hi = lo;
+            }
+            if (n) break;
+            if (trace) fprintf(stderr, "compress_device: no line end in [%llu, +%llu)\n", (unsigned long long)pos,
+                               (unsigned long long)lim);
+            if (lim >= cfg.max_chunk) return ST_E_ARG;   // a line longer than max_chunk
+            lim = std::min<uint64_t>(2 * lim, cfg.max_chunk);
+        }
+        const uint8_t *d_c = d_in + pos;
+        if (trace) fprintf(stderr, "compress_device: chunk [%llu, +%llu)\n", (unsigned long long)pos, (unsigned long long)n);
+        // ---- line index (as compress_stream) ----
+        const VcfcLineIndexLayout L1 = vcfc_line_index_layout(n, 0);
+        uint8_t *d_ix1 = static_cast<uint8_t *>(M.dev(Memory::D_IX1, L1.total1));
+        if (!d_ix1) return ST_E_HIP;
+        VcfcLineIndex x;
+        x.counts = d_small;
+        if (vcfc_line_index(d_c, n, d_ix1, L1, x, s) != hipSuccess || !d2h(hsmall, d_small, 8) || !sync())
+            return ST_E_HIP;
+        const uint64_t n_lines = hsmall[0];
+        const VcfcLineIndexLayout L = vcfc_line_index_layout(n, n_lines);
+        uint8_t *d_ix2 = static_cast<uint8_t *>(M.dev(Memory::D_IX2, L.total2));
+        uint8_t *d_lines = static_cast<uint8_t *>(M.dev(Memory::D_LINES, 32 * (n_lines + 1)));
+        uint8_t *d_rec = static_cast<uint8_t *>(M.dev(Memory::D_REC, 20 * (n_lines + 1)));
+        if (!d_ix2 || !d_lines || !d_rec) return ST_E_HIP;
+        uint8_t *q = d_lines;
+        x.line_off = reinterpret_cast<uint64_t *>(q); q += 8 * (n_lines + 1);
+        x.pass_before = reinterpret_cast<uint64_t *>(q); q += 8 * (n_lines + 1);
+        x.line_len = reinterpret_cast<uint32_t *>(q); q += 4 * (n_lines + 1);
+        x.line_no = reinterpret_cast<uint32_t *>(q);
+        uint64_t *d_rec_off = reinterpret_cast<uint64_t *>(d_rec);
+        x.pass_off = reinterpret_cast<uint32_t *>(d_rec + 8 * (n_lines + 1));
+        x.pass_len = x.pass_off + (n_lines + 1);
+        x.pass_no = x.pass_len + (n_lines + 1);
+        if (vcfc_line_index_place(d_c, n_lines, d_ix1, d_ix2, L, x, s) != hipSuccess || !d2h(hsmall, d_small, 24) ||
+            !sync())
+            return ST_E_HIP;
+        const uint64_t n_data = hsmall[1], n_pass = hsmall[2];
+        // ---- '#' lines: to the host, checked in order ----
+        std::vector<PassLine> pass;
+        int64_t hdr_err = -1;
+        uint64_t hdr_before = 0, pass_bytes = 0;
+        bool interleaved = false;
+        if (n_pass) {
+            std::vector<uint32_t> po(n_pass), pl(n_pass), pn(n_pass);
+            std::vector<uint64_t> pb(n_pass);
+            if (!d2h(po.data(), x.pass_off, 4 * n_pass) || !d2h(pl.data(), x.pass_len, 4 * n_pass) ||
+                !d2h(pn.data(), x.pass_no, 4 * n_pass) || !d2h(pb.data(), x.pass_before, 8 * n_pass) || !sync())
+                return ST_E_HIP;
+            for (uint64_t k = 0; k < n_pass; k++) {
+                PassLine p;
+                p.before = pb[k];
+                p.no = pn[k];
+                p.text.resize(pl[k] + 1);
+                if (pl[k] && !d2h(p.text.data(), d_c + po[k], pl[k])) return ST_E_HIP;
+                p.text[pl[k]] = '\n';
+                pass.push_back(std::move(p));
+            }
+            if (!sync()) return ST_E_HIP;
+            for (uint64_t k = 0; k < n_pass; k++) {
+                const PassLine &p = pass[k];
+                const uint64_t len = p.text.size() - 1;
+                if (!(len >= 2 && p.text[1] == '#') && !header_ok(p.text.data(), len)) {
+                    hdr_err = p.no;
+                    hdr_before = p.before;
+                    pass.resize(k);
+                    break;
+                }
+            }
+            for (const PassLine &p : pass) {
+                pass_bytes += p.text.size();
+                interleaved = interleaved || p.before != 0;
+            }
+        }
+        // ---- encode the data lines: straight into d_out behind the '#'
+        // lines, or (interleaved) into a scratch buffer ----
+        uint64_t good = n_data;
+        int st = ST_OK;
+        int64_t bad_line = -1;
+        uint8_t *d_recs = nullptr;
+        // record offsets: only the few the placement needs come to the host
+        auto rec_at = [&](uint64_t k, uint64_t *v) {
+            *v = 0;
+            return !n_data || k == 0 || (d2h(v, d_rec_off + k, 8) && sync());
+        };
+        if (n_data) {
+            const VcfcWorkspaceLayout W = vcfc_encode_workspace_layout(n_data, n);
+            uint8_t *ws = static_cast<uint8_t *>(M.dev(Memory::D_ENC_WS, W.total));
+            uint64_t cap;
+            if (interleaved) {
+                cap = vcfc_record_bound(n_data, n) + 64;
+                d_recs = static_cast<uint8_t *>(M.dev(Memory::D_OUT, cap));
+            } else {
+                if (o + pass_bytes > out_cap) return ST_E_NOSPACE;
+                d_recs = d_out + o + pass_bytes;
+                cap = out_cap - o - pass_bytes;
+            }
+            if (!ws || !d_recs) return ST_E_HIP;
+            VcfcEncodeArgs a;
+            a.buf = d_c; a.line_off = x.line_off; a.line_len = x.line_len; a.n = n_data;
+            a.line_bytes_hint = n;
+            a.out = d_recs; a.out_cap = cap; a.rec_off = d_rec_off;
+            vcfc_encode_args_workspace(a, ws, W);
+            a.err = d_small + 4;
+            if (vcfc_encode_device(a, s) != hipSuccess || !d2h(hsmall + 4, d_small + 4, 8) || !sync())
+                return ST_E_HIP;
+            const uint64_t errw = hsmall[4];
+            if (errw != VCFCD_NO_ERROR) {
+                good = errw >> 8;
+                st = (int)(errw & 0xFF);
+                if (st == ST_E_NOSPACE) return ST_E_NOSPACE;
+                uint32_t ln = 0;
+                if (!d2h(&ln, x.line_no + good, 4) || !sync()) return ST_E_HIP;
+                bad_line = ln;
+            }
+        }
+        bool stop = false;
+        if (hdr_err >= 0 && (bad_line < 0 || hdr_err < bad_line)) {
+            good = hdr_before;
+            st = ST_E_HEADER;
+            bad_line = hdr_err;
+            stop = true;
+        } else if (bad_line >= 0) {
+            stop = true;
+            while (!pass.empty() && pass.back().before > good) pass.pop_back();   // '#' lines after the failing row
+        }
+        // ---- place the '#' lines (and, interleaved, the record runs) ----
+        uint64_t at = 0;   // records placed so far
+        for (const PassLine &p : pass) {
+            uint64_t upto;
+            if (!rec_at(std::min<uint64_t>(p.before, good), &upto)) return ST_E_HIP;
+            if (upto > at) {
+                if (o + upto - at > out_cap) return ST_E_NOSPACE;
+                if (interleaved && hipMemcpyAsync(d_out + o, d_recs + at, upto - at, hipMemcpyDeviceToDevice, s) != hipSuccess)
+                    return ST_E_HIP;
+                o += upto - at;
+                at = upto;
+            }
+            if (o + p.text.size() > out_cap) return ST_E_NOSPACE;
+            if (hipMemcpyAsync(d_out + o, p.text.data(), p.text.size(), hipMemcpyHostToDevice, s) != hipSuccess)
+                return ST_E_HIP;
+            o += p.text.size();
+        }
+        uint64_t rec_end;
+        if (!rec_at(good, &rec_end)) return ST_E_HIP;
+        if (rec_end > at) {
+            if (o + rec_end - at > out_cap) return ST_E_NOSPACE;
+            if (interleaved && hipMemcpyAsync(d_out + o, d_recs + at, rec_end - at, hipMemcpyDeviceToDevice, s) != hipSuccess)
+                return ST_E_HIP;
+            o += rec_end - at;
+        }
+        if (!sync()) return ST_E_HIP;   // the '#' line texts are host vectors
+        *out_len = o;
+        if (stop) {
+            if (err_line) *err_line = (int64_t)(line_base + (uint64_t)bad_line + 1);
+            return st;
+        }
+        line_base += n_lines;
+        pos += n;
+    }
+    return ST_OK;
+}
+
 }  // namespace vcfc_ing

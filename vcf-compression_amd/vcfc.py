@@ -36,7 +36,7 @@ EXPORTS = [
     "vcfc_decode_records_device", "vcfc_parse_query", "vcfc_query_buffer", "vcfc_query_file",
     "vcfc_query_match_device", "vcfc_decode_selected_device", "vcfc_sparse_query_file",
     "vcfc_sparsify_shard", "vcfc_ctx_set_ingest_chunk", "vcfc_record_hash_device",
-    "vcfc_compress_range",
+    "vcfc_compress_range", "vcfc_compress_device",
 ]
 
 
@@ -80,6 +80,7 @@ def lib():
     L.vcfc_compress_bound.restype = u64
     L.vcfc_compress_bound.argtypes = [u64]
     L.vcfc_compress_buffer.argtypes = [vp, vp, u64, vp, u64, ctypes.POINTER(u64), ctypes.POINTER(i64)]
+    L.vcfc_compress_device.argtypes = [vp, vp, u64, vp, u64, ctypes.POINTER(u64), ctypes.POINTER(i64)]
     L.vcfc_timer_create.argtypes = [ctypes.POINTER(vp)]
     L.vcfc_timer_destroy.argtypes = [vp]
     L.vcfc_timer_destroy.restype = None
@@ -199,6 +200,14 @@ class Context:
                                         ctypes.byref(n), ctypes.byref(line))
         raise_for(st, "line %d" % line.value)
         return out[:n.value].tobytes()
+
+    def compress_device(self, d_in, n, d_out, out_cap):
+        """compress() over file bytes in device memory (pointers): d_in[0, n)
+        -> d_out; returns (status, out_len, err_line) without raising."""
+        k = ctypes.c_uint64(0)
+        line = ctypes.c_int64(-1)
+        st = lib().vcfc_compress_device(self._h, d_in, n, d_out, out_cap, ctypes.byref(k), ctypes.byref(line))
+        return st, k.value, line.value
 
     def compress_status(self, data):
         """Like compress_buffer without raising: (status, bytes, err_line).
