@@ -160,13 +160,13 @@ struct VcfcLineIndex {
     uint64_t *counts;       // {lines, data lines, pass lines}
 };
 struct VcfcLineIndexLayout {
-    uint64_t seg_cnt, seg_base, nl, slot, partials1, total1;         // phase 1 workspace
-    uint64_t is_data, is_pass, data_rank, pass_rank, partials2, total2;   // phase 2 workspace
+    uint64_t seg_cnt, seg_base, slot, partials1, total1;             // phase 1 workspace
+    uint64_t nl, is_data, is_pass, data_rank, pass_rank, partials2, total2;   // phase 2 workspace
 };
 VcfcLineIndexLayout vcfc_line_index_layout(uint64_t chunk_bytes, uint64_t n_lines);
-// phase 1: '\n' positions of buf[0, n) (last byte '\n'); counts[0] = lines
+// phase 1: '\n' count of buf[0, n) (last byte '\n'); counts[0] = lines
 hipError_t vcfc_line_index(const uint8_t *buf, uint64_t n, uint8_t *ws, const VcfcLineIndexLayout &L,
                            const VcfcLineIndex &x, hipStream_t s);
-// phase 2 (n_lines = counts[0]): data / pass line arrays; counts[1], counts[2]
-hipError_t vcfc_line_index_place(const uint8_t *buf, uint64_t n_lines, const uint8_t *ws1, uint8_t *ws2,
+// phase 2 (n_lines = counts[0]): '\n' positions, data / pass line arrays; counts[1], counts[2]
+hipError_t vcfc_line_index_place(const uint8_t *buf, uint64_t n, uint64_t n_lines, const uint8_t *ws1, uint8_t *ws2,
                                  const VcfcLineIndexLayout &L, const VcfcLineIndex &x, hipStream_t s);

@@ -66,6 +66,14 @@ __device__ __forceinline__ uint32_t nl_window(const uint8_t *buf, uint64_t n, ui
     return vw::readlane(inc, 63);
 }
 
+// '\n' mask of a lane's 16 bytes already loaded
+__device__ __forceinline__ uint32_t nl_mask_v(uint4 v) {
+    return nl_bits(v.x) | nl_bits(v.y) << 4 | nl_bits(v.z) << 8 | nl_bits(v.w) << 12;
+}
+
+// One pass over the segment: all its loads are issued before the first
+// window is processed (16 x 16 B per lane in flight), except in the chunk's
+// last segment, whose bytes past n must not be read as 16-byte blocks.
 __global__ __launch_bounds__(256) void k_nl_scan(const uint8_t *buf, uint64_t n, uint64_t n_seg, uint32_t *seg_cnt,
                                                  uint32_t *slot) {
     const uint64_t seg = (uint64_t)blockIdx.x * IX_WAVES + vw::readfirst(threadIdx.x >> 6);
@@ -73,7 +81,28 @@ __global__ __launch_bounds__(256) void k_nl_scan(const uint8_t *buf, uint64_t n,
     const uint32_t l = vw::lane_id();
     uint32_t *sl = slot + seg * NL_SLOT;
     uint32_t c = 0;
-    for (uint32_t w = 0; w < SEG; w += WIN) c += nl_window(buf, n, seg * SEG + w + 16 * l, sl, c, NL_SLOT);
+    if ((seg + 1) * SEG > n) {
+        for (uint32_t w = 0; w < SEG; w += WIN) c += nl_window(buf, n, seg * SEG + w + 16 * l, sl, c, NL_SLOT);
+    } else {
+        constexpr uint32_t NW = SEG / WIN;
+        uint4 v[NW];
+        const uint4 *src = reinterpret_cast<const uint4 *>(buf + seg * SEG) + l;
+#pragma unroll
+        for (uint32_t k = 0; k < NW; k++) v[k] = src[k * (WIN / 16)];
+#pragma unroll
+        for (uint32_t k = 0; k < NW; k++) {
+            uint32_t m = nl_mask_v(v[k]);
+            const uint32_t cnt = __builtin_popcount(m);
+            const uint32_t inc = vw::scan_add(cnt);
+            uint32_t o = c + inc - cnt;
+            const uint32_t p = (uint32_t)(seg * SEG) + k * WIN + 16 * l;
+            while (m && o < NL_SLOT) {
+                sl[o++] = p + __builtin_ctz(m);
+                m &= m - 1;
+            }
+            c += vw::readlane(inc, 63);
+        }
+    }
     if (l == 0) seg_cnt[seg] = c;
 }
 
@@ -130,17 +159,16 @@ __global__ __launch_bounds__(256) void k_line_place(const uint32_t *nl, uint64_t
 // '\n'); phase 2 on the line count phase 1 found.
 VcfcLineIndexLayout vcfc_line_index_layout(uint64_t chunk_bytes, uint64_t n_lines) {
     auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
-    const uint64_t lines = chunk_bytes + 1;
     const uint64_t seg = (chunk_bytes + SEG - 1) / SEG + 1;
     VcfcLineIndexLayout L;
     uint64_t o = 0;
     L.seg_cnt = o; o = al(o + 4 * seg);
     L.seg_base = o; o = al(o + 8 * (seg + 1));
-    L.nl = o; o = al(o + 4 * lines);
     L.slot = o; o = al(o + 4ull * NL_SLOT * seg);
     L.partials1 = o; o = al(o + 8 * ((seg + 4095) / 4096 + 1));
     L.total1 = o;
     o = 0;
+    L.nl = o; o = al(o + 4 * (n_lines + 1));
     L.is_data = o; o = al(o + 4 * (n_lines + 1));
     L.is_pass = o; o = al(o + 4 * (n_lines + 1));
     L.data_rank = o; o = al(o + 8 * (n_lines + 1));
@@ -150,8 +178,8 @@ VcfcLineIndexLayout vcfc_line_index_layout(uint64_t chunk_bytes, uint64_t n_line
     return L;
 }
 
-// Phase 1: '\n' positions of buf[0, n) (n <= chunk_bytes of the layout; the
-// last byte must be '\n'); x.counts[0] = lines.  Phase 2 needs that count on
+// Phase 1: '\n' count of buf[0, n) (n <= chunk_bytes of the layout; the
+// last byte must be '\n') and the kept positions; x.counts[0] = lines.  Phase 2 needs that count on
 // the host (its grids), as the encoder needs the data line count.  The
 // output arrays of `x` hold up to n / 2 data lines (a data line has at least
 // one byte and its '\n') and n pass lines.
@@ -160,7 +188,6 @@ hipError_t vcfc_line_index(const uint8_t *buf, uint64_t n, uint8_t *ws, const Vc
     // ws: phase 1 workspace (L.total1 bytes)
     uint32_t *seg_cnt = reinterpret_cast<uint32_t *>(ws + L.seg_cnt);
     uint64_t *seg_base = reinterpret_cast<uint64_t *>(ws + L.seg_base);
-    uint32_t *nl = reinterpret_cast<uint32_t *>(ws + L.nl);
     uint32_t *slot = reinterpret_cast<uint32_t *>(ws + L.slot);
     uint64_t *partials = reinterpret_cast<uint64_t *>(ws + L.partials1);
     hipError_t e;
@@ -170,16 +197,18 @@ hipError_t vcfc_line_index(const uint8_t *buf, uint64_t n, uint8_t *ws, const Vc
     hipLaunchKernelGGL(k_nl_scan, sg, blk, 0, s, buf, n, n_seg, seg_cnt, slot);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = vcfc_scan_u32(seg_cnt, n_seg, partials, seg_base, s)) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_nl_place, sg, blk, 0, s, buf, n, n_seg, seg_cnt, slot, seg_base, nl);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
     return hipMemcpyAsync(x.counts, seg_base + n_seg, 8, hipMemcpyDeviceToDevice, s);
 }
 
-// Phase 2, once the host knows the line count (counts[0]); ws1 = phase 1's
+// Phase 2, once the host knows the line count (counts[0]): the '\n'
+// positions in order, then the data / pass tables; ws1 = phase 1's
 // workspace, ws2 = L.total2 bytes for vcfc_line_index_layout(chunk, n_lines).
-hipError_t vcfc_line_index_place(const uint8_t *buf, uint64_t n_lines, const uint8_t *ws1, uint8_t *ws2,
+hipError_t vcfc_line_index_place(const uint8_t *buf, uint64_t n, uint64_t n_lines, const uint8_t *ws1, uint8_t *ws2,
                                  const VcfcLineIndexLayout &L, const VcfcLineIndex &x, hipStream_t s) {
-    const uint32_t *nl = reinterpret_cast<const uint32_t *>(ws1 + L.nl);
+    const uint32_t *seg_cnt = reinterpret_cast<const uint32_t *>(ws1 + L.seg_cnt);
+    const uint64_t *seg_base = reinterpret_cast<const uint64_t *>(ws1 + L.seg_base);
+    const uint32_t *slot = reinterpret_cast<const uint32_t *>(ws1 + L.slot);
+    uint32_t *nl = reinterpret_cast<uint32_t *>(ws2 + L.nl);
     uint32_t *is_data = reinterpret_cast<uint32_t *>(ws2 + L.is_data);
     uint32_t *is_pass = reinterpret_cast<uint32_t *>(ws2 + L.is_pass);
     uint64_t *data_rank = reinterpret_cast<uint64_t *>(ws2 + L.data_rank);
@@ -187,6 +216,10 @@ hipError_t vcfc_line_index_place(const uint8_t *buf, uint64_t n_lines, const uin
     uint64_t *partials = reinterpret_cast<uint64_t *>(ws2 + L.partials2);
     hipError_t e;
     if (n_lines == 0) return hipMemsetAsync(x.counts + 1, 0, 16, s);
+    const uint64_t n_seg = (n + SEG - 1) / SEG;
+    hipLaunchKernelGGL(k_nl_place, dim3((unsigned)((n_seg + IX_WAVES - 1) / IX_WAVES)), dim3(64 * IX_WAVES), 0, s, buf,
+                       n, n_seg, seg_cnt, slot, seg_base, nl);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
     const dim3 g((unsigned)((n_lines + 255) / 256)), blk(256);
     hipLaunchKernelGGL(k_line_kind, g, blk, 0, s, buf, nl, n_lines, is_data, is_pass);
     if ((e = hipGetLastError()) != hipSuccess) return e;

@@ -373,7 +373,7 @@ inline int compress_stream(Source &src, const Sink &sink, Memory &M, hipStream_t
         x.pass_off = reinterpret_cast<uint32_t *>(d_rec + 8 * (max_data + 1));
         x.pass_len = x.pass_off + (max_data + 1);
         x.pass_no = x.pass_len + (max_data + 1);
-        if (vcfc_line_index_place(d_in, n_lines, d_ix1, d_ix2, L, x, s) != hipSuccess ||
+        if (vcfc_line_index_place(d_in, n, n_lines, d_ix1, d_ix2, L, x, s) != hipSuccess ||
             hipMemcpyAsync(hsmall, d_small, 24, hipMemcpyDeviceToHost, s) != hipSuccess || !sync())
             return finish(ST_E_HIP);
         const uint64_t n_data = hsmall[1], n_pass = hsmall[2];
@@ -565,7 +565,7 @@ inline int compress_device(const uint8_t *d_in, uint64_t N, uint8_t *d_out, uint
         x.pass_off = reinterpret_cast<uint32_t *>(d_rec + 8 * (n_lines + 1));
         x.pass_len = x.pass_off + (n_lines + 1);
         x.pass_no = x.pass_len + (n_lines + 1);
-        if (vcfc_line_index_place(d_c, n_lines, d_ix1, d_ix2, L, x, s) != hipSuccess || !d2h(hsmall, d_small, 24) ||
+        if (vcfc_line_index_place(d_c, n, n_lines, d_ix1, d_ix2, L, x, s) != hipSuccess || !d2h(hsmall, d_small, 24) ||
             !sync())
             return ST_E_HIP;
         const uint64_t n_data = hsmall[1], n_pass = hsmall[2];
