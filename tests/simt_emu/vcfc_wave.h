@@ -39,6 +39,16 @@ inline uint32_t scan_max(uint32_t v) {
     v = umax(v, dpp(0u, v, 0x143, 0xc, 0xf, false));
     return v;
 }
+inline uint32_t last_nz(uint32_t v, uint32_t t) { return v ? v : t; }
+inline uint32_t scan_last_nz(uint32_t v) {
+    v = last_nz(v, dpp(0u, v, 0x111, 0xf, 0xf, false));
+    v = last_nz(v, dpp(0u, v, 0x112, 0xf, 0xf, false));
+    v = last_nz(v, dpp(0u, v, 0x114, 0xf, 0xf, false));
+    v = last_nz(v, dpp(0u, v, 0x118, 0xf, 0xf, false));
+    v = last_nz(v, dpp(0u, v, 0x142, 0xa, 0xf, false));
+    v = last_nz(v, dpp(0u, v, 0x143, 0xc, 0xf, false));
+    return v;
+}
 inline uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t s) {
     return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * (s & 3)));
 }

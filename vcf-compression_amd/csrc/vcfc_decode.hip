@@ -457,10 +457,10 @@ __device__ __forceinline__ void write_one(const VcfcDecodeArgs &a, uint64_t i, u
             lastw = w[q] ? w[q] : lastw;
             w[q] = lastw;
         }
-        // word entering the lane: the last start in an earlier lane, else carry
-        const uint32_t src = vw::shr1z(vw::scan_max(lastw ? l + 1 : 0u));
-        const uint32_t inw = vw::shfl(lastw, src ? src - 1 : 0u);
-        const uint32_t enter = src ? inw : carry;
+        // word entering the lane: the last start in an earlier lane (words are
+        // never 0: byte 3 is TAB), else carry
+        const uint32_t inw = vw::shr1z(vw::scan_last_nz(lastw));
+        const uint32_t enter = inw ? inw : carry;
 #pragma unroll
         for (uint32_t q = 0; q < PL; q++) w[q] = w[q] ? w[q] : enter;
         const uint32_t t0 = j0 + PL * l;

@@ -81,6 +81,18 @@ __device__ __forceinline__ uint32_t scan_max(uint32_t v) {
     v = umax(v, __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false));
     return v;
 }
+// inclusive "last non-zero" scan: lane l gets the value of the highest lane
+// <= l whose v is non-zero (0 if none); DPP steps as scan_max
+__device__ __forceinline__ uint32_t last_nz(uint32_t v, uint32_t t) { return v ? v : t; }
+__device__ __forceinline__ uint32_t scan_last_nz(uint32_t v) {
+    v = last_nz(v, __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false));
+    v = last_nz(v, __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false));
+    v = last_nz(v, __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false));
+    v = last_nz(v, __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false));
+    v = last_nz(v, __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false));
+    v = last_nz(v, __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false));
+    return v;
+}
 // byte select: result byte i = byte sel[i] of (s0:s1) for sel 0..7, 0x0C -> 0x00
 __device__ __forceinline__ uint32_t perm(uint32_t s0, uint32_t s1, uint32_t sel) {
     return __builtin_amdgcn_perm(s0, s1, sel);
