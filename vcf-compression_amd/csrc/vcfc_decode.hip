@@ -52,6 +52,12 @@ constexpr int DL_OK = 0, DL_END = 1, DL_ERR = 2;
 __device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
 __device__ __forceinline__ uint32_t umin32(uint32_t a, uint32_t b) { return a < b ? a : b; }
 
+// bit i set <=> byte i of w is zero (exact)
+__device__ __forceinline__ uint32_t zero_bytes4(uint32_t w) {
+    const uint32_t t = ~(((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w | 0x7F7F7F7Fu);
+    return ((t >> 7) & 1u) | ((t >> 14) & 2u) | ((t >> 21) & 4u) | ((t >> 28) & 8u);
+}
+
 __device__ __forceinline__ uint32_t be30(const uint8_t *h) {
     return ((uint32_t)(h[0] & 0x3Fu) << 24) | ((uint32_t)h[1] << 16) | ((uint32_t)h[2] << 8) | h[3];
 }
@@ -421,15 +427,29 @@ __device__ __forceinline__ void write_one(const VcfcDecodeArgs &a, uint64_t i, u
     const uint32_t slen = (uint32_t)(a.line_off[i + 1] - L0 - 4ull * S);   // REQ' = line - 4S
     // copy REQ', and check what a light plan assumed: 9 TABs in REQ, REQ'
     // ends at REQ's first NUL (an exact plan made both true)
+    // (4 bytes per lane, 256 per step: one step for REQs of the usual size)
     uint32_t tabs = 0, z = req;
-    for (uint32_t b0 = 0; b0 < req; b0 += 64) {
-        sg.need(rs + 8 + b0);
-        const uint32_t k = b0 + l;
-        const uint32_t b = k < req ? sg.at(rs + 8 + k) : 0xFFu;
-        if (k < slen) line[k] = (uint8_t)b;
-        tabs += (uint32_t)vw::popc64(vw::ballot(b == '\t'));
-        const uint64_t zm = vw::ballot(b == 0);
-        if (zm && z == req) z = b0 + (uint32_t)__builtin_ctzll(zm);
+    for (uint32_t b0 = 0; b0 < req; b0 += 256) {
+        sg.need(rs + 8 + b0, 256);
+        const uint32_t k = b0 + 4 * l;
+        uint32_t w = 0xFFFFFFFFu, vm = 0;   // vm: bytes of REQ among the four
+        if (k < req) {
+            __builtin_memcpy(&w, sg.lds + (rs + 8 + k - sg.cbase), 4);   // (unaligned ds_read_b32)
+            vm = req - k >= 4 ? 0xFu : (1u << (req - k)) - 1u;
+        }
+        const uint32_t tm = zero_bytes4(w ^ 0x09090909u) & vm, zmk = zero_bytes4(w) & vm;
+        if (k + 4 <= slen) {
+            __builtin_memcpy(line + k, &w, 4);
+        } else {
+            for (uint32_t i = 0; i < 3; i++)
+                if (k + i < slen) line[k + i] = (uint8_t)(w >> (8 * i));
+        }
+        tabs += vw::readlane(vw::scan_add((uint32_t)__builtin_popcount(tm)), 63);
+        const uint64_t zl = vw::ballot(zmk != 0);
+        if (zl && z == req) {
+            const uint32_t f = (uint32_t)__builtin_ctzll(zl);
+            z = b0 + 4 * f + (uint32_t)__builtin_ctz(vw::readlane(zmk, f));
+        }
     }
     const bool req_bad = tabs != 9 || z != slen;
     uint8_t *tok = line + slen;
