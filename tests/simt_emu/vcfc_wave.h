@@ -81,6 +81,7 @@ inline int popc64(uint64_t m) { return __builtin_popcountll(m); }
 inline int hibit64(uint64_t m) { return 63 - __builtin_clzll(m); }
 inline uint32_t mulhi(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }
 inline uint4 gload16(const void *base, uint32_t idx) { return ((const uint4 *)base)[idx]; }
+inline uint4 uload16(const void *p) { uint4 v; memcpy(&v, p, 16); return v; }
 inline uint32_t gload4(const void *base, uint32_t idx) { return ((const uint32_t *)base)[idx]; }
 inline void gstore16(void *base, uint64_t byte_off, uint4 v) { *(uint4 *)((uint8_t *)base + byte_off) = v; }
 inline void gstore16_nt(void *base, uint64_t byte_off, uint4 v) { gstore16(base, byte_off, v); }

@@ -1288,6 +1288,113 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t *__restrict__ pri
 }
 
 // ---------------------------------------------------------------------------
+// Output-ordered compaction (default): the output is cut into 4 KiB tiles;
+// a grid of waves strides over the tiles, and within a tile lane l writes the
+// 16-byte blocks l, l + 64, l + 128, l + 192, so every store instruction
+// covers 1 KiB of the output contiguously and every output line is written
+// once, by one wave.  A block's bytes come from the record holding its first
+// byte (an unaligned 16-B load from that record's staging), merged with the
+// overflow slot's first bytes where the block crosses record byte
+// VCFC_PRIM, and with the next record's first bytes where it crosses a
+// record end (records hold >= 26 bytes, so a block meets at most two).
+// k_tile_first gives each tile the row holding its first byte.
+constexpr uint32_t CT = 4096;   // output bytes per tile
+
+__global__ __launch_bounds__(256) void k_tile_first(const uint64_t *__restrict__ rec_off, uint64_t n, uint64_t out_cap,
+                                                    uint32_t *__restrict__ tile_first, uint64_t *err) {
+    const uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= n) return;
+    const uint64_t a = rec_off[r], b = rec_off[r + 1];
+    if (b > out_cap) atomicMin((unsigned long long *)err, (unsigned long long)((r << 8) | VCFCD_E_NOSPACE));
+    for (uint64_t t = (a + CT - 1) / CT; t * CT < b; t++) tile_first[t] = (uint32_t)r;
+}
+
+// bytes [0, s) of a, then b's first 16 - s bytes (0 < s < 16)
+__device__ __forceinline__ uint4 merge16(uint4 a, uint4 b, uint32_t s) {
+    const uint4 sh = realign16(make_uint4(0, 0, 0, 0), b, 16u - s);
+    auto m = [&](uint32_t d) {
+        return s >= 4 * d + 4 ? ~0u : s <= 4 * d ? 0u : (1u << (8 * (s - 4 * d))) - 1u;
+    };
+    const uint32_t m0 = m(0), m1 = m(1), m2 = m(2), m3 = m(3);
+    return make_uint4((a.x & m0) | (sh.x & ~m0), (a.y & m1) | (sh.y & ~m1), (a.z & m2) | (sh.z & ~m2),
+                      (a.w & m3) | (sh.w & ~m3));
+}
+
+__global__ __launch_bounds__(256) void k_compact_out(const uint8_t *__restrict__ prims,
+                                                     const uint8_t *__restrict__ slots,
+                                                     const uint64_t *__restrict__ slot_off,
+                                                     const uint64_t *__restrict__ rec_off, uint64_t n,
+                                                     const uint32_t *__restrict__ tile_first,
+                                                     uint8_t *__restrict__ out, uint64_t out_cap) {
+    const uint32_t l = vw::lane_id();
+    const uint64_t g = (uint64_t)blockIdx.x * 4 + vw::readfirst(threadIdx.x >> 6);
+    const uint64_t G = (uint64_t)gridDim.x * 4;
+    const uint64_t total = rec_off[n];
+    const uint64_t lim = total < out_cap ? total : out_cap;
+    const uint64_t ntile = (lim + CT - 1) / CT;
+    for (uint64_t t = g; t < ntile; t += G) {
+        const uint64_t o0 = t * CT;
+        const uint64_t r0 = tile_first[t];
+        // rows r0 .. r0 + 63: their starts (lane j holds row r0 + j); rows
+        // past n start "at infinity"
+        const uint64_t ro = r0 + l <= n ? rec_off[r0 + l] : ~0ull;
+        const uint64_t so = r0 + l < n ? slot_off[r0 + l] : 0;
+        // rows that start before the tile ends; a tile over more than 63
+        // rows (records of < 64 B on average) takes the rows in batches
+        uint64_t base = r0;   // row of lane 0's values
+        uint64_t rov = ro, sov = so;
+        // per block: the row holding its first byte (start, end, slot) and
+        // the row holding its last byte (a block meets at most two non-empty
+        // records; empty rows -- failed lines -- start where the next begins)
+        uint32_t idx[4], idx2[4];
+        uint64_t st[4], en[4], sl[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) { idx[k] = 0; idx2[k] = 0; st[k] = 0; en[k] = 0; sl[k] = 0; }
+        for (;;) {
+            const uint64_t bnd = vw::ballot(rov < o0 + CT);   // rows (of this batch) starting before the tile end
+            const uint32_t nr = (uint32_t)vw::popc64(bnd);    // a prefix of the lanes (starts are sorted)
+            const uint32_t nu = nr < 63 ? nr : 63;            // lane j + 1 holds row j's end
+            for (uint32_t j = 0; j < nu; j++) {
+                const uint64_t rj = ((uint64_t)vw::readlane((uint32_t)(rov >> 32), j) << 32) | vw::readlane((uint32_t)rov, j);
+                const uint64_t ej = ((uint64_t)vw::readlane((uint32_t)(rov >> 32), j + 1) << 32) | vw::readlane((uint32_t)rov, j + 1);
+                const uint64_t sj = ((uint64_t)vw::readlane((uint32_t)(sov >> 32), j) << 32) | vw::readlane((uint32_t)sov, j);
+                const uint32_t ij = (uint32_t)(base - r0) + j;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint64_t o = o0 + 16u * (l + 64u * k);
+                    if (o >= rj) { idx[k] = ij; st[k] = rj; en[k] = ej; sl[k] = sj; }
+                    if (o + 15 >= rj) idx2[k] = ij;
+                }
+            }
+            if (nr < 64) break;
+            // lane 63's row starts inside the tile too: next batch from row base + 63
+            base += 63;
+            rov = base + l <= n ? rec_off[base + l] : ~0ull;
+            sov = base + l < n ? slot_off[base + l] : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint64_t o = o0 + 16u * (l + 64u * k);
+            if (o >= lim) continue;
+            const uint64_t r = r0 + idx[k];
+            const uint64_t x = o - st[k];   // offset in the record
+            const uint8_t *prim = prims + (uint64_t)VCFC_PRIM * r;
+            const uint8_t *slot = slots + sl[k];
+            uint4 v = x + 16 <= VCFC_PRIM ? vw::uload16(prim + x) : x >= VCFC_PRIM ? vw::uload16(slot + (x - VCFC_PRIM)) : vw::uload16(prim + x);
+            if (x < VCFC_PRIM && x + 16 > VCFC_PRIM) v = merge16(v, vw::uload16(slot), (uint32_t)(VCFC_PRIM - x));
+            if (o + 16 > en[k] && en[k] < lim)   // the next non-empty record starts at en
+                v = merge16(v, vw::uload16(prims + (uint64_t)VCFC_PRIM * (r0 + idx2[k])), (uint32_t)(en[k] - o));
+            if (o + 16 <= lim) {
+                vw::gstore16(out, o, v);
+            } else {
+                const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+                for (uint32_t i = 0; o + i < lim; i++) out[o + i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Exclusive scan u32 -> u64 (n + 1 outputs).  MODE 0: identity, MODE 1:
 // vcfc_slot_bytes(len).  4096 items per 256-thread block.
 constexpr int SCAN_ITEMS = 16, SCAN_THREADS = 256, SCAN_TILE = SCAN_ITEMS * SCAN_THREADS;
@@ -1380,6 +1487,7 @@ VcfcWorkspaceLayout vcfc_encode_workspace_layout(uint64_t n, uint64_t total_line
     L.partials = o; o = al(o + 8 * ((n + SCAN_TILE - 1) / SCAN_TILE + 1));
     L.err = o; o = al(o + 8);
     L.retry_count = o; o = al(o + 8);
+    L.tile_first = o; o = al(o + 4 * (vcfc_record_bound(n, total_line_bytes) / CT + 2));
     L.prim = o; o = al(o + (uint64_t)VCFC_PRIM * n);
     L.slots = o; o = al(o + total_line_bytes + total_line_bytes / 2 + 64 * (n + 1));
     L.dbg = o;
@@ -1412,8 +1520,9 @@ hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t s, hipEvent_t
     e = launch_scan<0>(a.rec_size, a.n, a.partials, a.rec_off, s);
     if (e != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[3], s);
-    // records of rows longer than 64 KiB on average (biobank-wide rows) get a
-    // whole wave each
+#ifdef VCFC_ROW_COMPACT
+    // (A/B builds) row-ordered compaction: records of rows longer than 64 KiB
+    // on average (biobank-wide rows) get a whole wave each
 #ifndef VCFC_WIDE_ROW
 #define VCFC_WIDE_ROW (64ull << 10)
 #endif
@@ -1423,6 +1532,18 @@ hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t s, hipEvent_t
     else
         hipLaunchKernelGGL(k_compact<16>, dim3((unsigned)((a.n + 15) / 16)), dim3(256), 0, s, a.prim, a.slots,
                            a.slot_off, a.rec_off, a.n, a.out, a.out_cap, a.err);
+#else
+    hipLaunchKernelGGL(k_tile_first, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, s, a.rec_off, a.n, a.out_cap,
+                       a.tile_first, a.err);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    {
+        // a grid of 8 waves per SIMD striding over the tiles (uniform work)
+        const uint64_t tiles = vcfc_record_bound(a.n, a.line_bytes_hint) / CT + 1;
+        const uint64_t blocks = tiles < 8192 ? (tiles + 3) / 4 : 2048;
+        hipLaunchKernelGGL(k_compact_out, dim3((unsigned)blocks), dim3(256), 0, s, a.prim, a.slots, a.slot_off,
+                           a.rec_off, a.n, a.tile_first, a.out, a.out_cap);
+    }
+#endif
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[4], s);
     return hipSuccess;

@@ -132,6 +132,11 @@ __device__ __forceinline__ uint4 gload16(const void *base, uint32_t idx) {
     const v4u v = ((g_cv4u *)base)[idx];
     return make_uint4(v.x, v.y, v.z, v.w);
 }
+// 16 bytes at any byte address (global_load_dwordx4 takes unaligned addresses)
+__device__ __forceinline__ uint4 uload16(const void *p) {
+    const v4u v = *((g_cv4u *)((__attribute__((address_space(1))) const uint8_t *)p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
 __device__ __forceinline__ uint32_t gload4(const void *base, uint32_t idx) {
     return ((g_cu32 *)base)[idx];
 }
