@@ -1298,7 +1298,11 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t *__restrict__ pri
 // VCFC_PRIM, and with the next record's first bytes where it crosses a
 // record end (records hold >= 26 bytes, so a block meets at most two).
 // k_tile_first gives each tile the row holding its first byte.
-constexpr uint32_t CT = 4096;   // output bytes per tile
+#ifndef VCFC_CT_BLOCKS
+#define VCFC_CT_BLOCKS 4
+#endif
+constexpr uint32_t CTB = VCFC_CT_BLOCKS;   // 16-B blocks per lane per tile
+constexpr uint32_t CT = 1024 * CTB;        // output bytes per tile
 
 __global__ __launch_bounds__(256) void k_tile_first(const uint64_t *__restrict__ rec_off, uint64_t n, uint64_t out_cap,
                                                     uint32_t *__restrict__ tile_first, uint64_t *err) {
@@ -1346,10 +1350,10 @@ __global__ __launch_bounds__(256) void k_compact_out(const uint8_t *__restrict__
         // per block: the row holding its first byte (start, end, slot) and
         // the row holding its last byte (a block meets at most two non-empty
         // records; empty rows -- failed lines -- start where the next begins)
-        uint32_t idx[4], idx2[4];
-        uint64_t st[4], en[4], sl[4];
+        uint32_t idx[CTB], idx2[CTB];
+        uint64_t st[CTB], en[CTB], sl[CTB];
 #pragma unroll
-        for (int k = 0; k < 4; k++) { idx[k] = 0; idx2[k] = 0; st[k] = 0; en[k] = 0; sl[k] = 0; }
+        for (int k = 0; k < (int)CTB; k++) { idx[k] = 0; idx2[k] = 0; st[k] = 0; en[k] = 0; sl[k] = 0; }
         for (;;) {
             const uint64_t bnd = vw::ballot(rov < o0 + CT);   // rows (of this batch) starting before the tile end
             const uint32_t nr = (uint32_t)vw::popc64(bnd);    // a prefix of the lanes (starts are sorted)
@@ -1360,7 +1364,7 @@ __global__ __launch_bounds__(256) void k_compact_out(const uint8_t *__restrict__
                 const uint64_t sj = ((uint64_t)vw::readlane((uint32_t)(sov >> 32), j) << 32) | vw::readlane((uint32_t)sov, j);
                 const uint32_t ij = (uint32_t)(base - r0) + j;
 #pragma unroll
-                for (int k = 0; k < 4; k++) {
+                for (int k = 0; k < (int)CTB; k++) {
                     const uint64_t o = o0 + 16u * (l + 64u * k);
                     if (o >= rj) { idx[k] = ij; st[k] = rj; en[k] = ej; sl[k] = sj; }
                     if (o + 15 >= rj) idx2[k] = ij;
@@ -1373,7 +1377,7 @@ __global__ __launch_bounds__(256) void k_compact_out(const uint8_t *__restrict__
             sov = base + l < n ? slot_off[base + l] : 0;
         }
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
+        for (int k = 0; k < (int)CTB; k++) {
             const uint64_t o = o0 + 16u * (l + 64u * k);
             if (o >= lim) continue;
             const uint64_t r = r0 + idx[k];
