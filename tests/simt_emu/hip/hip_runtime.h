@@ -52,6 +52,11 @@ inline hipError_t hipStreamWaitEvent(hipStream_t, hipEvent_t, unsigned) { return
 inline void __syncthreads() { emu::collective(emu::OP_SYNCTHREADS, 0, 0, 0); }
 
 template <class T> inline T atomicAdd(T *p, T v) { T o = *p; *p = o + v; return o; }
+// agent-scope relaxed loads/stores (blocks run one after the other here)
+#define __HIP_MEMORY_SCOPE_AGENT 3
+template <class T> inline T __hip_atomic_load(const T *p, int, int) { return *(volatile const T *)p; }
+template <class T> inline void __hip_atomic_store(T *p, T v, int, int) { *(volatile T *)p = v; }
+inline void __builtin_amdgcn_s_sleep(int) {}
 template <class T> inline T atomicMin(T *p, T v) { T o = *p; if (v < o) *p = v; return o; }
 template <class T> inline T atomicMax(T *p, T v) { T o = *p; if (v > o) *p = v; return o; }
 template <class T> inline T atomicOr(T *p, T v) { T o = *p; *p = o | v; return o; }

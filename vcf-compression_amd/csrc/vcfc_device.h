@@ -33,6 +33,7 @@ struct VcfcEncodeArgs {
     uint64_t *partials;        // scan partials
     uint64_t *err;             // 1 word
     uint32_t *retry_count;     // rows that took the general kernel (test builds only, VCFC_COUNT_RETRIES)
+    uint8_t *lb;               // look-back scan state (tickets, tile flags; zeroed per encode)
     uint32_t *tile_first;      // per 4 KiB output tile: the row holding its first byte (compaction)
     uint8_t *prim;             // per-row primary staging: record bytes [0, VCFC_PRIM) at prim + VCFC_PRIM * row
     uint8_t *slots;            // per-row overflow slots: record bytes [VCFC_PRIM, ...) at slots + slot_off[row]
@@ -47,7 +48,7 @@ struct VcfcEncodeArgs {
 #define VCFC_PRIM 1024u
 
 struct VcfcWorkspaceLayout {
-    uint64_t slot_off, rec_size, partials, err, retry_count, tile_first, prim, slots, dbg, total;
+    uint64_t slot_off, rec_size, partials, err, lb, lb_bytes, retry_count, tile_first, prim, slots, dbg, total;
 };
 
 // Bytes of per-row staging for a line of `len` bytes: covers the worst-case
@@ -71,6 +72,7 @@ inline void vcfc_encode_args_workspace(VcfcEncodeArgs &a, uint8_t *ws, const Vcf
     a.rec_size = reinterpret_cast<uint32_t *>(ws + L.rec_size);
     a.partials = reinterpret_cast<uint64_t *>(ws + L.partials);
     a.retry_count = reinterpret_cast<uint32_t *>(ws + L.retry_count);
+    a.lb = ws + L.lb;
     a.tile_first = reinterpret_cast<uint32_t *>(ws + L.tile_first);
     a.prim = ws + L.prim;
     a.slots = ws + L.slots;

@@ -1480,6 +1480,96 @@ hipError_t launch_scan(const uint32_t *in, uint64_t n, uint64_t *partials, uint6
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Single-pass exclusive scan u32 -> u64 (n + 1 outputs) with decoupled
+// look-back over tiles of SCAN_TILE items: the encoder's two scans in one
+// launch each instead of three.  Tiles take a ticket in launch order, so a
+// tile only ever waits for tiles whose blocks are already running.  A tile's
+// state is one 8-byte word {status:2, value:62} written by a single
+// agent-scope store and polled with agent-scope loads (one naturally aligned
+// word: no payload to order; MI355X_MICROARCH.md, inter-workgroup
+// visibility).  MODE as launch_scan; TILES (the size scan) also gives every
+// 4 KiB output tile its first row (k_compact_out) and flags records that end
+// past out_cap.  State (tickets, flags) zeroed before the launch.
+constexpr uint64_t LB_AGG = 1ull << 62, LB_INC = 2ull << 62, LB_VAL = LB_AGG - 1;
+
+__device__ __forceinline__ uint64_t lb_load(const uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void lb_store(uint64_t *p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int MODE, bool TILES>
+__global__ __launch_bounds__(256) void k_scan_lb(const uint32_t *__restrict__ in, uint64_t n, uint32_t *ticket,
+                                                 uint64_t *flags, uint64_t *__restrict__ out,
+                                                 uint32_t *__restrict__ tile_first, uint64_t out_cap, uint64_t *err) {
+    __shared__ uint64_t sh[SCAN_THREADS];
+    __shared__ uint32_t s_tile;
+    __shared__ uint64_t s_excl;
+    if (threadIdx.x == 0) s_tile = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const uint64_t tile = s_tile;
+    const uint64_t base = tile * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
+    uint64_t vals[SCAN_ITEMS];
+    uint64_t sum = 0;
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; i++) {
+        vals[i] = base + i < n ? scan_xf<MODE>(in[base + i]) : 0;
+        sum += vals[i];
+    }
+    uint64_t agg;
+    const uint64_t texcl = block_excl_scan_u64(sum, sh, &agg);
+    if (threadIdx.x < 64) {   // wave 0: publish the aggregate, look back
+        const uint32_t l = threadIdx.x;
+        if (l == 0) lb_store(flags + tile, (tile == 0 ? LB_INC : LB_AGG) | agg);
+        uint64_t excl = 0;
+        if (tile > 0) {
+            int64_t p = (int64_t)tile - 1;   // the window covers tiles p, p - 1, ..., p - 63
+            for (;;) {
+                const int64_t q = p - (int64_t)l;
+                const uint64_t f = q >= 0 ? lb_load(flags + q) : LB_INC;   // (before tile 0: an inclusive 0)
+                const uint64_t inc = vw::ballot((f >> 62) == 2);
+                const uint32_t k = inc ? (uint32_t)__builtin_ctzll(inc) : 64u;   // nearest inclusive prefix
+                const uint64_t ready = vw::ballot((f >> 62) != 0);
+                const uint64_t need = k < 64 ? (k == 63 ? ~0ull : ((2ull << k) - 1)) : ~0ull;
+                if ((ready & need) != need) {   // a tile before it has not published yet
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                const uint64_t v = l <= k ? (f & LB_VAL) : 0;
+                // wave total of v, exact: four 16-bit limbs (64 x 0xFFFF fits 32 bits)
+                const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+                const uint64_t tlo = (uint64_t)vw::readlane(vw::scan_add(lo & 0xFFFFu), 63) +
+                                     ((uint64_t)vw::readlane(vw::scan_add(lo >> 16), 63) << 16);
+                const uint64_t thi = (uint64_t)vw::readlane(vw::scan_add(hi & 0xFFFFu), 63) +
+                                     ((uint64_t)vw::readlane(vw::scan_add(hi >> 16), 63) << 16);
+                excl += tlo + (thi << 32);
+                if (k < 64) break;
+                p -= 64;
+            }
+            if (l == 0) lb_store(flags + tile, LB_INC | (excl + agg));
+        }
+        if (l == 0) s_excl = excl;
+    }
+    __syncthreads();
+    uint64_t run = s_excl + texcl;
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; i++) {
+        const uint64_t r = base + i;
+        if (r < n) {
+            out[r] = run;
+            if (TILES) {
+                const uint64_t b = run + vals[i];
+                if (b > out_cap) atomicMin((unsigned long long *)err, (unsigned long long)((r << 8) | VCFCD_E_NOSPACE));
+                for (uint64_t t = (run + CT - 1) / CT; t * CT < b; t++) tile_first[t] = (uint32_t)r;
+            }
+            if (r + 1 == n) out[n] = run + vals[i];
+        }
+        run += vals[i];
+    }
+}
+
 }  // namespace
 
 VcfcWorkspaceLayout vcfc_encode_workspace_layout(uint64_t n, uint64_t total_line_bytes) {
@@ -1490,7 +1580,13 @@ VcfcWorkspaceLayout vcfc_encode_workspace_layout(uint64_t n, uint64_t total_line
     L.rec_size = o; o = al(o + 4 * (n + 1));
     L.partials = o; o = al(o + 8 * ((n + SCAN_TILE - 1) / SCAN_TILE + 1));
     L.err = o; o = al(o + 8);
-    L.retry_count = o; o = al(o + 8);
+    // look-back scan state, zeroed by one memset per encode: the two scans'
+    // tickets, the retry counter, the two scans' tile flags
+    const uint64_t nt = (n + SCAN_TILE - 1) / SCAN_TILE + 1;
+    L.lb = o;
+    L.retry_count = o + 8;
+    L.lb_bytes = 16 + 16 * nt;
+    o = al(o + L.lb_bytes);
     L.tile_first = o; o = al(o + 4 * (vcfc_record_bound(n, total_line_bytes) / CT + 2));
     L.prim = o; o = al(o + (uint64_t)VCFC_PRIM * n);
     L.slots = o; o = al(o + total_line_bytes + total_line_bytes / 2 + 64 * (n + 1));
@@ -1506,11 +1602,20 @@ hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t s, hipEvent_t
     hipError_t e = hipMemsetAsync(a.err, 0xFF, 8, s);
     if (e != hipSuccess) return e;
     if (a.n == 0) return hipMemsetAsync(a.rec_off, 0, 8, s);
+    const uint64_t nt = (a.n + SCAN_TILE - 1) / SCAN_TILE;   // scan tiles
+    uint32_t *tickets = reinterpret_cast<uint32_t *>(a.lb);
+    uint64_t *flags_a = reinterpret_cast<uint64_t *>(a.lb + 16), *flags_b = flags_a + nt + 1;
+    if ((e = hipMemsetAsync(a.lb, 0, 16 + 16 * (nt + 1), s)) != hipSuccess) return e;   // (also retry_count)
     if (ev) (void)hipEventRecord(ev[0], s);
+#ifdef VCFC_SCAN3
     e = launch_scan<1>(a.line_len, a.n, a.partials, a.slot_off, s);
     if (e != hipSuccess) return e;
+#else
+    hipLaunchKernelGGL((k_scan_lb<1, false>), dim3((unsigned)nt), dim3(SCAN_THREADS), 0, s, a.line_len, a.n, tickets,
+                       flags_a, a.slot_off, nullptr, 0, nullptr);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+#endif
     if (ev) (void)hipEventRecord(ev[1], s);
-    if ((e = hipMemsetAsync(a.retry_count, 0, 4, s)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_encode_fast, dim3((unsigned)((a.n + K1_WAVES - 1) / K1_WAVES)), dim3(64 * K1_WAVES), 0, s, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     {
@@ -1521,8 +1626,14 @@ hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t s, hipEvent_t
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (ev) (void)hipEventRecord(ev[2], s);
+#if defined(VCFC_SCAN3) || defined(VCFC_ROW_COMPACT)
     e = launch_scan<0>(a.rec_size, a.n, a.partials, a.rec_off, s);
     if (e != hipSuccess) return e;
+#else
+    hipLaunchKernelGGL((k_scan_lb<0, true>), dim3((unsigned)nt), dim3(SCAN_THREADS), 0, s, a.rec_size, a.n,
+                       tickets + 1, flags_b, a.rec_off, a.tile_first, a.out_cap, a.err);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+#endif
     if (ev) (void)hipEventRecord(ev[3], s);
 #ifdef VCFC_ROW_COMPACT
     // (A/B builds) row-ordered compaction: records of rows longer than 64 KiB
@@ -1537,9 +1648,11 @@ hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t s, hipEvent_t
         hipLaunchKernelGGL(k_compact<16>, dim3((unsigned)((a.n + 15) / 16)), dim3(256), 0, s, a.prim, a.slots,
                            a.slot_off, a.rec_off, a.n, a.out, a.out_cap, a.err);
 #else
+#ifdef VCFC_SCAN3
     hipLaunchKernelGGL(k_tile_first, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, s, a.rec_off, a.n, a.out_cap,
                        a.tile_first, a.err);
     if ((e = hipGetLastError()) != hipSuccess) return e;
+#endif
     {
         // a grid of 8 waves per SIMD striding over the tiles (uniform work)
         const uint64_t tiles = vcfc_record_bound(a.n, a.line_bytes_hint) / CT + 1;
