@@ -494,7 +494,7 @@ def bench_devfile(args, torch, vcfc, workload):
            "data": "synthetic (generated in HBM; header + data lines as one device buffer)",
            "config": {"workload": "%s %d samples x %d variants, %.2f GB file in HBM (BASELINE configs[1])"
                                   % (law_name(args.law), S, n, N / 1e9),
-                      "file_bytes": N, "output_bytes": want_len, "chunk": "4 GiB of whole lines"},
+                      "file_bytes": N, "output_bytes": want_len, "chunk": "the whole file (one line index, one encode)"},
            "roofline": {"kernel": "line index + encoder (whole step)", "bound": "hbm",
                         "achieved": round((2 * N + want_len) / (ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round((2 * N + want_len) / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),

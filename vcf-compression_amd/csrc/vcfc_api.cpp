@@ -642,7 +642,7 @@ int vcfc_compress_buffer(vcfc_ctx *c, const uint8_t *in, uint64_t n, uint8_t *ou
 }
 
 // compress() over VCF file bytes resident in device memory: line index +
-// encoder on the GPU, chunks of whole lines of up to 4 GiB (the context's
+// encoder on the GPU over the whole input at once (or chunks of the context's
 // ingest chunk when one is set), output left in device memory
 // (vcfc_ing::compress_device).
 int vcfc_compress_device(vcfc_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_out, uint64_t out_cap,
@@ -653,7 +653,7 @@ int vcfc_compress_device(vcfc_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *
     if (hipSetDevice(c->device) != hipSuccess) return VCFC_E_HIP;
     CtxIngestMemory M(c);
     vcfc_ing::Config cfg;
-    cfg.max_chunk = (4ull << 30) - (64ull << 10);   // the line index's positions are 32-bit
+    cfg.max_chunk = 1ull << 40;   // (line lengths are 32-bit; the index's positions 64-bit)
     const uint64_t want = c->ingest_chunk ? c->ingest_chunk : cfg.max_chunk;
     cfg.chunk = std::min<uint64_t>(want, std::max<uint64_t>((n + 4095) & ~4095ull, 4096));
     return vcfc_ing::compress_device(d_in, n, d_out, out_cap, out_len, M, c->stream, cfg, err_line);

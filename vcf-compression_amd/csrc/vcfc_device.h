@@ -157,11 +157,11 @@ struct VcfcLineIndex {
     uint64_t *line_off;     // data line j: chunk offset, length, 0-based line number in the chunk
     uint32_t *line_len;
     uint32_t *line_no;
-    uint32_t *pass_off;     // '#' line q: chunk offset, length, line number, data lines before it
+    uint64_t *pass_off;     // '#' line q: chunk offset, length, line number, data lines before it
     uint32_t *pass_len;
     uint32_t *pass_no;
     uint64_t *pass_before;
-    uint64_t *counts;       // {lines, data lines, pass lines}
+    uint64_t *counts;       // {lines, data lines, pass lines, a line of >= 4 GiB}
 };
 struct VcfcLineIndexLayout {
     uint64_t seg_cnt, seg_base, slot, partials1, total1;             // phase 1 workspace

@@ -31,7 +31,7 @@ namespace {
 constexpr uint32_t SEG = 16384;          // bytes per wave
 constexpr uint32_t WIN = 1024;           // bytes per wave step (16 per lane)
 constexpr uint32_t IX_WAVES = 4;
-constexpr uint32_t NL_SLOT = 256;        // '\n' positions kept per segment by k_nl_scan
+constexpr uint32_t NL_SLOT = 128;        // '\n' positions kept per segment by k_nl_scan
 
 // bit j: byte j of x is '\n' (exact per byte)
 __device__ __forceinline__ uint32_t nl_bits(uint32_t x) {
@@ -53,14 +53,14 @@ __device__ __forceinline__ uint32_t nl_mask16(const uint8_t *buf, uint64_t n, ui
 
 // positions of the '\n' bytes of one 1 KiB window (lane l: bytes [p, p + 16))
 // at out[o0 + rank] for ranks below `lim`; returns the window's count
-__device__ __forceinline__ uint32_t nl_window(const uint8_t *buf, uint64_t n, uint64_t p, uint32_t *out, uint64_t o0,
+__device__ __forceinline__ uint32_t nl_window(const uint8_t *buf, uint64_t n, uint64_t p, uint64_t *out, uint64_t o0,
                                               uint64_t lim) {
     uint32_t m = nl_mask16(buf, n, p);
     const uint32_t c = __builtin_popcount(m);
     const uint32_t inc = vw::scan_add(c);
     uint64_t o = o0 + inc - c;
     while (m && o < lim) {
-        out[o++] = (uint32_t)(p + __builtin_ctz(m));
+        out[o++] = p + (uint64_t)__builtin_ctz(m);
         m &= m - 1;
     }
     return vw::readlane(inc, 63);
@@ -75,11 +75,11 @@ __device__ __forceinline__ uint32_t nl_mask_v(uint4 v) {
 // window is processed (16 x 16 B per lane in flight), except in the chunk's
 // last segment, whose bytes past n must not be read as 16-byte blocks.
 __global__ __launch_bounds__(256) void k_nl_scan(const uint8_t *buf, uint64_t n, uint64_t n_seg, uint32_t *seg_cnt,
-                                                 uint32_t *slot) {
+                                                 uint64_t *slot) {
     const uint64_t seg = (uint64_t)blockIdx.x * IX_WAVES + vw::readfirst(threadIdx.x >> 6);
     if (seg >= n_seg) return;
     const uint32_t l = vw::lane_id();
-    uint32_t *sl = slot + seg * NL_SLOT;
+    uint64_t *sl = slot + seg * NL_SLOT;
     uint32_t c = 0;
     if ((seg + 1) * SEG > n) {
         for (uint32_t w = 0; w < SEG; w += WIN) c += nl_window(buf, n, seg * SEG + w + 16 * l, sl, c, NL_SLOT);
@@ -95,9 +95,9 @@ __global__ __launch_bounds__(256) void k_nl_scan(const uint8_t *buf, uint64_t n,
             const uint32_t cnt = __builtin_popcount(m);
             const uint32_t inc = vw::scan_add(cnt);
             uint32_t o = c + inc - cnt;
-            const uint32_t p = (uint32_t)(seg * SEG) + k * WIN + 16 * l;
+            const uint64_t p = seg * SEG + k * WIN + 16 * l;
             while (m && o < NL_SLOT) {
-                sl[o++] = p + __builtin_ctz(m);
+                sl[o++] = p + (uint64_t)__builtin_ctz(m);
                 m &= m - 1;
             }
             c += vw::readlane(inc, 63);
@@ -107,14 +107,14 @@ __global__ __launch_bounds__(256) void k_nl_scan(const uint8_t *buf, uint64_t n,
 }
 
 __global__ __launch_bounds__(256) void k_nl_place(const uint8_t *buf, uint64_t n, uint64_t n_seg, const uint32_t *seg_cnt,
-                                                  const uint32_t *slot, const uint64_t *seg_base, uint32_t *nl) {
+                                                  const uint64_t *slot, const uint64_t *seg_base, uint64_t *nl) {
     const uint64_t seg = (uint64_t)blockIdx.x * IX_WAVES + vw::readfirst(threadIdx.x >> 6);
     if (seg >= n_seg) return;
     const uint32_t l = vw::lane_id();
     const uint32_t c = seg_cnt[seg];
-    uint32_t *dst = nl + seg_base[seg];
+    uint64_t *dst = nl + seg_base[seg];
     if (c <= NL_SLOT) {
-        const uint32_t *sl = slot + seg * NL_SLOT;
+        const uint64_t *sl = slot + seg * NL_SLOT;
         for (uint32_t k = l; k < c; k += 64) dst[k] = sl[k];
         return;
     }
@@ -122,32 +122,33 @@ __global__ __launch_bounds__(256) void k_nl_place(const uint8_t *buf, uint64_t n
     for (uint32_t w = 0; w < SEG; w += WIN) o += nl_window(buf, n, seg * SEG + w + 16 * l, dst, o, ~0ull);
 }
 
-__global__ __launch_bounds__(256) void k_line_kind(const uint8_t *buf, const uint32_t *nl, uint64_t n_lines,
+__global__ __launch_bounds__(256) void k_line_kind(const uint8_t *buf, const uint64_t *nl, uint64_t n_lines,
                                                    uint32_t *is_data, uint32_t *is_pass) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_lines) return;
-    const uint32_t s = i ? nl[i - 1] + 1 : 0u;
+    const uint64_t s = i ? nl[i - 1] + 1 : 0u;
     const bool nonempty = nl[i] > s;
     const bool hash = nonempty && buf[s] == '#';
     is_data[i] = nonempty && !hash;
     is_pass[i] = hash;
 }
 
-__global__ __launch_bounds__(256) void k_line_place(const uint32_t *nl, uint64_t n_lines, const uint64_t *data_rank,
+__global__ __launch_bounds__(256) void k_line_place(const uint64_t *nl, uint64_t n_lines, const uint64_t *data_rank,
                                                     const uint64_t *pass_rank, VcfcLineIndex x) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_lines) return;
-    const uint32_t s = i ? nl[i - 1] + 1 : 0u;
+    const uint64_t s = i ? nl[i - 1] + 1 : 0u;
     const uint64_t d = data_rank[i];
+    if (nl[i] - s > 0xFFFFFFFFull) atomicMax((unsigned long long *)(x.counts + 3), 1ull);   // line lengths are 32-bit
     if (data_rank[i + 1] > d) {
         x.line_off[d] = s;
-        x.line_len[d] = nl[i] - s;
+        x.line_len[d] = (uint32_t)(nl[i] - s);
         x.line_no[d] = (uint32_t)i;
     }
     const uint64_t q = pass_rank[i];
     if (pass_rank[i + 1] > q) {
         x.pass_off[q] = s;
-        x.pass_len[q] = nl[i] - s;
+        x.pass_len[q] = (uint32_t)(nl[i] - s);
         x.pass_no[q] = (uint32_t)i;
         x.pass_before[q] = d;
     }
@@ -164,11 +165,11 @@ VcfcLineIndexLayout vcfc_line_index_layout(uint64_t chunk_bytes, uint64_t n_line
     uint64_t o = 0;
     L.seg_cnt = o; o = al(o + 4 * seg);
     L.seg_base = o; o = al(o + 8 * (seg + 1));
-    L.slot = o; o = al(o + 4ull * NL_SLOT * seg);
+    L.slot = o; o = al(o + 8ull * NL_SLOT * seg);
     L.partials1 = o; o = al(o + 8 * ((seg + 4095) / 4096 + 1));
     L.total1 = o;
     o = 0;
-    L.nl = o; o = al(o + 4 * (n_lines + 1));
+    L.nl = o; o = al(o + 8 * (n_lines + 1));
     L.is_data = o; o = al(o + 4 * (n_lines + 1));
     L.is_pass = o; o = al(o + 4 * (n_lines + 1));
     L.data_rank = o; o = al(o + 8 * (n_lines + 1));
@@ -188,7 +189,7 @@ hipError_t vcfc_line_index(const uint8_t *buf, uint64_t n, uint8_t *ws, const Vc
     // ws: phase 1 workspace (L.total1 bytes)
     uint32_t *seg_cnt = reinterpret_cast<uint32_t *>(ws + L.seg_cnt);
     uint64_t *seg_base = reinterpret_cast<uint64_t *>(ws + L.seg_base);
-    uint32_t *slot = reinterpret_cast<uint32_t *>(ws + L.slot);
+    uint64_t *slot = reinterpret_cast<uint64_t *>(ws + L.slot);
     uint64_t *partials = reinterpret_cast<uint64_t *>(ws + L.partials1);
     hipError_t e;
     if (n == 0) return hipMemsetAsync(x.counts, 0, 24, s);
@@ -207,15 +208,16 @@ hipError_t vcfc_line_index_place(const uint8_t *buf, uint64_t n, uint64_t n_line
                                  const VcfcLineIndexLayout &L, const VcfcLineIndex &x, hipStream_t s) {
     const uint32_t *seg_cnt = reinterpret_cast<const uint32_t *>(ws1 + L.seg_cnt);
     const uint64_t *seg_base = reinterpret_cast<const uint64_t *>(ws1 + L.seg_base);
-    const uint32_t *slot = reinterpret_cast<const uint32_t *>(ws1 + L.slot);
-    uint32_t *nl = reinterpret_cast<uint32_t *>(ws2 + L.nl);
+    const uint64_t *slot = reinterpret_cast<const uint64_t *>(ws1 + L.slot);
+    uint64_t *nl = reinterpret_cast<uint64_t *>(ws2 + L.nl);
     uint32_t *is_data = reinterpret_cast<uint32_t *>(ws2 + L.is_data);
     uint32_t *is_pass = reinterpret_cast<uint32_t *>(ws2 + L.is_pass);
     uint64_t *data_rank = reinterpret_cast<uint64_t *>(ws2 + L.data_rank);
     uint64_t *pass_rank = reinterpret_cast<uint64_t *>(ws2 + L.pass_rank);
     uint64_t *partials = reinterpret_cast<uint64_t *>(ws2 + L.partials2);
     hipError_t e;
-    if (n_lines == 0) return hipMemsetAsync(x.counts + 1, 0, 16, s);
+    if (n_lines == 0) return hipMemsetAsync(x.counts + 1, 0, 24, s);
+    if ((e = hipMemsetAsync(x.counts + 3, 0, 8, s)) != hipSuccess) return e;
     const uint64_t n_seg = (n + SEG - 1) / SEG;
     hipLaunchKernelGGL(k_nl_place, dim3((unsigned)((n_seg + IX_WAVES - 1) / IX_WAVES)), dim3(64 * IX_WAVES), 0, s, buf,
                        n, n_seg, seg_cnt, slot, seg_base, nl);

@@ -363,19 +363,20 @@ inline int compress_stream(Source &src, const Sink &sink, Memory &M, hipStream_t
         x.pass_before = reinterpret_cast<uint64_t *>(q); q += 8 * (max_data + 1);
         x.line_len = reinterpret_cast<uint32_t *>(q); q += 4 * (max_data + 1);
         x.line_no = reinterpret_cast<uint32_t *>(q); q += 4 * (max_data + 1);
-        std::vector<uint32_t> pass_off, pass_len, pass_no;
-        std::vector<uint64_t> pass_before;
+        std::vector<uint32_t> pass_len, pass_no;
+        std::vector<uint64_t> pass_off, pass_before;
         // the pass arrays (off, len, no) share one buffer with the record offsets
-        const uint64_t rec_bytes_needed = 8 * (max_data + 1) + 12 * (max_data + 1);
+        const uint64_t rec_bytes_needed = 16 * (max_data + 1) + 8 * (max_data + 1);
         uint8_t *d_rec = static_cast<uint8_t *>(M.dev(Memory::D_REC, rec_bytes_needed));
         if (!d_rec) return finish(ST_E_HIP);
         uint64_t *d_rec_off = reinterpret_cast<uint64_t *>(d_rec);
-        x.pass_off = reinterpret_cast<uint32_t *>(d_rec + 8 * (max_data + 1));
-        x.pass_len = x.pass_off + (max_data + 1);
+        x.pass_off = reinterpret_cast<uint64_t *>(d_rec + 8 * (max_data + 1));
+        x.pass_len = reinterpret_cast<uint32_t *>(d_rec + 16 * (max_data + 1));
         x.pass_no = x.pass_len + (max_data + 1);
         if (vcfc_line_index_place(d_in, n, n_lines, d_ix1, d_ix2, L, x, s) != hipSuccess ||
-            hipMemcpyAsync(hsmall, d_small, 24, hipMemcpyDeviceToHost, s) != hipSuccess || !sync())
+            hipMemcpyAsync(hsmall, d_small, 32, hipMemcpyDeviceToHost, s) != hipSuccess || !sync())
             return finish(ST_E_HIP);
+        if (hsmall[3]) return finish(ST_E_ARG);
         const uint64_t n_data = hsmall[1], n_pass = hsmall[2];
         // '#' lines: bytes from the host copy, checked in order; the first
         // header line with < 8 terms stops the input there
@@ -384,7 +385,7 @@ inline int compress_stream(Source &src, const Sink &sink, Memory &M, hipStream_t
         uint64_t hdr_before = 0;
         if (n_pass) {
             pass_off.resize(n_pass); pass_len.resize(n_pass); pass_no.resize(n_pass); pass_before.resize(n_pass);
-            if (hipMemcpyAsync(pass_off.data(), x.pass_off, 4 * n_pass, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            if (hipMemcpyAsync(pass_off.data(), x.pass_off, 8 * n_pass, hipMemcpyDeviceToHost, s) != hipSuccess ||
                 hipMemcpyAsync(pass_len.data(), x.pass_len, 4 * n_pass, hipMemcpyDeviceToHost, s) != hipSuccess ||
                 hipMemcpyAsync(pass_no.data(), x.pass_no, 4 * n_pass, hipMemcpyDeviceToHost, s) != hipSuccess ||
                 hipMemcpyAsync(pass_before.data(), x.pass_before, 8 * n_pass, hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -485,7 +486,7 @@ inline int compress_stream(Source &src, const Sink &sink, Memory &M, hipStream_t
 // holds the file's bytes as read (N > 0, d_in[N - 1] == '\n'), the .vcfc bytes
 // go to d_out[0, *out_len).  The GPU stage of compress_stream without the
 // transfer stages: chunks of whole lines (up to cfg.chunk bytes, grown to
-// hold a longer line, up to cfg.max_chunk: the index's positions are 32-bit)
+// hold a longer line, up to cfg.max_chunk; by default the whole input)
 // are line-indexed and encoded in place; a chunk whose '#' lines all precede
 // its data lines (every real VCF) is encoded straight behind them into
 // d_out, one with interleaved '#' lines through a scratch buffer.  The host
@@ -554,7 +555,7 @@ inline int compress_device(const uint8_t *d_in, uint64_t N, uint8_t *d_out, uint
         const VcfcLineIndexLayout L = vcfc_line_index_layout(n, n_lines);
         uint8_t *d_ix2 = static_cast<uint8_t *>(M.dev(Memory::D_IX2, L.total2));
         uint8_t *d_lines = static_cast<uint8_t *>(M.dev(Memory::D_LINES, 32 * (n_lines + 1)));
-        uint8_t *d_rec = static_cast<uint8_t *>(M.dev(Memory::D_REC, 20 * (n_lines + 1)));
+        uint8_t *d_rec = static_cast<uint8_t *>(M.dev(Memory::D_REC, 24 * (n_lines + 1)));
         if (!d_ix2 || !d_lines || !d_rec) return ST_E_HIP;
         uint8_t *q = d_lines;
         x.line_off = reinterpret_cast<uint64_t *>(q); q += 8 * (n_lines + 1);
@@ -562,12 +563,13 @@ inline int compress_device(const uint8_t *d_in, uint64_t N, uint8_t *d_out, uint
         x.line_len = reinterpret_cast<uint32_t *>(q); q += 4 * (n_lines + 1);
         x.line_no = reinterpret_cast<uint32_t *>(q);
         uint64_t *d_rec_off = reinterpret_cast<uint64_t *>(d_rec);
-        x.pass_off = reinterpret_cast<uint32_t *>(d_rec + 8 * (n_lines + 1));
-        x.pass_len = x.pass_off + (n_lines + 1);
+        x.pass_off = reinterpret_cast<uint64_t *>(d_rec + 8 * (n_lines + 1));
+        x.pass_len = reinterpret_cast<uint32_t *>(d_rec + 16 * (n_lines + 1));
         x.pass_no = x.pass_len + (n_lines + 1);
-        if (vcfc_line_index_place(d_c, n, n_lines, d_ix1, d_ix2, L, x, s) != hipSuccess || !d2h(hsmall, d_small, 24) ||
+        if (vcfc_line_index_place(d_c, n, n_lines, d_ix1, d_ix2, L, x, s) != hipSuccess || !d2h(hsmall, d_small, 32) ||
             !sync())
             return ST_E_HIP;
+        if (hsmall[3]) return ST_E_ARG;   // a line of 4 GiB or more
         const uint64_t n_data = hsmall[1], n_pass = hsmall[2];
         // ---- '#' lines: to the host, checked in order ----
         std::vector<PassLine> pass;
@@ -575,9 +577,9 @@ inline int compress_device(const uint8_t *d_in, uint64_t N, uint8_t *d_out, uint
         uint64_t hdr_before = 0, pass_bytes = 0;
         bool interleaved = false;
         if (n_pass) {
-            std::vector<uint32_t> po(n_pass), pl(n_pass), pn(n_pass);
-            std::vector<uint64_t> pb(n_pass);
-            if (!d2h(po.data(), x.pass_off, 4 * n_pass) || !d2h(pl.data(), x.pass_len, 4 * n_pass) ||
+            std::vector<uint32_t> pl(n_pass), pn(n_pass);
+            std::vector<uint64_t> po(n_pass), pb(n_pass);
+            if (!d2h(po.data(), x.pass_off, 8 * n_pass) || !d2h(pl.data(), x.pass_len, 4 * n_pass) ||
                 !d2h(pn.data(), x.pass_no, 4 * n_pass) || !d2h(pb.data(), x.pass_before, 8 * n_pass) || !sync())
                 return ST_E_HIP;
             for (uint64_t k = 0; k < n_pass; k++) {
