@@ -25,6 +25,8 @@ law 2 "general shapes" (SURVEY §8(d) D3): chrX-shaped rows of five kinds,
 The 9 leading columns are built on the host; the genotype columns (the
 dominant bytes) are generated on the GPU by vcfc_synth_rows_device.
 """
+import os
+
 import numpy as np
 
 BASES = np.array(list("ATGC"))
@@ -61,6 +63,8 @@ def prefixes(n, law, seed, row0=0, samples=2504):
     gt_len = None
     if law == 2:
         kind = rng.choice(5, n, p=LAW2_KINDS)
+        if os.environ.get("VCFC_LAW2_KIND"):   # diagnostics: every row of one kind
+            kind[:] = int(os.environ["VCFC_LAW2_KIND"])
         gaps = rng.geometric(1.0 / 32.0, n)
         pos = 2781479 + row0 * 32 + np.cumsum(gaps) - gaps[0]
         an = 2 * samples
