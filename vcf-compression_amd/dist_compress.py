@@ -209,11 +209,17 @@ def main():
         return out.view(world, len(vals)).cpu().tolist()
 
     if mode == "sparsify":
-        if ctx is None:
-            vcfc.raise_for(vcfc.E_HIP)
-        st = sparsify_shards(rank, world,
-                             lambda write: ctx.sparsify_shard(in_path, out_path if write else None, rank, world),
-                             lambda: ctx.sparsify_status(in_path, out_path), allgather)
+        # (a rank without a context reports E_HIP through the all-gathers
+        # instead of raising before them: the other ranks would wait forever)
+        def shard(write):
+            if ctx is None:
+                return vcfc.E_HIP, [0, 0, None, 0]
+            return ctx.sparsify_shard(in_path, out_path if write else None, rank, world)
+
+        def whole():
+            return vcfc.E_HIP if ctx is None else ctx.sparsify_status(in_path, out_path)
+
+        st = sparsify_shards(rank, world, shard, whole, allgather)
         line = -1
     else:
         st, total, line = compress_shard(in_path, out_path, rank, world, compress_range, allgather)
