@@ -71,14 +71,15 @@ def data_lines(vcf):
 LAST_RETRIES = [0]
 
 
-def emu_encode(buf, line_off, line_len):
-    """Run the product encode pipeline on the emulator.
-    Returns (status, records bytes, rec_off array, err_word); the number of
-    rows the fast kernel handed to the general kernel is left in
-    LAST_RETRIES[0]."""
+def emu_encode(buf, line_off, line_len, cap=None):
+    """Run the product encode pipeline on the emulator (output capacity
+    `cap`, default the bound).  Returns (status, records bytes, rec_off
+    array, err_word); the number of rows the fast kernel handed to the
+    general kernel is left in LAST_RETRIES[0]."""
     n = len(line_off)
-    cap = int(sum(int(x) * 3 // 2 + 32 for x in line_len)) + 64
-    out = np.zeros(cap, dtype=np.uint8)
+    full = int(sum(int(x) * 3 // 2 + 32 for x in line_len)) + 64
+    cap = full if cap is None else cap
+    out = np.zeros(max(cap, full), dtype=np.uint8)   # (bytes past cap must stay untouched)
     rec_off = np.zeros(n + 1, dtype=np.uint64)
     src = np.frombuffer(buf, dtype=np.uint8).copy()
     lo = np.ascontiguousarray(line_off, dtype=np.uint64)
@@ -90,6 +91,8 @@ def emu_encode(buf, line_off, line_len):
                                rec_off.ctypes.data, ctypes.byref(err), ctypes.byref(sw), ctypes.byref(rt))
     LAST_RETRIES[0] = rt.value
     total = int(rec_off[n]) if n else 0
+    if cap < full:
+        assert not out[cap:].any(), "bytes written past out_cap"
     return st, out[:total].tobytes(), rec_off, err.value
 
 

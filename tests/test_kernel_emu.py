@@ -252,3 +252,27 @@ def test_many_rows_scan_tiles_and_compaction_tiles():
     st, out2, ro2, err2 = run(bad)
     assert err2 == (500 << 8) | 1
     assert out2[:int(ro2[500])] == out[:int(ro[500])]
+
+
+def test_output_capacity_short():
+    """out_cap below the records' total: the first row whose record ends past
+    it is reported (VCFC_E_NOSPACE, row << 8 | 4), the records before it are
+    intact, nothing is written past out_cap."""
+    rnd = random.Random(5)
+    lines = []
+    for i in range(300):
+        toks = [rnd.choice([b"0|0", b"0|1", b"1|1", b"0|2"]) for _ in range(rnd.choice([3, 60, 400]))]
+        lines.append(b"\t".join([b"1", b"%d" % i, b"a", b"b", b"c", b"d", b"e", b"f", b"GT"] + toks))
+    st, out, ro, err = run(lines)
+    assert err == (1 << 64) - 1
+    for cut_row in (0, 37, 211):
+        cap = int(ro[cut_row]) + int(ro[cut_row + 1] - ro[cut_row]) // 2
+        buf = bytearray()
+        offs, lens = [], []
+        for ln in lines:
+            offs.append(len(buf))
+            lens.append(len(ln))
+            buf += ln + b"\n"
+        st2, out2, ro2, err2 = E.emu_encode(bytes(buf), np.array(offs, np.uint64), np.array(lens, np.uint32), cap=cap)
+        assert err2 == (cut_row << 8) | 4, (cut_row, hex(err2))
+        assert out2[:int(ro[cut_row])] == out[:int(ro[cut_row])]

@@ -1389,7 +1389,11 @@ __global__ __launch_bounds__(256) void k_compact_out(const uint8_t *__restrict__
             if (o + 16 > en[k] && en[k] < lim)   // the next non-empty record starts at en
                 v = merge16(v, vw::uload16(prims + (uint64_t)VCFC_PRIM * (r0 + idx2[k])), (uint32_t)(en[k] - o));
             if (o + 16 <= lim) {
+#ifdef VCFC_COMPACT_NT
+                vw::gstore16_nt(out, o, v);
+#else
                 vw::gstore16(out, o, v);
+#endif
             } else {
                 const uint32_t w[4] = {v.x, v.y, v.z, v.w};
                 for (uint32_t i = 0; o + i < lim; i++) out[o + i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
