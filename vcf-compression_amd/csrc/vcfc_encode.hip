@@ -1389,7 +1389,10 @@ __global__ __launch_bounds__(256) void k_compact_out(const uint8_t *__restrict__
             if (o + 16 > en[k] && en[k] < lim)   // the next non-empty record starts at en
                 v = merge16(v, vw::uload16(prims + (uint64_t)VCFC_PRIM * (r0 + idx2[k])), (uint32_t)(en[k] - o));
             if (o + 16 <= lim) {
-#ifdef VCFC_COMPACT_NT
+#ifndef VCFC_COMPACT_TEMPORAL
+                // non-temporal: the records leave the chip (D2H, a file, the
+                // next stage), and the next batch's encode keeps L2 / MALL to
+                // itself (-0.8 % per step in an A/B, ab_compact_nt.txt)
                 vw::gstore16_nt(out, o, v);
 #else
                 vw::gstore16(out, o, v);
