@@ -571,6 +571,9 @@ __device__ __forceinline__ void esc8(const uint32_t (&d)[TPL8], int32_t t0, int3
     // {0,1}) iff a and b are '0'/'1' and the separator is '|'.  Class byte =
     // 0x90 + 2a + b, escapes 0x94; an escape's bytes never reach a neighbour.
     uint32_t cbL, cbH, eL, eH;   // eL/eH: 0xFF in the byte of each escape slot
+#ifdef VCFC_ASM_MARK
+    asm volatile(";esc8_begin" ::: "memory");
+#endif
     esc_classes(d[0], d[1], d[2], d[3], cbL, eL);
     esc_classes(d[4], d[5], d[6], d[7], cbH, eH);
     f.esc = vw::ballot((eL | eH) != 0) != 0;
@@ -600,7 +603,9 @@ __device__ __forceinline__ void esc8(const uint32_t (&d)[TPL8], int32_t t0, int3
     const uint32_t sH = (xH | (xH >> 1) | (xH >> 2) | (cbH >> 2)) & 0x01010101u;
     const uint32_t sb = stride4(sL, sH) & vbits;
     const uint32_t eb = stride4((cbL >> 2) & 0x01010101u, (cbH >> 2) & 0x01010101u) & vbits;   // escape slots
+#ifdef VCFC_ESC_EMIT1
     const uint32_t cp4 = stride4(cpL & 0x07070707u, cpH & 0x07070707u);       // class of slot j-1 at bits 4j
+#endif
     const uint32_t lane_rs = sb ? (uint32_t)(t0 + 8) - ((uint32_t)__builtin_clz(sb) >> 2) : 0u;
     const uint32_t incl = vw::scan_max(lane_rs);
     const uint32_t rin = vw::umax(vw::shr1z(incl), f.prs);
@@ -627,11 +632,15 @@ __device__ __forceinline__ void esc8(const uint32_t (&d)[TPL8], int32_t t0, int3
     // unconditional: a byte or escape word the lane does not emit goes to its
     // dummy word, so the slots need no branches; an escape's four bytes
     // (0xE1 and its token) leave as one unaligned ds_write_b32.
+#ifdef VCFC_ASM_MARK
+    asm volatile(";esc8_emit" ::: "memory");
+#endif
     const uint32_t base = (r.wpos + incl2 - cnt) & RMASK;
     uint8_t *const lb = r.lds + base;
     uint8_t *const dm = r.lds + RING_DUMMY + 4u * vw::lane_id();
     *(full ? lb : dm) = (uint8_t)(m0 | cap);
     uint32_t o = full ? 1u : 0u;
+#ifdef VCFC_ESC_EMIT1
     uint32_t jp = 0;
 #pragma unroll
     for (int j = 0; j < (int)TPL8; j++) {
@@ -649,12 +658,44 @@ __device__ __forceinline__ void esc8(const uint32_t (&d)[TPL8], int32_t t0, int3
         o += e ? 4u : 0u;
         if (s) jp = (uint32_t)j;
     }
+#else
+    // The first start's lead byte follows the full byte (nothing else comes
+    // before the first start: escapes are starts).  Later starts close the
+    // run begun at the previous start: lead = mask(class) + length, where the
+    // class table gives 0x08 for an escape predecessor, whose run has length
+    // 1 (0x09 = TAB).  Per slot: the byte's address is dm + s * (lb + o - dm)
+    // (s, e in {0, 1}; one 24-bit multiply-add instead of a compare and a
+    // select), and the offsets advance by s and 4 e.
+    *(lead1 ? lb + o : dm) = (uint8_t)b1;
+    o += lead1 ? 1u : 0u;
+    const uint32_t sbr = sb & (sb - 1u);   // starts after the first
+    const uint32_t dmi = RING_DUMMY + 4u * vw::lane_id();
+    const int32_t ldm = (int32_t)base - (int32_t)dmi;
+    const uint32_t mL = vw::perm(0x08u, 0x80C0A000u, cpL & 0x07070707u) + 0x03020100u;   // mask + slot index
+    const uint32_t mH = vw::perm(0x08u, 0x80C0A000u, cpH & 0x07070707u) + 0x07060504u;
+    int32_t njp = -(int32_t)j1;   // minus the previous start
+#pragma unroll
+    for (int j = 0; j < (int)TPL8; j++) {
+        const int32_t s = (int32_t)((sbr >> (4 * j)) & 1u);
+        const int32_t e = (int32_t)((eb >> (4 * j)) & 1u);
+        const uint32_t b = ((((j < 4) ? mL : mH) >> (8 * (j & 3))) & 0xFFu) + (uint32_t)njp;
+        r.lds[dmi + (uint32_t)__mul24(s, ldm + (int32_t)o)] = (uint8_t)b;
+        o += (uint32_t)s;
+        const uint32_t pay = (d[j] << 8) | 0xE1u;   // 0xE1, then the token's three bytes
+        __builtin_memcpy(r.lds + (dmi + (uint32_t)__mul24(e, ldm + (int32_t)o)), &pay, 4);
+        o += 4u * (uint32_t)e;
+        njp = s ? -j : njp;
+    }
+#endif
     const bool wrap = base + cnt > RING;
     if (vw::ballot(wrap)) {
         if (wrap) {
             for (uint32_t q = RING; q < base + cnt; q++) r.lds[q - RING] = r.lds[q];
         }
     }
+#ifdef VCFC_ASM_MARK
+    asm volatile(";esc8_end" ::: "memory");
+#endif
     r.wpos += vw::readlane(incl2, 63);
     f.pcls = (vw::readlane(cbH, 63) >> 24) & 7u;
     f.prs = vw::umax(vw::readlane(incl, 63), f.prs);
