@@ -57,11 +57,6 @@ template <class T> inline T atomicAdd(T *p, T v) { T o = *p; *p = o + v; return 
 template <class T> inline T __hip_atomic_load(const T *p, int, int) { return *(volatile const T *)p; }
 template <class T> inline void __hip_atomic_store(T *p, T v, int, int) { *(volatile T *)p = v; }
 inline void __builtin_amdgcn_s_sleep(int) {}
-// signed 24 x 24-bit multiply (v_mad_i32_i24 / v_mul_i32_i24)
-inline int __mul24(int a, int b) {
-    const int64_t x = (int64_t)(int32_t)((uint32_t)a << 8) >> 8, y = (int64_t)(int32_t)((uint32_t)b << 8) >> 8;
-    return (int)(uint32_t)(uint64_t)(x * y);
-}
 template <class T> inline T atomicMin(T *p, T v) { T o = *p; if (v < o) *p = v; return o; }
 template <class T> inline T atomicMax(T *p, T v) { T o = *p; if (v > o) *p = v; return o; }
 template <class T> inline T atomicOr(T *p, T v) { T o = *p; *p = o | v; return o; }

@@ -679,10 +679,10 @@ __device__ __forceinline__ void esc8(const uint32_t (&d)[TPL8], int32_t t0, int3
         const int32_t s = (int32_t)((sbr >> (4 * j)) & 1u);
         const int32_t e = (int32_t)((eb >> (4 * j)) & 1u);
         const uint32_t b = ((((j < 4) ? mL : mH) >> (8 * (j & 3))) & 0xFFu) + (uint32_t)njp;
-        r.lds[dmi + (uint32_t)__mul24(s, ldm + (int32_t)o)] = (uint8_t)b;
+        r.lds[(uint32_t)vw::mad24(s, ldm + (int32_t)o, (int32_t)dmi)] = (uint8_t)b;
         o += (uint32_t)s;
         const uint32_t pay = (d[j] << 8) | 0xE1u;   // 0xE1, then the token's three bytes
-        __builtin_memcpy(r.lds + (dmi + (uint32_t)__mul24(e, ldm + (int32_t)o)), &pay, 4);
+        __builtin_memcpy(r.lds + (uint32_t)vw::mad24(e, ldm + (int32_t)o, (int32_t)dmi), &pay, 4);
         o += 4u * (uint32_t)e;
         njp = s ? -j : njp;
     }
