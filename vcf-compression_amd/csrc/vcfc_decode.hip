@@ -203,22 +203,6 @@ __device__ __forceinline__ ItemLane scan_window(uint32_t v4, uint32_t b0, uint32
     return r;
 }
 
-// item word "a|b\t" (little-endian) of the item starting with byte x at
-// position k (escapes: its 3 payload bytes)
-template <class G>
-__device__ __forceinline__ uint32_t item_word(uint32_t x, uint32_t k, G &&at) {
-    uint32_t w;
-    if (x == 0xE1u) {
-        w = at(k + 1) | (at(k + 2) << 8) | (at(k + 3) << 16);
-    } else if (x < 0x80u) {
-        w = 0x307C30u;
-    } else {
-        const uint32_t m = x & 0xE0u;
-        w = (m == 0xA0u ? 0x30u : 0x31u) | 0x7C00u | ((m == 0xC0u ? 0x30u : 0x31u) << 16);
-    }
-    return w | 0x09000000u;
-}
-
 // A record staged through LDS in pieces of up to SB bytes (plus 8 bytes of
 // look-ahead), loaded with 16-byte buffer loads: one load latency per piece
 // instead of one per 64-byte window, and no global load between the
@@ -506,18 +490,34 @@ __device__ __forceinline__ void write_one(const VcfcDecodeArgs &a, uint64_t i, u
     };
     const uint32_t s0 = rs + 8 + req, s1 = re - 1;
     ItemState st;
-    auto at = [&](uint32_t k) { return sg.at(k); };
     for (uint32_t cur = s0 & ~3u; cur < s1; cur += 256) {
         sg.need(cur, 256 + 8);
         const uint32_t b = umin32(cur + 256, s1);
-        const ItemLane it = scan_window(sg.at4(cur + 4 * l), cur, s0, b, s1, st);
-        uint32_t w[4];
+        // the lane's dword and the next one (an escape's payload may run into it)
+        const uint32_t v4 = sg.at4(cur + 4 * l), v4n = sg.at4(cur + 4 * l + 4);
+        const ItemLane it = scan_window(v4, cur, s0, b, s1, st);
+        // item words "a|b\t" (little-endian), branch-free: an escape (0xE1)
+        // gives its 3 payload bytes, a 0|0 run byte (< 0x80) "0|0", a phased
+        // run byte 0x80 / 0xA0 / 0xC0 "1|1" / "0|1" / "1|0"; and the token
+        // index of each item start (~0 for bytes that start none: never in a tile)
+        uint32_t w[4], ws[4];
 #pragma unroll
-        for (uint32_t j = 0; j < 4; j++) w[j] = (it.start >> j) & 1u ? item_word(sg.at(cur + 4 * l + j), cur + 4 * l + j, at) : 0u;
+        for (uint32_t j = 0; j < 4; j++) {
+            const uint32_t x = (v4 >> (8 * j)) & 0xFFu;
+            const uint32_t pay = (j < 3 ? vw::alignbyte(v4n, v4, j + 1) : v4n) & 0x00FFFFFFu;
+            const uint32_t m = x >> 5;   // 4: 1|1, 5: 0|1, 6: 1|0
+            const uint32_t ph = (m == 5u ? 0x30u : 0x31u) | 0x7C00u | ((m == 6u ? 0x30u : 0x31u) << 16);
+            w[j] = (x == 0xE1u ? pay : x < 0x80u ? 0x307C30u : ph) | 0x09000000u;
+            ws[j] = (it.start >> j) & 1u ? it.gb[j] : ~0u;
+        }
         for (;;) {
+            // every item writes: its slot if it starts in this tile, else
+            // the lane's dummy word past the tile (no branches)
 #pragma unroll
-            for (uint32_t j = 0; j < 4; j++)
-                if (((it.start >> j) & 1u) && it.gb[j] >= j0 && it.gb[j] < j0 + TB) W[it.gb[j] - j0] = w[j];
+            for (uint32_t j = 0; j < 4; j++) {
+                const uint32_t o = ws[j] - j0;
+                W[o < TB ? o : TB + l] = w[j];
+            }
             if (st.got < j0 + TB || j0 + TB > S) break;   // the tile is not complete yet
             tile_out(TB);
             j0 += TB;
@@ -540,10 +540,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VCFC_DEC_WP
 __global__ __launch_bounds__(256) void k_dec_write(VcfcDecodeArgs a, uint64_t first, uint64_t last) {
 #endif
     __shared__ __attribute__((aligned(16))) uint8_t sbuf[DEC_WAVES * SBUF];
-    __shared__ __attribute__((aligned(16))) uint32_t tbuf[DEC_WAVES * TB];
+    __shared__ __attribute__((aligned(16))) uint32_t tbuf[DEC_WAVES * (TB + 64)];   // tile + a dummy word per lane
     const uint32_t wave = vw::readfirst(threadIdx.x >> 6);
     uint8_t *sb = sbuf + wave * SBUF;
-    uint32_t *W = tbuf + wave * TB;
+    uint32_t *W = tbuf + wave * (TB + 64);
     const uint64_t g = (uint64_t)blockIdx.x * DEC_WAVES + wave;
     if (!SEL) {
         if (first + g < last) write_one(a, first + g, sb, W);
