@@ -156,22 +156,36 @@ struct ItemState {
 };
 struct ItemLane {
     uint32_t start;    // bit j: byte j of the lane's dword starts an item
-    uint32_t cnt[4];   // tokens of each byte's item (0 if not a start)
     uint32_t gb[4];    // tokens before each byte's item
 };
 
+// bit j <- bit 8j + 7 of x (one flag per byte, as 0x80 in that byte)
+__device__ __forceinline__ uint32_t msb4(uint32_t x) {
+    return ((x >> 7) & 1u) | ((x >> 14) & 2u) | ((x >> 21) & 4u) | ((x >> 28) & 8u);
+}
+// bits [lo, hi) of a 4-bit mask (0 <= lo, hi <= 4)
+__device__ __forceinline__ uint32_t bits4(uint32_t lo, uint32_t hi) {
+    return ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+}
+
+// All four bytes of the lane at once (4-bit masks, one bit per byte): which
+// bytes are in [s0, b), escape flags (0xE1), payload and terminator bytes,
+// item starts and their token counts (a byte < 0x80 counts itself, a byte
+// >= 0x80 its low 5 bits: 1 for 0xE1), and the checks of a simple record --
+// payload bytes are < 0x80 and neither TAB nor LF, terminators are TAB, a
+// start is not an escape code other than 0xE1, an escape's 3 bytes and
+// terminator end before s1, and no item counts 0 tokens.
 __device__ __forceinline__ ItemLane scan_window(uint32_t v4, uint32_t b0, uint32_t s0, uint32_t b, uint32_t s1,
                                                 ItemState &st) {
     const uint32_t l = vw::lane_id();
     const uint32_t k0 = b0 + 4 * l;
-    uint32_t valid = 0, e = 0, by[4];
-#pragma unroll
-    for (uint32_t j = 0; j < 4; j++) {
-        by[j] = (v4 >> (8 * j)) & 0xFFu;
-        const bool vj = k0 + j >= s0 && k0 + j < b;
-        valid |= (vj ? 1u : 0u) << j;
-        e |= (vj && by[j] == 0xE1u ? 1u : 0u) << j;
-    }
+    const uint32_t valid = bits4(s0 > k0 ? umin32(s0 - k0, 4u) : 0u, b > k0 ? umin32(b - k0, 4u) : 0u);
+    const uint32_t tabM = zero_bytes4(v4 ^ 0x09090909u), lfM = zero_bytes4(v4 ^ 0x0A0A0A0Au);
+    const uint32_t e1M = zero_bytes4(v4 ^ 0xE1E1E1E1u), escM = zero_bytes4((v4 & 0xE0E0E0E0u) ^ 0xE0E0E0E0u);
+    const uint32_t hb = v4 & 0x80808080u;
+    const uint32_t hi8 = (hb << 1) - (hb >> 7);                   // 0xFF in the bytes >= 0x80
+    const uint32_t c8 = v4 & (~hi8 | 0x1F1F1F1Fu);                // each byte's token count
+    const uint32_t e = valid & e1M;
     const uint32_t ep = vw::shr1(e, st.ecarry);     // escape flags of the previous lane
     st.ecarry = vw::readlane(e, 63);
     const uint32_t c = (e << 4) | ep;               // previous lane's bytes below this lane's
@@ -179,26 +193,21 @@ __device__ __forceinline__ ItemLane scan_window(uint32_t v4, uint32_t b0, uint32
     const uint32_t T = ep;                          // terminator bytes (4 after a flag)
     ItemLane r;
     r.start = valid & ~P & ~T;
-    bool lb = false;
-    uint32_t sum = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < 4; j++) {
-        const uint32_t x = by[j];
-        const bool vj = (valid >> j) & 1u, pj = (P >> j) & 1u, tj = (T >> j) & 1u, sj = (r.start >> j) & 1u;
-        if (vj && pj && !tj) lb = lb || x >= 0x80u || x == '\t' || x == '\n';
-        if (vj && tj) lb = lb || x != '\t';
-        if (sj) lb = lb || ((x & 0xE0u) == 0xE0u && (x != 0xE1u || k0 + j + 4 > s1));   // escape: 3 bytes + TAB/final LF
-        const uint32_t cj = !sj ? 0u : x == 0xE1u ? 1u : x < 0x80u ? x : (x & 0x1Fu);
-        lb = lb || (sj && cj == 0);
-        r.cnt[j] = cj;
-        r.gb[j] = sum;
-        sum += cj;
-    }
-    st.bad = st.bad || vw::ballot(lb) != 0;
+    const int32_t lim = (int32_t)(s1 - k0) - 4;     // an escape at byte j needs j <= lim
+    const uint32_t overM = lim >= 3 ? 0u : lim < 0 ? 0xFu : (0xFu << (lim + 1)) & 0xFu;
+    const uint32_t bad = (P & ~T & (msb4(hb) | tabM | lfM)) | (T & ~tabM) |
+                         (r.start & ((escM & ~e1M) | (e1M & overM) | zero_bytes4(c8)));
+    st.bad = st.bad || vw::ballot((bad & valid) != 0) != 0;
+    const uint32_t s8 = (r.start & 1u) | ((r.start & 2u) << 7) | ((r.start & 4u) << 14) | ((r.start & 8u) << 21);
+    const uint32_t cs = c8 & (s8 * 0xFFu);          // counts of the starts
+    const uint32_t q0 = cs & 0xFFu, q1 = (cs >> 8) & 0xFFu, q2 = (cs >> 16) & 0xFFu, q3 = cs >> 24;
+    const uint32_t sum = q0 + q1 + q2 + q3;
     const uint32_t inc = vw::scan_add(sum);
     const uint32_t base = st.got + (inc - sum);
-#pragma unroll
-    for (uint32_t j = 0; j < 4; j++) r.gb[j] += base;
+    r.gb[0] = base;
+    r.gb[1] = base + q0;
+    r.gb[2] = base + q0 + q1;
+    r.gb[3] = base + q0 + q1 + q2;
     st.got += vw::readlane(inc, 63);
     return r;
 }
