@@ -1223,7 +1223,10 @@ __global__ __launch_bounds__(256) void k_encode_fast(VcfcEncodeArgs a) {
 // one after the other.  A small grid (n / 128 blocks) costs the headline
 // rows, which flag none, next to nothing; 32 rows per wave keep the waves of
 // the law-2 rows (75 % flagged) balanced.
-constexpr uint32_t GEN_ROWS = 32;   // rows per wave of the general kernel
+#ifndef VCFC_GEN_ROWS
+#define VCFC_GEN_ROWS 32
+#endif
+constexpr uint32_t GEN_ROWS = VCFC_GEN_ROWS;   // rows per wave of the general kernel
 #ifndef VCFC_GEN_WPE
 #define VCFC_GEN_WPE 0
 #endif
