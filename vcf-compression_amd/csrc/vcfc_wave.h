@@ -83,14 +83,35 @@ __device__ __forceinline__ uint32_t scan_max(uint32_t v) {
 }
 // inclusive "last non-zero" scan: lane l gets the value of the highest lane
 // <= l whose v is non-zero (0 if none); DPP steps as scan_max
-__device__ __forceinline__ uint32_t last_nz(uint32_t v, uint32_t t) { return v ? v : t; }
+// Written out in asm as scan_add: one compare and one v_cndmask_b32 with the
+// DPP source per step (v stays where it is non-zero, else takes the shifted
+// value; lanes outside the row read 0 / are not written), where hipcc emits
+// a zeroing move, a DPP move, a compare and a select.  The compare and an
+// s_nop 0 are the two wait states before each DPP read of v.
 __device__ __forceinline__ uint32_t scan_last_nz(uint32_t v) {
-    v = last_nz(v, __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false));
-    v = last_nz(v, __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false));
-    v = last_nz(v, __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false));
-    v = last_nz(v, __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false));
-    v = last_nz(v, __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false));
-    v = last_nz(v, __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false));
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_cmp_ne_u32 vcc, 0, %0\n\t"
+        "s_nop 0\n\t"
+        "v_cndmask_b32_dpp %0, %0, %0, vcc row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_cmp_ne_u32 vcc, 0, %0\n\t"
+        "s_nop 0\n\t"
+        "v_cndmask_b32_dpp %0, %0, %0, vcc row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_cmp_ne_u32 vcc, 0, %0\n\t"
+        "s_nop 0\n\t"
+        "v_cndmask_b32_dpp %0, %0, %0, vcc row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_cmp_ne_u32 vcc, 0, %0\n\t"
+        "s_nop 0\n\t"
+        "v_cndmask_b32_dpp %0, %0, %0, vcc row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_cmp_ne_u32 vcc, 0, %0\n\t"
+        "s_nop 0\n\t"
+        "v_cndmask_b32_dpp %0, %0, %0, vcc row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+        "v_cmp_ne_u32 vcc, 0, %0\n\t"
+        "s_nop 0\n\t"
+        "v_cndmask_b32_dpp %0, %0, %0, vcc row_bcast:31 row_mask:0xc bank_mask:0xf"
+        : "+v"(v)
+        :
+        : "vcc");
     return v;
 }
 // byte select: result byte i = byte sel[i] of (s0:s1) for sel 0..7, 0x0C -> 0x00
