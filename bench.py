@@ -147,8 +147,10 @@ def cpu_baseline(rows, torch, args):
     return (res, out, k)
 
 
-def load_pmc(workload_key):
-    p = os.path.join(REPO, "profiles", "pmc_k_encode.json")
+def load_pmc(workload_key, name="pmc_k_encode.json"):
+    """HBM bytes per launch from a committed rocprofv3 PMC summary
+    (profiles/<name>) when it was measured on this workload, else None."""
+    p = os.path.join(REPO, "profiles", name)
     if not os.path.exists(p):
         return None
     try:
@@ -285,7 +287,8 @@ def bench_decode(args, torch, vcfc, workload):
                       "record_bytes": rec_bytes, "line_bytes": total},
            "roofline": {"kernel": "k_dec_plan + k_dec_write", "bound": "hbm",
                         "achieved": round(alg / (ev_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(alg / (ev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                        "frac": round(alg / (ev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                        "traffic": load_pmc("%s/%dx%d" % (law_name(args.law), S, n), "pmc_k_dec.json"),
                         "algorithmic_bytes_per_launch": alg, "avg_launch_ms": round(ev_ms, 4)},
            "output_identical_to_input_rows": identical}
     if not args.no_cpu_baseline:
