@@ -603,9 +603,6 @@ __device__ __forceinline__ void esc8(const uint32_t (&d)[TPL8], int32_t t0, int3
     const uint32_t sH = (xH | (xH >> 1) | (xH >> 2) | (cbH >> 2)) & 0x01010101u;
     const uint32_t sb = stride4(sL, sH) & vbits;
     const uint32_t eb = stride4((cbL >> 2) & 0x01010101u, (cbH >> 2) & 0x01010101u) & vbits;   // escape slots
-#ifdef VCFC_ESC_EMIT1
-    const uint32_t cp4 = stride4(cpL & 0x07070707u, cpH & 0x07070707u);       // class of slot j-1 at bits 4j
-#endif
     const uint32_t lane_rs = sb ? (uint32_t)(t0 + 8) - ((uint32_t)__builtin_clz(sb) >> 2) : 0u;
     const uint32_t incl = vw::scan_max(lane_rs);
     const uint32_t rin = vw::umax(vw::shr1z(incl), f.prs);
@@ -640,25 +637,6 @@ __device__ __forceinline__ void esc8(const uint32_t (&d)[TPL8], int32_t t0, int3
     uint8_t *const dm = r.lds + RING_DUMMY + 4u * vw::lane_id();
     *(full ? lb : dm) = (uint8_t)(m0 | cap);
     uint32_t o = full ? 1u : 0u;
-#ifdef VCFC_ESC_EMIT1
-    uint32_t jp = 0;
-#pragma unroll
-    for (int j = 0; j < (int)TPL8; j++) {
-        const bool s = (sb >> (4 * j)) & 1u;
-        const bool e = (eb >> (4 * j)) & 1u;
-        const uint32_t pc = (cp4 >> (4 * j)) & 7u;
-        const bool first = (uint32_t)j == j1;
-        const bool lead = s && (!first || lead1);
-        const uint32_t b = first ? b1
-                         : (pc == CLS_ESC ? 0x09u : (vw::perm(0x80C0A000u, 0x80C0A000u, pc) | ((uint32_t)j - jp)));
-        *(lead ? lb + o : dm) = (uint8_t)b;
-        o += lead ? 1u : 0u;
-        const uint32_t pay = (d[j] << 8) | 0xE1u;   // 0xE1, then the token's three bytes
-        __builtin_memcpy(e ? lb + o : dm, &pay, 4);
-        o += e ? 4u : 0u;
-        if (s) jp = (uint32_t)j;
-    }
-#else
     // The first start's lead byte follows the full byte (nothing else comes
     // before the first start: escapes are starts).  Later starts close the
     // run begun at the previous start: lead = mask(class) + length, where the
@@ -686,7 +664,6 @@ __device__ __forceinline__ void esc8(const uint32_t (&d)[TPL8], int32_t t0, int3
         o += 4u * (uint32_t)e;
         njp = s ? -j : njp;
     }
-#endif
     const bool wrap = base + cnt > RING;
     if (vw::ballot(wrap)) {
         if (wrap) {
