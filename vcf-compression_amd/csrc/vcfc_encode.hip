@@ -40,7 +40,7 @@ constexpr uint32_t RMASK = RING - 1;
 // start afterwards) + one dummy word per lane (branch-free stores)
 constexpr uint32_t RING_TAIL = 64;
 constexpr uint32_t RING_DUMMY = RING + RING_TAIL;
-constexpr uint32_t RING_STRIDE = RING_DUMMY + 4 * 64;
+constexpr uint32_t RING_STRIDE = RING_DUMMY + 4 * 64;   // (one dummy word is used: see esc8)
 constexpr uint32_t BURST = 1024;       // flush granule (64 lanes x 16 B)
 constexpr uint32_t CLS_ESC = 4, CLS_NONE = 5;
 
@@ -314,7 +314,7 @@ __device__ bool gt_general(const Chunk &cur, int32_t tf, FastState &f, Ring &r) 
     for (int j = 0; j < (int)TPL; j++) d[j] = vw::alignbyte(cur.w(j + 1), cur.w(j), phi);
     const int32_t t0 = tf + (int32_t)(TPL * l);
     const uint32_t u0 = (uint32_t)(t0 + 1);
-    const uint32_t dummy = RING_DUMMY + 4 * l;
+    const uint32_t dummy = RING_DUMMY;   // shared dummy word (see esc8)
     bool v[TPL];
 #pragma unroll
     for (int j = 0; j < (int)TPL; j++) v[j] = (uint32_t)(t0 + j) < T;
@@ -634,7 +634,11 @@ __device__ __forceinline__ void esc8(const uint32_t (&d)[TPL8], int32_t t0, int3
 #endif
     const uint32_t base = (r.wpos + incl2 - cnt) & RMASK;
     uint8_t *const lb = r.lds + base;
-    uint8_t *const dm = r.lds + RING_DUMMY + 4u * vw::lane_id();
+    // Stores that emit nothing go to one dummy word shared by the wave:
+    // same-address stores add no bank conflict, where a dummy word per lane
+    // collides with the real stores of other lanes on the same banks (law 0:
+    // 3.09 -> 2.64 ms k_encode in an A/B, profiles/r02/ab/ab_dummy_law0.txt).
+    uint8_t *const dm = r.lds + RING_DUMMY;
     *(full ? lb : dm) = (uint8_t)(m0 | cap);
     uint32_t o = full ? 1u : 0u;
     // The first start's lead byte follows the full byte (nothing else comes
@@ -647,7 +651,7 @@ __device__ __forceinline__ void esc8(const uint32_t (&d)[TPL8], int32_t t0, int3
     *(lead1 ? lb + o : dm) = (uint8_t)b1;
     o += lead1 ? 1u : 0u;
     const uint32_t sbr = sb & (sb - 1u);   // starts after the first
-    const uint32_t dmi = RING_DUMMY + 4u * vw::lane_id();
+    const uint32_t dmi = RING_DUMMY;
     const int32_t ldm = (int32_t)base - (int32_t)dmi;
     const uint32_t mL = vw::perm(0x08u, 0x80C0A000u, cpL & 0x07070707u) + 0x03020100u;   // mask + slot index
     const uint32_t mH = vw::perm(0x08u, 0x80C0A000u, cpH & 0x07070707u) + 0x07060504u;
@@ -959,7 +963,7 @@ __device__ uint32_t encode_general(const uint8_t *__restrict__ line, uint32_t le
                 const uint32_t inc2 = vw::scan_add(cnt);
                 const uint32_t base = (r.wpos + inc2 - cnt) & RMASK;
                 uint8_t *const lb = r.lds + base;
-                uint8_t *const dm = r.lds + RING_DUMMY + 4u * l;
+                uint8_t *const dm = r.lds + RING_DUMMY;   // shared dummy word (see esc8)
                 uint32_t o = 0;
 #pragma unroll
                 for (int i = 0; i < 16; i++) {
@@ -1074,7 +1078,7 @@ __device__ uint32_t encode_general(const uint8_t *__restrict__ line, uint32_t le
         const uint32_t inc2 = vw::scan_add(cnt);
         const uint32_t base = (r.wpos + inc2 - cnt) & RMASK;
         uint8_t *const lb = r.lds + base;
-        uint8_t *const dm = r.lds + RING_DUMMY + 4u * l;
+        uint8_t *const dm = r.lds + RING_DUMMY;   // shared dummy word (see esc8)
         // pass 1: the raw bytes, each at its place after the bytes inserted before it
         uint32_t o = 0;
 #pragma unroll
