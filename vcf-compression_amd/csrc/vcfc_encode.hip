@@ -30,6 +30,10 @@
 #include <hip/hip_runtime.h>
 #include <vcfc_wave.h>   // angle brackets: tests/simt_emu shadows it
 #include "vcfc_device.h"
+#include <cstdlib>
+
+// most row pieces of one encode (VCFC_PIECES, see vcfc_encode_device)
+#define VCFC_PIECES_MAX 16u
 
 namespace {
 
@@ -1173,14 +1177,14 @@ __device__ __forceinline__ bool row_setup(const VcfcEncodeArgs &a, uint64_t row,
 #define VCFC_FAST_WPE 6
 #endif
 #if VCFC_FAST_WPE
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VCFC_FAST_WPE, VCFC_FAST_WPE))) void k_encode_fast(VcfcEncodeArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VCFC_FAST_WPE, VCFC_FAST_WPE))) void k_encode_fast(VcfcEncodeArgs a, uint64_t row_lo, uint64_t row_hi) {
 #else
-__global__ __launch_bounds__(256) void k_encode_fast(VcfcEncodeArgs a) {
+__global__ __launch_bounds__(256) void k_encode_fast(VcfcEncodeArgs a, uint64_t row_lo, uint64_t row_hi) {
 #endif
     __shared__ __attribute__((aligned(16))) uint8_t lds[K1_WAVES * RING_STRIDE];
     const uint32_t wave = vw::readfirst(threadIdx.x >> 6);   // wave-uniform: scalar row/len/loop control
-    const uint64_t row = (uint64_t)blockIdx.x * K1_WAVES + wave;
-    if (row >= a.n) return;
+    const uint64_t row = row_lo + (uint64_t)blockIdx.x * K1_WAVES + wave;   // rows [row_lo, row_hi): one piece
+    if (row >= row_hi) return;
 #ifdef VCFC_ROW_TIMES
     const uint64_t t_start = wall_clock64();
 #endif
@@ -1212,15 +1216,15 @@ constexpr uint32_t GEN_ROWS = VCFC_GEN_ROWS;   // rows per wave of the general k
 #define VCFC_GEN_WPE 0
 #endif
 #if VCFC_GEN_WPE
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VCFC_GEN_WPE, VCFC_GEN_WPE))) void k_encode_general(VcfcEncodeArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VCFC_GEN_WPE, VCFC_GEN_WPE))) void k_encode_general(VcfcEncodeArgs a, uint64_t row_lo, uint64_t row_hi) {
 #else
-__global__ __launch_bounds__(256) void k_encode_general(VcfcEncodeArgs a) {
+__global__ __launch_bounds__(256) void k_encode_general(VcfcEncodeArgs a, uint64_t row_lo, uint64_t row_hi) {
 #endif
     __shared__ __attribute__((aligned(16))) uint8_t lds[K1_WAVES * RING_STRIDE];
     const uint32_t wave = vw::readfirst(threadIdx.x >> 6);
-    const uint64_t row0 = ((uint64_t)blockIdx.x * K1_WAVES + wave) * GEN_ROWS;
+    const uint64_t row0 = row_lo + ((uint64_t)blockIdx.x * K1_WAVES + wave) * GEN_ROWS;
     const uint32_t l = vw::lane_id();
-    const bool flagged = l < GEN_ROWS && row0 + l < a.n && a.rec_size[row0 + l] == VCFCD_RETRY;
+    const bool flagged = l < GEN_ROWS && row0 + l < row_hi && a.rec_size[row0 + l] == VCFCD_RETRY;
     uint64_t todo = vw::ballot(flagged);
     while (todo) {
         const uint64_t row = row0 + (uint64_t)__builtin_ctzll(todo);
@@ -1354,14 +1358,20 @@ __global__ __launch_bounds__(256) void k_compact_out(const uint8_t *__restrict__
                                                      const uint64_t *__restrict__ slot_off,
                                                      const uint64_t *__restrict__ rec_off, uint64_t n,
                                                      const uint32_t *__restrict__ tile_first,
-                                                     uint8_t *__restrict__ out, uint64_t out_cap) {
+                                                     uint8_t *__restrict__ out, uint64_t out_cap,
+                                                     uint64_t row_lo, bool last) {
+    // Rows [row_lo, n) of one piece (the whole batch: row_lo = 0, last).  A
+    // piece writes the tiles from the one holding its first byte (which may
+    // begin in the previous piece: that piece stops short of it) to the last
+    // tile it completes; the last piece also writes the final partial tile.
     const uint32_t l = vw::lane_id();
     const uint64_t g = (uint64_t)blockIdx.x * 4 + vw::readfirst(threadIdx.x >> 6);
     const uint64_t G = (uint64_t)gridDim.x * 4;
     const uint64_t total = rec_off[n];
     const uint64_t lim = total < out_cap ? total : out_cap;
-    const uint64_t ntile = (lim + CT - 1) / CT;
-    for (uint64_t t = g; t < ntile; t += G) {
+    const uint64_t ntile = last ? (lim + CT - 1) / CT : (total < out_cap ? total / CT : (lim + CT - 1) / CT);
+    const uint64_t t0 = row_lo ? rec_off[row_lo] / CT : 0;
+    for (uint64_t t = t0 + g; t < ntile; t += G) {
         const uint64_t o0 = t * CT;
         const uint64_t r0 = tile_first[t];
         // rows r0 .. r0 + 63: their starts (lane j holds row r0 + j); rows
@@ -1535,7 +1545,10 @@ __device__ __forceinline__ void lb_store(uint64_t *p, uint64_t v) {
 template <int MODE, bool TILES>
 __global__ __launch_bounds__(256) void k_scan_lb(const uint32_t *__restrict__ in, uint64_t n, uint32_t *ticket,
                                                  uint64_t *flags, uint64_t *__restrict__ out,
-                                                 uint32_t *__restrict__ tile_first, uint64_t out_cap, uint64_t *err) {
+                                                 uint32_t *__restrict__ tile_first, uint64_t out_cap, uint64_t *err,
+                                                 const uint64_t *base_in, uint64_t row_base) {
+    // base_in (a piece after the first): the scan starts at *base_in, the
+    // previous piece's total; row_base: the piece's first row (error codes)
     __shared__ uint64_t sh[SCAN_THREADS];
     __shared__ uint32_t s_tile;
     __shared__ uint64_t s_excl;
@@ -1554,8 +1567,9 @@ __global__ __launch_bounds__(256) void k_scan_lb(const uint32_t *__restrict__ in
     const uint64_t texcl = block_excl_scan_u64(sum, sh, &agg);
     if (threadIdx.x < 64) {   // wave 0: publish the aggregate, look back
         const uint32_t l = threadIdx.x;
-        if (l == 0) lb_store(flags + tile, (tile == 0 ? LB_INC : LB_AGG) | agg);
-        uint64_t excl = 0;
+        const uint64_t b0 = (tile == 0 && base_in) ? *base_in : 0;
+        if (l == 0) lb_store(flags + tile, (tile == 0 ? LB_INC : LB_AGG) | (b0 + agg));
+        uint64_t excl = b0;
         if (tile > 0) {
             int64_t p = (int64_t)tile - 1;   // the window covers tiles p, p - 1, ..., p - 63
             for (;;) {
@@ -1593,8 +1607,8 @@ __global__ __launch_bounds__(256) void k_scan_lb(const uint32_t *__restrict__ in
             out[r] = run;
             if (TILES) {
                 const uint64_t b = run + vals[i];
-                if (b > out_cap) atomicMin((unsigned long long *)err, (unsigned long long)((r << 8) | VCFCD_E_NOSPACE));
-                for (uint64_t t = (run + CT - 1) / CT; t * CT < b; t++) tile_first[t] = (uint32_t)r;
+                if (b > out_cap) atomicMin((unsigned long long *)err, (unsigned long long)(((row_base + r) << 8) | VCFCD_E_NOSPACE));
+                for (uint64_t t = (run + CT - 1) / CT; t * CT < b; t++) tile_first[t] = (uint32_t)(row_base + r);
             }
             if (r + 1 == n) out[n] = run + vals[i];
         }
@@ -1617,7 +1631,7 @@ VcfcWorkspaceLayout vcfc_encode_workspace_layout(uint64_t n, uint64_t total_line
     const uint64_t nt = (n + SCAN_TILE - 1) / SCAN_TILE + 1;
     L.lb = o;
     L.retry_count = o + 8;
-    L.lb_bytes = 16 + 16 * nt;
+    L.lb_bytes = 16 + 16 * nt + 12 * VCFC_PIECES_MAX;   // + per-piece tickets and flag windows
     o = al(o + L.lb_bytes);
     L.tile_first = o; o = al(o + 4 * (vcfc_record_bound(n, total_line_bytes) / CT + 2));
     L.prim = o; o = al(o + (uint64_t)VCFC_PRIM * n);
@@ -1630,40 +1644,110 @@ VcfcWorkspaceLayout vcfc_encode_workspace_layout(uint64_t n, uint64_t total_line
     return L;
 }
 
+// Pieces (VCFC_PIECES, default 1): the batch's rows in P consecutive
+// pieces; piece j's size scan and compaction run on a second stream while
+// piece j + 1 encodes, so the compaction's HBM traffic fills the encoder's
+// tail and its issue-bound stretches instead of following it.
+static int encode_pieces() {
+    const char *e = getenv("VCFC_PIECES");
+    const int v = e ? atoi(e) : 1;
+    return v < 1 ? 1 : v > (int)VCFC_PIECES_MAX ? (int)VCFC_PIECES_MAX : v;
+}
+
+// per-thread second stream and events of the piece pipeline (one device)
+struct PieceStreams {
+    int dev = -1;
+    hipStream_t s2 = nullptr;
+    hipEvent_t ev[VCFC_PIECES_MAX + 1] = {};
+};
+static hipError_t piece_streams(PieceStreams *&ps) {
+    static thread_local PieceStreams t;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (t.dev != dev) {
+        if ((e = hipStreamCreateWithFlags(&t.s2, hipStreamNonBlocking)) != hipSuccess) return e;
+        for (auto &x : t.ev)
+            if ((e = hipEventCreateWithFlags(&x, hipEventDisableTiming)) != hipSuccess) return e;
+        t.dev = dev;
+    }
+    ps = &t;
+    return hipSuccess;
+}
+
 hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t s, hipEvent_t *ev) {
     hipError_t e = hipMemsetAsync(a.err, 0xFF, 8, s);
     if (e != hipSuccess) return e;
     if (a.n == 0) return hipMemsetAsync(a.rec_off, 0, 8, s);
     const uint64_t nt = (a.n + SCAN_TILE - 1) / SCAN_TILE;   // scan tiles
+    // lb: tickets (slot scan, size scan), retry counter, slot-scan flags
+    // (nt + 1), size-scan flags (nt + 1 + one spare per piece), piece tickets
     uint32_t *tickets = reinterpret_cast<uint32_t *>(a.lb);
     uint64_t *flags_a = reinterpret_cast<uint64_t *>(a.lb + 16), *flags_b = flags_a + nt + 1;
-    if ((e = hipMemsetAsync(a.lb, 0, 16 + 16 * (nt + 1), s)) != hipSuccess) return e;   // (also retry_count)
+    uint32_t *ptickets = reinterpret_cast<uint32_t *>(flags_b + nt + 1 + VCFC_PIECES_MAX);
+    if ((e = hipMemsetAsync(a.lb, 0, 16 + 16 * (nt + 1) + 12 * VCFC_PIECES_MAX, s)) != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[0], s);
 #ifdef VCFC_SCAN3
     e = launch_scan<1>(a.line_len, a.n, a.partials, a.slot_off, s);
     if (e != hipSuccess) return e;
 #else
     hipLaunchKernelGGL((k_scan_lb<1, false>), dim3((unsigned)nt), dim3(SCAN_THREADS), 0, s, a.line_len, a.n, tickets,
-                       flags_a, a.slot_off, nullptr, 0, nullptr);
+                       flags_a, a.slot_off, nullptr, 0, nullptr, nullptr, 0);
     if ((e = hipGetLastError()) != hipSuccess) return e;
 #endif
     if (ev) (void)hipEventRecord(ev[1], s);
-    hipLaunchKernelGGL(k_encode_fast, dim3((unsigned)((a.n + K1_WAVES - 1) / K1_WAVES)), dim3(64 * K1_WAVES), 0, s, a);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    {
-        // GEN_ROWS rows per wave (see k_encode_general)
-        const uint64_t per_block = (uint64_t)K1_WAVES * GEN_ROWS;
-        hipLaunchKernelGGL(k_encode_general, dim3((unsigned)((a.n + per_block - 1) / per_block)), dim3(64 * K1_WAVES), 0,
-                           s, a);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
+    const uint64_t per_gblock = (uint64_t)K1_WAVES * GEN_ROWS;   // GEN_ROWS rows per wave (see k_encode_general)
+    // a grid of 8 waves per SIMD striding over the output tiles (uniform work)
+    const uint64_t tiles = vcfc_record_bound(a.n, a.line_bytes_hint) / CT + 1;
+    const uint64_t cblocks = tiles < 8192 ? (tiles + 3) / 4 : 2048;
+#if !defined(VCFC_SCAN3) && !defined(VCFC_ROW_COMPACT)
+    int P = encode_pieces();
+    if ((uint64_t)P * SCAN_TILE > a.n) P = 1;   // a piece holds at least one scan tile
+    if (P > 1) {
+        PieceStreams *ps = nullptr;
+        if ((e = piece_streams(ps)) != hipSuccess) return e;
+        for (int j = 0; j < P; j++) {
+            // piece bounds on scan tiles: piece j's flags start at tile R_j / SCAN_TILE + j
+            const uint64_t lo = a.n * (uint64_t)j / (uint64_t)P / SCAN_TILE * SCAN_TILE;
+            const uint64_t hi = j + 1 == P ? a.n : a.n * (uint64_t)(j + 1) / (uint64_t)P / SCAN_TILE * SCAN_TILE;
+            const uint64_t m = hi - lo, mt = (m + SCAN_TILE - 1) / SCAN_TILE;
+            hipLaunchKernelGGL(k_encode_fast, dim3((unsigned)((m + K1_WAVES - 1) / K1_WAVES)), dim3(64 * K1_WAVES), 0, s,
+                               a, lo, hi);
+            hipLaunchKernelGGL(k_encode_general, dim3((unsigned)((m + per_gblock - 1) / per_gblock)),
+                               dim3(64 * K1_WAVES), 0, s, a, lo, hi);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+            if ((e = hipEventRecord(ps->ev[j], s)) != hipSuccess) return e;
+            if ((e = hipStreamWaitEvent(ps->s2, ps->ev[j], 0)) != hipSuccess) return e;
+            hipLaunchKernelGGL((k_scan_lb<0, true>), dim3((unsigned)mt), dim3(SCAN_THREADS), 0, ps->s2, a.rec_size + lo,
+                               m, ptickets + j, flags_b + lo / SCAN_TILE + j, a.rec_off + lo, a.tile_first, a.out_cap,
+                               a.err, j ? a.rec_off + lo : nullptr, lo);
+            hipLaunchKernelGGL(k_compact_out, dim3((unsigned)cblocks), dim3(256), 0, ps->s2, a.prim, a.slots,
+                               a.slot_off, a.rec_off, hi, a.tile_first, a.out, a.out_cap, lo, j + 1 == P);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+        }
+        if (ev) {
+            (void)hipEventRecord(ev[2], s);   // encode done; the compaction of the last piece follows
+            (void)hipEventRecord(ev[3], s);
+        }
+        if ((e = hipEventRecord(ps->ev[P], ps->s2)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(s, ps->ev[P], 0)) != hipSuccess) return e;
+        if (ev) (void)hipEventRecord(ev[4], s);
+        return hipSuccess;
     }
+#endif
+    hipLaunchKernelGGL(k_encode_fast, dim3((unsigned)((a.n + K1_WAVES - 1) / K1_WAVES)), dim3(64 * K1_WAVES), 0, s, a,
+                       (uint64_t)0, a.n);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_encode_general, dim3((unsigned)((a.n + per_gblock - 1) / per_gblock)), dim3(64 * K1_WAVES), 0,
+                       s, a, (uint64_t)0, a.n);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[2], s);
 #if defined(VCFC_SCAN3) || defined(VCFC_ROW_COMPACT)
     e = launch_scan<0>(a.rec_size, a.n, a.partials, a.rec_off, s);
     if (e != hipSuccess) return e;
 #else
     hipLaunchKernelGGL((k_scan_lb<0, true>), dim3((unsigned)nt), dim3(SCAN_THREADS), 0, s, a.rec_size, a.n,
-                       tickets + 1, flags_b, a.rec_off, a.tile_first, a.out_cap, a.err);
+                       tickets + 1, flags_b, a.rec_off, a.tile_first, a.out_cap, a.err, nullptr, 0);
     if ((e = hipGetLastError()) != hipSuccess) return e;
 #endif
     if (ev) (void)hipEventRecord(ev[3], s);
@@ -1685,13 +1769,8 @@ hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t s, hipEvent_t
                        a.tile_first, a.err);
     if ((e = hipGetLastError()) != hipSuccess) return e;
 #endif
-    {
-        // a grid of 8 waves per SIMD striding over the tiles (uniform work)
-        const uint64_t tiles = vcfc_record_bound(a.n, a.line_bytes_hint) / CT + 1;
-        const uint64_t blocks = tiles < 8192 ? (tiles + 3) / 4 : 2048;
-        hipLaunchKernelGGL(k_compact_out, dim3((unsigned)blocks), dim3(256), 0, s, a.prim, a.slots, a.slot_off,
-                           a.rec_off, a.n, a.tile_first, a.out, a.out_cap);
-    }
+    hipLaunchKernelGGL(k_compact_out, dim3((unsigned)cblocks), dim3(256), 0, s, a.prim, a.slots, a.slot_off,
+                       a.rec_off, a.n, a.tile_first, a.out, a.out_cap, (uint64_t)0, true);
 #endif
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[4], s);
