@@ -528,7 +528,11 @@ __device__ __forceinline__ void write_one(const VcfcDecodeArgs &a, uint64_t i, u
 #pragma unroll
             for (uint32_t j = 0; j < 4; j++) {
                 const uint32_t o = ws[j] - j0;
+#ifdef VCFC_DEC_SHARED_DUMMY
+                W[o < TB ? o : TB] = w[j];   // one dummy word shared by the wave
+#else
                 W[o < TB ? o : TB + l] = w[j];
+#endif
             }
             if (st.got < j0 + TB || j0 + TB > S) break;   // the tile is not complete yet
             tile_out(TB);
