@@ -41,10 +41,12 @@ constexpr int K1_WAVES = 4;            // rows per 256-thread block
 constexpr uint32_t RING = 4096;        // per-wave LDS ring (bytes)
 constexpr uint32_t RMASK = RING - 1;
 // + a 64-byte tail (a lane's bytes written past the ring end, moved to its
-// start afterwards) + one dummy word per lane (branch-free stores)
+// start afterwards; a lane writes at most 48 bytes per step) + one dummy word
+// shared by the wave for the stores that emit nothing (branch-free stores,
+// see esc8), padded to keep the next wave's ring 16-B aligned
 constexpr uint32_t RING_TAIL = 64;
 constexpr uint32_t RING_DUMMY = RING + RING_TAIL;
-constexpr uint32_t RING_STRIDE = RING_DUMMY + 4 * 64;   // (one dummy word is used: see esc8)
+constexpr uint32_t RING_STRIDE = RING_DUMMY + 16;
 constexpr uint32_t BURST = 1024;       // flush granule (64 lanes x 16 B)
 constexpr uint32_t CLS_ESC = 4, CLS_NONE = 5;
 
