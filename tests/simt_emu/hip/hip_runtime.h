@@ -49,6 +49,9 @@ inline hipError_t hipEventCreateWithFlags(hipEvent_t *e, unsigned) { *e = nullpt
 inline hipError_t hipEventDestroy(hipEvent_t) { return hipSuccess; }
 inline hipError_t hipStreamWaitEvent(hipStream_t, hipEvent_t, unsigned) { return hipSuccess; }
 inline hipError_t hipGetDevice(int *d) { *d = 0; return hipSuccess; }
+#define hipDeviceAttributeMultiprocessorCount 0
+inline hipError_t hipDeviceGetAttribute(int *v, int, int) { *v = 4; return hipSuccess; }
+template <class F> inline hipError_t hipOccupancyMaxActiveBlocksPerMultiprocessor(int *n, F, int, size_t) { *n = 2; return hipSuccess; }
 
 inline void __syncthreads() { emu::collective(emu::OP_SYNCTHREADS, 0, 0, 0); }
 

@@ -1224,13 +1224,27 @@ __global__ __launch_bounds__(256) void k_encode_general(VcfcEncodeArgs a, uint64
 #endif
     __shared__ __attribute__((aligned(16))) uint8_t lds[K1_WAVES * RING_STRIDE];
     const uint32_t wave = vw::readfirst(threadIdx.x >> 6);
-    const uint64_t row0 = row_lo + ((uint64_t)blockIdx.x * K1_WAVES + wave) * GEN_ROWS;
     const uint32_t l = vw::lane_id();
+#ifdef VCFC_GEN_PERSIST
+    // a resident grid (every wave starts at once): wave w takes rows
+    // row_lo + w + k W, the flags of 64 of them per load, so the flagged rows
+    // spread evenly over the waves and no late round of waves runs alone
+    const uint64_t W = (uint64_t)gridDim.x * K1_WAVES, w = (uint64_t)blockIdx.x * K1_WAVES + wave;
+    for (uint64_t k0 = 0; row_lo + w + k0 * W < row_hi; k0 += 64) {
+    const uint64_t rl = row_lo + w + (k0 + l) * W;
+    const bool flagged = rl < row_hi && a.rec_size[rl] == VCFCD_RETRY;
+    uint64_t todo = vw::ballot(flagged);
+    while (todo) {
+        const uint64_t row = row_lo + w + (k0 + (uint64_t)__builtin_ctzll(todo)) * W;
+        todo &= todo - 1;
+#else
+    const uint64_t row0 = row_lo + ((uint64_t)blockIdx.x * K1_WAVES + wave) * GEN_ROWS;
     const bool flagged = l < GEN_ROWS && row0 + l < row_hi && a.rec_size[row0 + l] == VCFCD_RETRY;
     uint64_t todo = vw::ballot(flagged);
     while (todo) {
         const uint64_t row = row0 + (uint64_t)__builtin_ctzll(todo);
         todo &= todo - 1;
+#endif
 #ifdef VCFC_COUNT_RETRIES   // test builds (tests/simt_emu): rows that took the general kernel
         if (l == 0) atomicAdd(a.retry_count, 1u);
 #endif
@@ -1243,6 +1257,31 @@ __global__ __launch_bounds__(256) void k_encode_general(VcfcEncodeArgs a, uint64
             if (st != VCFCD_OK) atomicMin((unsigned long long *)a.err, (unsigned long long)((row << 8) | st));
         }
     }
+#ifdef VCFC_GEN_PERSIST
+    }
+#endif
+}
+
+// blocks of k_encode_general to launch for m rows
+static uint64_t general_blocks(uint64_t m) {
+#ifdef VCFC_GEN_PERSIST
+    static int resident = 0;   // blocks resident on the whole device (same for every device of a node)
+    if (!resident) {
+        int dev = 0, cus = 0, per_cu = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_encode_general, 64 * K1_WAVES, 0) != hipSuccess ||
+            cus <= 0 || per_cu <= 0)
+            resident = 1024;
+        else
+            resident = cus * per_cu;
+    }
+    const uint64_t need = (m + K1_WAVES - 1) / K1_WAVES;
+    return need < (uint64_t)resident ? need : (uint64_t)resident;
+#else
+    const uint64_t per_block = (uint64_t)K1_WAVES * GEN_ROWS;   // GEN_ROWS rows per wave
+    return (m + per_block - 1) / per_block;
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -1698,7 +1737,6 @@ hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t s, hipEvent_t
     if ((e = hipGetLastError()) != hipSuccess) return e;
 #endif
     if (ev) (void)hipEventRecord(ev[1], s);
-    const uint64_t per_gblock = (uint64_t)K1_WAVES * GEN_ROWS;   // GEN_ROWS rows per wave (see k_encode_general)
     // a grid of 8 waves per SIMD striding over the output tiles (uniform work)
     const uint64_t tiles = vcfc_record_bound(a.n, a.line_bytes_hint) / CT + 1;
     const uint64_t cblocks = tiles < 8192 ? (tiles + 3) / 4 : 2048;
@@ -1715,8 +1753,8 @@ hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t s, hipEvent_t
             const uint64_t m = hi - lo, mt = (m + SCAN_TILE - 1) / SCAN_TILE;
             hipLaunchKernelGGL(k_encode_fast, dim3((unsigned)((m + K1_WAVES - 1) / K1_WAVES)), dim3(64 * K1_WAVES), 0, s,
                                a, lo, hi);
-            hipLaunchKernelGGL(k_encode_general, dim3((unsigned)((m + per_gblock - 1) / per_gblock)),
-                               dim3(64 * K1_WAVES), 0, s, a, lo, hi);
+            hipLaunchKernelGGL(k_encode_general, dim3((unsigned)general_blocks(m)), dim3(64 * K1_WAVES), 0, s, a, lo,
+                               hi);
             if ((e = hipGetLastError()) != hipSuccess) return e;
             if ((e = hipEventRecord(ps->ev[j], s)) != hipSuccess) return e;
             if ((e = hipStreamWaitEvent(ps->s2, ps->ev[j], 0)) != hipSuccess) return e;
@@ -1740,8 +1778,8 @@ hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t s, hipEvent_t
     hipLaunchKernelGGL(k_encode_fast, dim3((unsigned)((a.n + K1_WAVES - 1) / K1_WAVES)), dim3(64 * K1_WAVES), 0, s, a,
                        (uint64_t)0, a.n);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_encode_general, dim3((unsigned)((a.n + per_gblock - 1) / per_gblock)), dim3(64 * K1_WAVES), 0,
-                       s, a, (uint64_t)0, a.n);
+    hipLaunchKernelGGL(k_encode_general, dim3((unsigned)general_blocks(a.n)), dim3(64 * K1_WAVES), 0, s, a,
+                       (uint64_t)0, a.n);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[2], s);
 #if defined(VCFC_SCAN3) || defined(VCFC_ROW_COMPACT)
