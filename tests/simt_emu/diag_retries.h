@@ -1,0 +1,8 @@
+// TEST INFRASTRUCTURE ONLY: diagnostic hooks for the emulator build -- count
+// the rows the fast kernel hands to k_encode_general (emu_api.cpp reads it).
+#pragma once
+#define VCFC_DIAG_ROW_BEGIN()
+#define VCFC_DIAG_ROW_END(a, row)
+#define VCFC_DIAG_GENERAL_ROW(a) \
+    if (vw::lane_id() == 0) atomicAdd((a).retry_count, 1u)
+#define VCFC_DIAG_WS_BYTES(n) 0ull

@@ -82,3 +82,136 @@ def test_full_batch_every_record_and_round_trip(torch, vcfc, law):
     assert e == vcfc.NO_ERROR, hex(e)
     assert int(loff[n].item()) == rows.total_bytes
     assert bool(torch.equal(lines[:rows.total_bytes], rows.buf[:rows.total_bytes]))
+
+
+def _digest_check(torch, vcfc, rows, out, rec, n):
+    """Every record digest of the batch's first n rows against the threaded oracle."""
+    dev = rows.buf.device
+    rec_t = torch.from_numpy(rec[:n + 1].astype(np.int64)).to(dev)
+    h = torch.empty(n, dtype=torch.int64, device=dev)
+    vcfc.record_hash_device(out.data_ptr(), rec_t.data_ptr(), n, h.data_ptr(),
+                            torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize(dev)
+    got_h = h.cpu().numpy().view(np.uint64)
+    buf = rows.buf[:rows.total_bytes].cpu().numpy()
+    st, size, want_h = G.oracle_encode_rows_hash(buf, rows.line_off.cpu().numpy()[:n], rows.line_len.cpu().numpy()[:n],
+                                                 threads=threads())
+    del buf
+    assert (st == 0).all()
+    bad = np.nonzero((size.astype(np.uint64) != np.diff(rec[:n + 1])) | (want_h != got_h))[0]
+    assert bad.size == 0, "rows differ from the oracle: %s" % bad[:10].tolist()
+    return rec_t
+
+
+@pytest.mark.parametrize("law,n", [(1, 20_000), (0, 5_000)])
+def test_biobank_rows_every_record_and_round_trip(torch, vcfc, law, n):
+    """BASELINE configs[3] rows (100,000 samples = 400 KB per row; 8 GB of
+    lines for law 1): every record against the oracle (each row streams ~200
+    2 KiB chunks through the LDS ring, wrapping it ~100 times and flushing
+    many 1 KiB bursts), plus the decode round trip at S = 100,000."""
+    import workload
+    from test_gpu_encode import _device_encode
+    S = 100_000
+    dev = torch.device("cuda:0")
+    rows = workload.DeviceRows(torch, vcfc, n, S, law, seed=301 + law, device="cuda:0")
+    out, rec, err = _device_encode(torch, vcfc, rows)
+    assert err == vcfc.NO_ERROR
+    rec_t = _digest_check(torch, vcfc, rows, out, rec, n)
+    dws_bytes = vcfc.decode_workspace_size(n)
+    dws = torch.empty(dws_bytes, dtype=torch.uint8, device=dev)
+    cap = rows.total_bytes + 64
+    lines = torch.empty(cap, dtype=torch.uint8, device=dev)
+    loff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    derr = torch.empty(1, dtype=torch.int64, device=dev)
+    for exact in (False, True):
+        vcfc.decode_records_device(out.data_ptr(), int(rec[n]), rec_t.data_ptr(), n, S, lines.data_ptr(), cap,
+                                   loff.data_ptr(), dws.data_ptr(), dws_bytes, derr.data_ptr(),
+                                   torch.cuda.current_stream(dev).cuda_stream, exact=exact)
+        torch.cuda.synchronize(dev)
+        e = int(derr.cpu().numpy().view(np.uint64)[0])
+        if e == vcfc.NO_ERROR or (e & 0xFF) != 4:
+            break
+    assert e == vcfc.NO_ERROR, hex(e)
+    assert int(loff[n].item()) == rows.total_bytes
+    assert bool(torch.equal(lines[:rows.total_bytes], rows.buf[:rows.total_bytes]))
+
+
+def _header(S):
+    return ("##fileformat=VCFv4.2\n#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT"
+            + "".join("\tS%d" % i for i in range(S)) + "\n").encode()
+
+
+def test_range_query_full_batch(torch, vcfc):
+    """BASELINE configs[4]: range queries over the 2504 x 1M chr22-shaped
+    batch's records in HBM (query_compressed_file, reference
+    src/main.cpp:3777-3929: CHROM/POS match per record, matching records
+    decoded): the middle 12.5 %, the first record, the last record, an empty
+    POS window, another CHROM, and every record.  The returned lines must be
+    exactly the input rows whose POS lies in the range, and the oracle's query
+    over a file of sampled records (the range edges and random ones) must give
+    the same lines."""
+    import workload
+    from test_gpu_encode import _device_encode
+    n, S = 1_000_000, 2504
+    dev = torch.device("cuda:0")
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    rows = workload.DeviceRows(torch, vcfc, n, S, 1, seed=41, device="cuda:0")
+    out, rec, err = _device_encode(torch, vcfc, rows)
+    assert err == vcfc.NO_ERROR
+    rec_t = torch.from_numpy(rec.astype(np.int64)).to(dev)
+    rec_bytes = int(rec[n])
+    pos = rows.pos
+    assert (np.diff(pos) > 0).all()
+    lo = np.append(rows.line_off.cpu().numpy().astype(np.int64), rows.total_bytes)
+    gap = int(np.nonzero(np.diff(pos) > 1)[0][0])
+    a = int(n * 0.4375)
+    cases = [("middle", "22", int(pos[a]), int(pos[a + n // 8 - 1]), a, a + n // 8 - 1),
+             ("first", "22", int(pos[0]), int(pos[0]), 0, 0),
+             ("last", "22", int(pos[-1]), int(pos[-1]), n - 1, n - 1),
+             ("empty", "22", int(pos[gap]) + 1, int(pos[gap]) + 1, None, None),
+             ("other_chrom", "21", 0, (1 << 63) - 1, None, None),
+             ("all", "22", 0, (1 << 63) - 1, 0, n - 1)]
+    flag = torch.empty(n + 64, dtype=torch.uint8, device=dev)
+    merr = torch.empty(1, dtype=torch.int64, device=dev)
+    derr = torch.empty(1, dtype=torch.int64, device=dev)
+    dws_bytes = vcfc.decode_workspace_size(n)
+    dws = torch.empty(dws_bytes, dtype=torch.uint8, device=dev)
+    cap = rows.total_bytes + 64
+    lines = torch.empty(cap, dtype=torch.uint8, device=dev)
+    loff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    rng = np.random.default_rng(5)
+    hdr = _header(S)
+    recs = out[:rec_bytes].cpu()
+    for name, chrom, qs, qe, ra, rb in cases:
+        ref = chrom.encode()
+        d_ref = torch.tensor(list(ref), dtype=torch.uint8, device=dev)
+        st = vcfc.query_match_device(out.data_ptr(), rec_t.data_ptr(), n, d_ref.data_ptr(), len(ref), True, qs, qe,
+                                     flag.data_ptr(), merr.data_ptr(), stream)
+        vcfc.raise_for(st)
+        vcfc.decode_selected_device(out.data_ptr(), rec_bytes, rec_t.data_ptr(), flag.data_ptr(), n, S,
+                                    lines.data_ptr(), cap, loff.data_ptr(), dws.data_ptr(), dws_bytes,
+                                    derr.data_ptr(), stream)
+        torch.cuda.synchronize(dev)
+        assert int(merr.cpu().numpy().view(np.uint64)[0]) == vcfc.NO_ERROR, name
+        assert int(derr.cpu().numpy().view(np.uint64)[0]) == vcfc.NO_ERROR, name
+        total = int(loff[n].item())
+        nsel = int(flag[:n].sum().item())
+        if ra is None:
+            assert nsel == 0 and total == 0, name
+        else:
+            assert nsel == rb - ra + 1, name
+            assert total == int(lo[rb + 1] - lo[ra]), name
+            assert bool(torch.equal(lines[:total], rows.buf[int(lo[ra]):int(lo[rb + 1])])), name
+        # the oracle on sampled records: the range edges and random rows
+        pick = {0, 1, n - 2, n - 1, gap, gap + 1}
+        if ra is not None:
+            pick |= {max(ra - 2, 0), max(ra - 1, 0), ra, min(ra + 1, n - 1), max(rb - 1, 0), rb, min(rb + 1, n - 1),
+                     min(rb + 2, n - 1)}
+        pick |= set(int(x) for x in rng.integers(0, n, 200))
+        pick = sorted(pick)
+        blob = hdr + b"".join(recs[int(rec[i]):int(rec[i + 1])].numpy().tobytes() for i in pick)
+        q = ("%s:%d-%d" % (chrom, qs, qe)).encode()
+        ost, olines = G.oracle_query(blob, q)
+        assert ost == 0, name
+        host = rows.host_lines([i for i in pick if ra is not None and ra <= i <= rb])
+        assert olines == b"".join(x + b"\n" for x in host), name

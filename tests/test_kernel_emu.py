@@ -276,40 +276,3 @@ def test_output_capacity_short():
         st2, out2, ro2, err2 = E.emu_encode(bytes(buf), np.array(offs, np.uint64), np.array(lens, np.uint32), cap=cap)
         assert err2 == (cut_row << 8) | 4, (cut_row, hex(err2))
         assert out2[:int(ro[cut_row])] == out[:int(ro[cut_row])]
-
-
-@pytest.mark.parametrize("pieces", [2, 3])
-def test_row_pieces(monkeypatch, pieces):
-    """VCFC_PIECES: the batch encoded in row pieces whose size scans continue
-    from the previous piece's total and whose compactions share the output
-    tile that straddles two pieces; records, offsets, the first failing row
-    and a short out_cap equal the one-piece run."""
-    rnd = random.Random(91)
-    lines = []
-    for i in range(4096 * pieces + 777):
-        k = rnd.choice([1, 2, 40, 300])
-        toks = [rnd.choice([b"0|0", b"0|1", b"1|1", b"0|2", b"./.", b"0"]) for _ in range(k)]
-        lines.append(b"\t".join([b"1", b"%d" % i, b"a", b"b", b"c", b"d", b"e", b"f", b"GT"] + toks))
-    st, out1, ro1, err1 = run(lines)
-    monkeypatch.setenv("VCFC_PIECES", str(pieces))
-    st, out, ro, err = run(lines)
-    assert err == err1 == (1 << 64) - 1
-    assert out == out1 and list(ro) == list(ro1)
-    for i in rnd.sample(range(len(lines)), 200) + [0, 4095, 4096, len(lines) - 1]:
-        assert out[int(ro[i]):int(ro[i + 1])] == G.oracle_encode_line(lines[i])[1], i
-    bad = list(lines)
-    bad[5000] = b"1\t2\t3\t4\t5\t6\t7"
-    st, out2, ro2, err2 = run(bad)
-    assert err2 == (5000 << 8) | 1
-    assert out2[:int(ro2[5000])] == out[:int(ro[5000])]
-    buf = bytearray()
-    offs, lens = [], []
-    for ln in lines:
-        offs.append(len(buf))
-        lens.append(len(ln))
-        buf += ln + b"\n"
-    cut = 4100
-    cap = int(ro[cut]) + 3
-    st3, out3, ro3, err3 = E.emu_encode(bytes(buf), np.array(offs, np.uint64), np.array(lens, np.uint32), cap=cap)
-    assert err3 == (cut << 8) | 4, hex(err3)
-    assert out3[:int(ro[cut])] == out[:int(ro[cut])]

@@ -1,5 +1,5 @@
 """Diagnostic: per-row start/end wall clock of k_encode_fast (a library built
-with -DVCFC_ROW_TIMES, picked by VCFC_LIB), and what a decoupled look-back
+with the tools/diag/row_times.h hooks, picked by VCFC_LIB), and what a decoupled look-back
 over row sizes would have to wait for: row i's output offset is known once
 every row < i has finished, i.e. at max(end[0..i]).
 

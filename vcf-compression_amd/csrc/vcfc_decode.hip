@@ -37,10 +37,7 @@ namespace {
 constexpr int DEC_WAVES = 4;   // records per 256-thread block
 constexpr uint32_t SB = 2048;              // sample bytes staged per piece (k_dec_write)
 constexpr uint32_t SBUF = SB + 48;         // + look-ahead, 16-B alignment slack, last block's overhang
-#ifndef VCFC_DEC_TB
-#define VCFC_DEC_TB 256
-#endif
-constexpr uint32_t TB = VCFC_DEC_TB;       // token words per LDS tile (k_dec_write): 4 per lane
+constexpr uint32_t TB = 256;   // token words per LDS tile (k_dec_write): 4 per lane (512: 1.9x, ab_dec_tile512.txt)
 
 // per-record status after planning
 constexpr uint32_t DS_SIMPLE = 0;   // line = REQ' + 4S bytes, item fill
@@ -488,11 +485,8 @@ __device__ __forceinline__ void write_one(const VcfcDecodeArgs &a, uint64_t i, u
         if (t0 + PL <= j0 + n_tok) {
 #pragma unroll
             for (uint32_t q = 0; q < PL; q += 4)
-#ifndef VCFC_DEC_TEMPORAL   // (non-temporal: -0.3 % in an A/B, ab_dec_nt.txt)
+                // (non-temporal: -0.3 % in an A/B, ab_dec_nt.txt)
                 vw::gstore16_nt(tok, 4ull * (t0 + q), make_uint4(w[q], w[q + 1], w[q + 2], w[q + 3]));
-#else
-                vw::gstore16(tok, 4ull * (t0 + q), make_uint4(w[q], w[q + 1], w[q + 2], w[q + 3]));
-#endif
         } else {
             for (uint32_t q = 0; q < PL; q++)
                 if (t0 + q < j0 + n_tok) *reinterpret_cast<uint32_t *>(tok + 4ull * (t0 + q)) = w[q];
@@ -530,11 +524,7 @@ __device__ __forceinline__ void write_one(const VcfcDecodeArgs &a, uint64_t i, u
 #pragma unroll
             for (uint32_t j = 0; j < 4; j++) {
                 const uint32_t o = ws[j] - j0;
-#ifndef VCFC_DEC_LANE_DUMMY
                 W[o < TB ? o : TB] = w[j];
-#else
-                W[o < TB ? o : TB + l] = w[j];
-#endif
             }
             if (st.got < j0 + TB || j0 + TB > S) break;   // the tile is not complete yet
             tile_out(TB);
@@ -548,20 +538,13 @@ __device__ __forceinline__ void write_one(const VcfcDecodeArgs &a, uint64_t i, u
         atomicMin((unsigned long long *)a.err, (unsigned long long)((i << 8) | 4u));
 }
 
-#ifndef VCFC_DEC_WPE
-#define VCFC_DEC_WPE 0
-#endif
 template <bool SEL>
-#if VCFC_DEC_WPE
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VCFC_DEC_WPE, VCFC_DEC_WPE))) void k_dec_write(VcfcDecodeArgs a, uint64_t first, uint64_t last) {
-#else
 __global__ __launch_bounds__(256) void k_dec_write(VcfcDecodeArgs a, uint64_t first, uint64_t last) {
-#endif
     __shared__ __attribute__((aligned(16))) uint8_t sbuf[DEC_WAVES * SBUF];
-    __shared__ __attribute__((aligned(16))) uint32_t tbuf[DEC_WAVES * (TB + 64)];   // tile + a dummy word per lane
+    __shared__ __attribute__((aligned(16))) uint32_t tbuf[DEC_WAVES * (TB + 4)];   // tile + the shared dummy word (16-B padded)
     const uint32_t wave = vw::readfirst(threadIdx.x >> 6);
     uint8_t *sb = sbuf + wave * SBUF;
-    uint32_t *W = tbuf + wave * (TB + 64);
+    uint32_t *W = tbuf + wave * (TB + 4);
     const uint64_t g = (uint64_t)blockIdx.x * DEC_WAVES + wave;
     if (!SEL) {
         if (first + g < last) write_one(a, first + g, sb, W);

@@ -32,13 +32,13 @@ struct VcfcEncodeArgs {
     uint32_t *rec_size;        // n
     uint64_t *partials;        // scan partials
     uint64_t *err;             // 1 word
-    uint32_t *retry_count;     // rows that took the general kernel (test builds only, VCFC_COUNT_RETRIES)
+    uint32_t *retry_count;     // rows that took the general kernel (emulator builds only, diag hooks)
     uint8_t *lb;               // look-back scan state (tickets, tile flags; zeroed per encode)
     uint32_t *tile_first;      // per 4 KiB output tile: the row holding its first byte (compaction)
     uint8_t *prim;             // per-row primary staging: record bytes [0, VCFC_PRIM) at prim + VCFC_PRIM * row
     uint8_t *slots;            // per-row overflow slots: record bytes [VCFC_PRIM, ...) at slots + slot_off[row]
     uint64_t slots_cap;
-    uint64_t *dbg;             // diagnostic builds only (VCFC_ROW_TIMES): per-row {start, end} wall clock; else null
+    uint64_t *dbg;             // diagnostic builds only (tools/diag hooks); else null
 };
 
 // Record staging: the first VCFC_PRIM bytes of every record go to a dense

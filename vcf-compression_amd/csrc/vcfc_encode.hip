@@ -3,14 +3,14 @@
 // Replaces compress_data_line (reference src/compress.cpp:5-203) for a batch
 // of lines resident in HBM.  Pipeline (all on one stream, no host sync):
 //
-//   scan<BOUND>  slot_off[i] = sum_{k<i} slot_bytes(len_k)     (tiny)
+//   k_scan_lb<1>      slot_off[i] = sum_{k<i} slot_bytes(len_k)   (tiny)
 //   k_encode_fast     one wave64 per row: tokenise, RLE-encode, stage the
 //                     record in an LDS ring, stream it to the row's staging in
-//                     1 KiB bursts; rows of another shape are queued
-//   k_encode_general  one wave per queued row (any shape)
-//   scan<IDENT>  rec_off[i] = sum_{k<i} rec_size_k             (tiny)
-//   k_compact    16 (long rows: 64) lanes per row: staging -> final offset,
-//                16-byte stores
+//                     1 KiB bursts; rows of another shape are flagged
+//   k_encode_general  one wave per 32 rows, encodes the flagged ones (any shape)
+//   k_scan_lb<0>      rec_off[i] = sum_{k<i} rec_size_k, + each 4 KiB output
+//                     tile's first row                           (tiny)
+//   k_compact_out     output-ordered: 4 KiB output tiles, 16-byte stores
 //
 // Record layout (reference compress.cpp:32-100,188-199):
 //   [LEN:4 BE|0xC0][REQ:4 BE|0xC0][cols 0..7 '\t'-joined]['\t'FORMAT]['\t']
@@ -30,10 +30,18 @@
 #include <hip/hip_runtime.h>
 #include <vcfc_wave.h>   // angle brackets: tests/simt_emu shadows it
 #include "vcfc_device.h"
-#include <cstdlib>
 
-// most row pieces of one encode (VCFC_PIECES, see vcfc_encode_device)
-#define VCFC_PIECES_MAX 16u
+// Diagnostic builds (tools/, tests/simt_emu) pass -DVCFC_DIAG='"hooks.h"' to
+// instrument the kernels; the product build defines every hook empty.
+#ifdef VCFC_DIAG
+#include VCFC_DIAG
+#endif
+#ifndef VCFC_DIAG_ROW_BEGIN
+#define VCFC_DIAG_ROW_BEGIN()            // k_encode_fast: a row starts
+#define VCFC_DIAG_ROW_END(a, row)        // k_encode_fast: the row's record is staged
+#define VCFC_DIAG_GENERAL_ROW(a)         // k_encode_general: a flagged row is taken
+#define VCFC_DIAG_WS_BYTES(n) 0ull       // extra workspace bytes (at VcfcWorkspaceLayout::dbg)
+#endif
 
 namespace {
 
@@ -185,14 +193,10 @@ struct Chunk {
     }
 };
 
-// cache policy of the encoder's line loads (read once): VCFC_PRE_AUX for the
-// prefix / general-step chunks, VCFC_GT_AUX for the genotype stream (2 = nt)
-#ifndef VCFC_PRE_AUX
-#define VCFC_PRE_AUX 0
-#endif
-#ifndef VCFC_GT_AUX
-#define VCFC_GT_AUX 0
-#endif
+// cache policy of the encoder's line loads: plain (non-temporal loads are
+// 30 % slower: the prefix / genotype chunk overlap and the look-ahead rely on
+// L2 hits, profiles/r01/ab/ab_nt_loads.txt)
+constexpr int PRE_AUX = 0, GT_AUX = 0;
 
 // The look-ahead dword after a lane's bytes is the next lane's first dword:
 // only lane 63 loads it (the other lanes' offsets lie past the range, so
@@ -207,8 +211,8 @@ __device__ __forceinline__ uint32_t la_off(uint32_t lane_bytes, uint32_t last) {
 __device__ __forceinline__ Chunk load_chunk(vw::brsrc rs, uint32_t c, uint32_t lo16) {
     Chunk k;
     const uint32_t off = c * CHUNK + lo16;   // lo16 = 16 * lane
-    k.a = vw::bload16(rs, off, VCFC_PRE_AUX);
-    k.y = vw::bload4(rs, off + 16u + la_off(lo16, 63 * BPL), VCFC_PRE_AUX);
+    k.a = vw::bload16(rs, off, PRE_AUX);
+    k.y = vw::bload4(rs, off + 16u + la_off(lo16, 63 * BPL), PRE_AUX);
     return k;
 }
 __device__ __forceinline__ Chunk look_ahead(Chunk k) {
@@ -437,9 +441,9 @@ struct Chunk8 {
 __device__ __forceinline__ Chunk8 load_chunk8(vw::brsrc rs, uint32_t C, uint32_t lo32) {
     Chunk8 k;
     const uint32_t off = C * CHUNK8 + lo32;   // lo32 = 32 * lane
-    k.a = vw::bload16(rs, off, VCFC_GT_AUX);
-    k.b = vw::bload16(rs, off + 16u, VCFC_GT_AUX);
-    k.y = vw::bload4(rs, off + 32u + la_off(lo32, 63 * BPL8), VCFC_GT_AUX);   // lane 63 only (see load_chunk)
+    k.a = vw::bload16(rs, off, GT_AUX);
+    k.b = vw::bload16(rs, off + 16u, GT_AUX);
+    k.y = vw::bload4(rs, off + 32u + la_off(lo32, 63 * BPL8), GT_AUX);   // lane 63 only (see load_chunk)
     return k;
 }
 
@@ -577,9 +581,6 @@ __device__ __forceinline__ void esc8(const uint32_t (&d)[TPL8], int32_t t0, int3
     // {0,1}) iff a and b are '0'/'1' and the separator is '|'.  Class byte =
     // 0x90 + 2a + b, escapes 0x94; an escape's bytes never reach a neighbour.
     uint32_t cbL, cbH, eL, eH;   // eL/eH: 0xFF in the byte of each escape slot
-#ifdef VCFC_ASM_MARK
-    asm volatile(";esc8_begin" ::: "memory");
-#endif
     esc_classes(d[0], d[1], d[2], d[3], cbL, eL);
     esc_classes(d[4], d[5], d[6], d[7], cbH, eH);
     f.esc = vw::ballot((eL | eH) != 0) != 0;
@@ -635,9 +636,6 @@ __device__ __forceinline__ void esc8(const uint32_t (&d)[TPL8], int32_t t0, int3
     // unconditional: a byte or escape word the lane does not emit goes to its
     // dummy word, so the slots need no branches; an escape's four bytes
     // (0xE1 and its token) leave as one unaligned ds_write_b32.
-#ifdef VCFC_ASM_MARK
-    asm volatile(";esc8_emit" ::: "memory");
-#endif
     const uint32_t base = (r.wpos + incl2 - cnt) & RMASK;
     uint8_t *const lb = r.lds + base;
     // Stores that emit nothing go to one dummy word shared by the wave:
@@ -680,9 +678,6 @@ __device__ __forceinline__ void esc8(const uint32_t (&d)[TPL8], int32_t t0, int3
             for (uint32_t q = RING; q < base + cnt; q++) r.lds[q - RING] = r.lds[q];
         }
     }
-#ifdef VCFC_ASM_MARK
-    asm volatile(";esc8_end" ::: "memory");
-#endif
     r.wpos += vw::readlane(incl2, 63);
     f.pcls = (vw::readlane(cbH, 63) >> 24) & 7u;
     f.prs = vw::umax(vw::readlane(incl, 63), f.prs);
@@ -829,27 +824,10 @@ __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring
     const uint32_t ncG = (T + SLOTS8 - 1) / SLOTS8;
     const uint32_t lo32 = BPL8 * l;
     uint32_t C0 = 0;
-#ifndef VCFC_GT_DEPTH
-#define VCFC_GT_DEPTH 3   // genotype chunks in flight per wave
-#endif
+    // three chunks in flight per wave (two: 8 waves/SIMD but +3 % on the
+    // headline law, ab_depth_occupancy.txt; four: 5 waves/SIMD, slower,
+    // ab_depth4*.txt)
     for (;;) {
-#if VCFC_GT_DEPTH == 2
-        Chunk8 b0 = load_chunk8(rsG, C0, lo32);
-        Chunk8 b1 = load_chunk8(rsG, C0 + 1, lo32);
-        vw::pin_loads();
-        uint32_t C = C0, gen = C0;
-        bool ok = true;
-        for (;;) {
-            if (ok) { ok = vw::readfirst(gt_step8(b0, C, f, r)); gen = C; }
-            b0 = load_chunk8(rsG, C + 2, lo32);
-            vw::pin_loads();
-            if (ok && C + 1 < ncG) { ok = vw::readfirst(gt_step8(b1, C + 1, f, r)); gen = C + 1; }
-            b1 = load_chunk8(rsG, C + 3, lo32);
-            vw::pin_loads();
-            C = vw::readfirst(C + 2);
-            if (!ok || C >= ncG) break;
-        }
-#else
         Chunk8 b0 = load_chunk8(rsG, C0, lo32);
         Chunk8 b1 = load_chunk8(rsG, C0 + 1, lo32);
         Chunk8 b2 = load_chunk8(rsG, C0 + 2, lo32);
@@ -869,7 +847,6 @@ __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring
             C = vw::readfirst(C + 3);
             if (!ok || C >= ncG) break;
         }
-#endif
         if (ok) break;
         // chunk `gen`: the general step over its two 1 KiB halves
         for (uint32_t h = 0; h < 2; h++) {
@@ -1174,29 +1151,18 @@ __device__ __forceinline__ bool row_setup(const VcfcEncodeArgs &a, uint64_t row,
 // for k_encode_general.
 // Pinned to 6 waves/SIMD (the SGPR count allows no more): without the pin the
 // branch-free escape emission takes 84 VGPRs and 5 waves, +5 % on the
-// headline rows (profiles/r02/ab/ab_esc8_emit.txt).  A/B builds override it.
-#ifndef VCFC_FAST_WPE
-#define VCFC_FAST_WPE 6
-#endif
-#if VCFC_FAST_WPE
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VCFC_FAST_WPE, VCFC_FAST_WPE))) void k_encode_fast(VcfcEncodeArgs a, uint64_t row_lo, uint64_t row_hi) {
-#else
-__global__ __launch_bounds__(256) void k_encode_fast(VcfcEncodeArgs a, uint64_t row_lo, uint64_t row_hi) {
-#endif
+// headline rows (profiles/r02/ab/ab_esc8_emit.txt).
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 6))) void k_encode_fast(VcfcEncodeArgs a, uint64_t row_lo, uint64_t row_hi) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[K1_WAVES * RING_STRIDE];
     const uint32_t wave = vw::readfirst(threadIdx.x >> 6);   // wave-uniform: scalar row/len/loop control
     const uint64_t row = row_lo + (uint64_t)blockIdx.x * K1_WAVES + wave;   // rows [row_lo, row_hi): one piece
     if (row >= row_hi) return;
-#ifdef VCFC_ROW_TIMES
-    const uint64_t t_start = wall_clock64();
-#endif
+    VCFC_DIAG_ROW_BEGIN();
     Ring r;
     if (!row_setup(a, row, lds + wave * RING_STRIDE, r)) return;
     uint32_t bytes = 0;
     const bool ok = encode_fast(a.buf + a.line_off[row], a.line_len[row], r, &bytes);
-#ifdef VCFC_ROW_TIMES
-    if (vw::lane_id() == 0) { a.dbg[2 * row] = t_start; a.dbg[2 * row + 1] = wall_clock64(); }
-#endif
+    VCFC_DIAG_ROW_END(a, row);
     if (vw::lane_id() == 0) {
         // not the fast shape: the general kernel's wave for this row takes
         // it (a flag per row, no shared queue: 750k rows appending to one
@@ -1210,44 +1176,21 @@ __global__ __launch_bounds__(256) void k_encode_fast(VcfcEncodeArgs a, uint64_t 
 // one after the other.  A small grid (n / 128 blocks) costs the headline
 // rows, which flag none, next to nothing; 32 rows per wave keep the waves of
 // the law-2 rows (75 % flagged) balanced.
-#ifndef VCFC_GEN_ROWS
-#define VCFC_GEN_ROWS 32
-#endif
-constexpr uint32_t GEN_ROWS = VCFC_GEN_ROWS;   // rows per wave of the general kernel
-#ifndef VCFC_GEN_WPE
-#define VCFC_GEN_WPE 0
-#endif
-#if VCFC_GEN_WPE
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VCFC_GEN_WPE, VCFC_GEN_WPE))) void k_encode_general(VcfcEncodeArgs a, uint64_t row_lo, uint64_t row_hi) {
-#else
+// (8 rows per wave: law 2 -1.5 %, headline +0.4 % in empty waves,
+// ab_genrows_*.txt; a resident grid striding over rows: law 2 +13.6 %,
+// ab_gen_persist.txt)
+constexpr uint32_t GEN_ROWS = 32;   // rows per wave of the general kernel
 __global__ __launch_bounds__(256) void k_encode_general(VcfcEncodeArgs a, uint64_t row_lo, uint64_t row_hi) {
-#endif
     __shared__ __attribute__((aligned(16))) uint8_t lds[K1_WAVES * RING_STRIDE];
     const uint32_t wave = vw::readfirst(threadIdx.x >> 6);
     const uint32_t l = vw::lane_id();
-#ifdef VCFC_GEN_PERSIST
-    // a resident grid (every wave starts at once): wave w takes rows
-    // row_lo + w + k W, the flags of 64 of them per load, so the flagged rows
-    // spread evenly over the waves and no late round of waves runs alone
-    const uint64_t W = (uint64_t)gridDim.x * K1_WAVES, w = (uint64_t)blockIdx.x * K1_WAVES + wave;
-    for (uint64_t k0 = 0; row_lo + w + k0 * W < row_hi; k0 += 64) {
-    const uint64_t rl = row_lo + w + (k0 + l) * W;
-    const bool flagged = rl < row_hi && a.rec_size[rl] == VCFCD_RETRY;
-    uint64_t todo = vw::ballot(flagged);
-    while (todo) {
-        const uint64_t row = row_lo + w + (k0 + (uint64_t)__builtin_ctzll(todo)) * W;
-        todo &= todo - 1;
-#else
     const uint64_t row0 = row_lo + ((uint64_t)blockIdx.x * K1_WAVES + wave) * GEN_ROWS;
     const bool flagged = l < GEN_ROWS && row0 + l < row_hi && a.rec_size[row0 + l] == VCFCD_RETRY;
     uint64_t todo = vw::ballot(flagged);
     while (todo) {
         const uint64_t row = row0 + (uint64_t)__builtin_ctzll(todo);
         todo &= todo - 1;
-#endif
-#ifdef VCFC_COUNT_RETRIES   // test builds (tests/simt_emu): rows that took the general kernel
-        if (l == 0) atomicAdd(a.retry_count, 1u);
-#endif
+        VCFC_DIAG_GENERAL_ROW(a);
         Ring r;
         if (!row_setup(a, row, lds + wave * RING_STRIDE, r)) continue;
         uint32_t bytes = 0;
@@ -1257,31 +1200,12 @@ __global__ __launch_bounds__(256) void k_encode_general(VcfcEncodeArgs a, uint64
             if (st != VCFCD_OK) atomicMin((unsigned long long *)a.err, (unsigned long long)((row << 8) | st));
         }
     }
-#ifdef VCFC_GEN_PERSIST
-    }
-#endif
 }
 
 // blocks of k_encode_general to launch for m rows
 static uint64_t general_blocks(uint64_t m) {
-#ifdef VCFC_GEN_PERSIST
-    static int resident = 0;   // blocks resident on the whole device (same for every device of a node)
-    if (!resident) {
-        int dev = 0, cus = 0, per_cu = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_encode_general, 64 * K1_WAVES, 0) != hipSuccess ||
-            cus <= 0 || per_cu <= 0)
-            resident = 1024;
-        else
-            resident = cus * per_cu;
-    }
-    const uint64_t need = (m + K1_WAVES - 1) / K1_WAVES;
-    return need < (uint64_t)resident ? need : (uint64_t)resident;
-#else
     const uint64_t per_block = (uint64_t)K1_WAVES * GEN_ROWS;   // GEN_ROWS rows per wave
     return (m + per_block - 1) / per_block;
-#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -1300,65 +1224,8 @@ __device__ __forceinline__ uint4 realign16(uint4 lo, uint4 hi, uint32_t sh) {
                       vw::alignbyte(o[3], o[2], s), vw::alignbyte(o[4], o[3], s));
 }
 
-// 16 lanes per row (four rows per wave): per pass, lane g of a row's group
-// loads the aligned 16-B staging block b0 + g (one load per lane) and takes
-// block b0 + g + 1 from lane g + 1 by DPP row_shl (the group is one DPP
-// row), so lanes 0..14 store 15 aligned, realigned 16-B output blocks.  The
-// destination's unaligned head and tail bytes are stored singly, their loads
-// issued with the blocks'.  Record bytes [0, VCFC_PRIM) come from the dense
-// primary array, the rest from the row's overflow slot.
-__device__ __forceinline__ uint4 stage_blk(const uint8_t *prim, const uint8_t *slot, uint64_t k) {
-    return k < VCFC_PRIM / 16 ? vw::gload16(prim, (uint32_t)k) : vw::gload16(slot, (uint32_t)(k - VCFC_PRIM / 16));
-}
-__device__ __forceinline__ uint8_t stage_byte(const uint8_t *prim, const uint8_t *slot, uint64_t x) {
-    return x < VCFC_PRIM ? prim[x] : slot[x - VCFC_PRIM];
-}
-// GROUP lanes per row: 16 (one DPP row; four rows per wave) for records of
-// a few KiB, 64 (the whole wave, DPP wave_shl) for long records.
-template <uint32_t GROUP>
-__device__ __forceinline__ uint32_t next_lane(uint32_t v) {
-    return GROUP == 16 ? vw::row_shl1(v) : vw::shl1(v, 0u);
-}
-template <uint32_t GROUP>
-__global__ __launch_bounds__(256) void k_compact(const uint8_t *__restrict__ prims,
-                                                 const uint8_t *__restrict__ slots,
-                                                 const uint64_t *__restrict__ slot_off,
-                                                 const uint64_t *__restrict__ rec_off, uint64_t n,
-                                                 uint8_t *__restrict__ out, uint64_t out_cap,
-                                                 uint64_t *err) {
-    const uint32_t g = threadIdx.x / GROUP, gl = threadIdx.x % GROUP;
-    const uint64_t row = (uint64_t)blockIdx.x * (256 / GROUP) + g;
-    const bool live = row < n;
-    uint64_t d0 = 0, d1 = 0;
-    if (live) { d0 = rec_off[row]; d1 = rec_off[row + 1]; }
-    const bool bad = d1 > out_cap;
-    if (bad && gl == 0) atomicMin((unsigned long long *)err, (unsigned long long)((row << 8) | VCFCD_E_NOSPACE));
-    const uint64_t sz = bad ? 0 : d1 - d0;
-    const uint8_t *prim = prims + (live ? (uint64_t)VCFC_PRIM * row : 0);
-    const uint8_t *slot = slots + (live ? slot_off[row] : 0);
-    uint8_t *dst = out + d0;
-    uint32_t head = (uint32_t)((16u - (d0 & 15u)) & 15u);
-    if (head > sz) head = (uint32_t)sz;
-    const uint64_t body = sz - head;
-    const uint64_t nblk = body >> 4;
-    const uint32_t tail = (uint32_t)(body & 15u);
-    const uint8_t hb = gl < head ? stage_byte(prim, slot, gl) : (uint8_t)0;
-    const uint8_t tb = gl < tail ? stage_byte(prim, slot, head + 16 * nblk + gl) : (uint8_t)0;
-    // passes run while any group of the wave has blocks left (DPP needs the whole wave)
-    for (uint64_t b0 = 0; vw::ballot(b0 < nblk); b0 += GROUP - 1) {
-        const uint64_t k = b0 + gl;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (k <= nblk && sz) v = stage_blk(prim, slot, k);   // block nblk: the last output block's upper bytes
-        const uint4 h = make_uint4(next_lane<GROUP>(v.x), next_lane<GROUP>(v.y), next_lane<GROUP>(v.z),
-                                   next_lane<GROUP>(v.w));
-        if (gl < GROUP - 1 && k < nblk) vw::gstore16(dst, head + 16 * k, realign16(v, h, head));
-    }
-    if (gl < head) dst[gl] = hb;
-    if (gl < tail) dst[head + 16 * nblk + gl] = tb;
-}
-
 // ---------------------------------------------------------------------------
-// Output-ordered compaction (default): the output is cut into 4 KiB tiles;
+// Output-ordered compaction: the output is cut into 4 KiB tiles;
 // a grid of waves strides over the tiles, and within a tile lane l writes the
 // 16-byte blocks l, l + 64, l + 128, l + 192, so every store instruction
 // covers 1 KiB of the output contiguously and every output line is written
@@ -1367,21 +1234,11 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t *__restrict__ pri
 // overflow slot's first bytes where the block crosses record byte
 // VCFC_PRIM, and with the next record's first bytes where it crosses a
 // record end (records hold >= 26 bytes, so a block meets at most two).
-// k_tile_first gives each tile the row holding its first byte.
-#ifndef VCFC_CT_BLOCKS
-#define VCFC_CT_BLOCKS 4
-#endif
-constexpr uint32_t CTB = VCFC_CT_BLOCKS;   // 16-B blocks per lane per tile
+// The size scan (k_scan_lb<0, true>) gives each tile the row holding its
+// first byte.  (4 KiB tiles: 2 KiB the same, 8 KiB +45 %, ab_compact_tile.txt;
+// the round-1 row-ordered kernel was 12 % slower, ab_compact_out.txt.)
+constexpr uint32_t CTB = 4;                // 16-B blocks per lane per tile
 constexpr uint32_t CT = 1024 * CTB;        // output bytes per tile
-
-__global__ __launch_bounds__(256) void k_tile_first(const uint64_t *__restrict__ rec_off, uint64_t n, uint64_t out_cap,
-                                                    uint32_t *__restrict__ tile_first, uint64_t *err) {
-    const uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (r >= n) return;
-    const uint64_t a = rec_off[r], b = rec_off[r + 1];
-    if (b > out_cap) atomicMin((unsigned long long *)err, (unsigned long long)((r << 8) | VCFCD_E_NOSPACE));
-    for (uint64_t t = (a + CT - 1) / CT; t * CT < b; t++) tile_first[t] = (uint32_t)r;
-}
 
 // bytes [0, s) of a, then b's first 16 - s bytes (0 < s < 16)
 __device__ __forceinline__ uint4 merge16(uint4 a, uint4 b, uint32_t s) {
@@ -1399,20 +1256,14 @@ __global__ __launch_bounds__(256) void k_compact_out(const uint8_t *__restrict__
                                                      const uint64_t *__restrict__ slot_off,
                                                      const uint64_t *__restrict__ rec_off, uint64_t n,
                                                      const uint32_t *__restrict__ tile_first,
-                                                     uint8_t *__restrict__ out, uint64_t out_cap,
-                                                     uint64_t row_lo, bool last) {
-    // Rows [row_lo, n) of one piece (the whole batch: row_lo = 0, last).  A
-    // piece writes the tiles from the one holding its first byte (which may
-    // begin in the previous piece: that piece stops short of it) to the last
-    // tile it completes; the last piece also writes the final partial tile.
+                                                     uint8_t *__restrict__ out, uint64_t out_cap) {
     const uint32_t l = vw::lane_id();
     const uint64_t g = (uint64_t)blockIdx.x * 4 + vw::readfirst(threadIdx.x >> 6);
     const uint64_t G = (uint64_t)gridDim.x * 4;
     const uint64_t total = rec_off[n];
     const uint64_t lim = total < out_cap ? total : out_cap;
-    const uint64_t ntile = last ? (lim + CT - 1) / CT : (total < out_cap ? total / CT : (lim + CT - 1) / CT);
-    const uint64_t t0 = row_lo ? rec_off[row_lo] / CT : 0;
-    for (uint64_t t = t0 + g; t < ntile; t += G) {
+    const uint64_t ntile = (lim + CT - 1) / CT;
+    for (uint64_t t = g; t < ntile; t += G) {
         const uint64_t o0 = t * CT;
         const uint64_t r0 = tile_first[t];
         // rows r0 .. r0 + 63: their starts (lane j holds row r0 + j); rows
@@ -1465,14 +1316,10 @@ __global__ __launch_bounds__(256) void k_compact_out(const uint8_t *__restrict__
             if (o + 16 > en[k] && en[k] < lim)   // the next non-empty record starts at en
                 v = merge16(v, vw::uload16(prims + (uint64_t)VCFC_PRIM * (r0 + idx2[k])), (uint32_t)(en[k] - o));
             if (o + 16 <= lim) {
-#ifndef VCFC_COMPACT_TEMPORAL
                 // non-temporal: the records leave the chip (D2H, a file, the
                 // next stage), and the next batch's encode keeps L2 / MALL to
                 // itself (-0.8 % per step in an A/B, ab_compact_nt.txt)
                 vw::gstore16_nt(out, o, v);
-#else
-                vw::gstore16(out, o, v);
-#endif
             } else {
                 const uint32_t w[4] = {v.x, v.y, v.z, v.w};
                 for (uint32_t i = 0; o + i < lim; i++) out[o + i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
@@ -1586,10 +1433,7 @@ __device__ __forceinline__ void lb_store(uint64_t *p, uint64_t v) {
 template <int MODE, bool TILES>
 __global__ __launch_bounds__(256) void k_scan_lb(const uint32_t *__restrict__ in, uint64_t n, uint32_t *ticket,
                                                  uint64_t *flags, uint64_t *__restrict__ out,
-                                                 uint32_t *__restrict__ tile_first, uint64_t out_cap, uint64_t *err,
-                                                 const uint64_t *base_in, uint64_t row_base) {
-    // base_in (a piece after the first): the scan starts at *base_in, the
-    // previous piece's total; row_base: the piece's first row (error codes)
+                                                 uint32_t *__restrict__ tile_first, uint64_t out_cap, uint64_t *err) {
     __shared__ uint64_t sh[SCAN_THREADS];
     __shared__ uint32_t s_tile;
     __shared__ uint64_t s_excl;
@@ -1608,9 +1452,8 @@ __global__ __launch_bounds__(256) void k_scan_lb(const uint32_t *__restrict__ in
     const uint64_t texcl = block_excl_scan_u64(sum, sh, &agg);
     if (threadIdx.x < 64) {   // wave 0: publish the aggregate, look back
         const uint32_t l = threadIdx.x;
-        const uint64_t b0 = (tile == 0 && base_in) ? *base_in : 0;
-        if (l == 0) lb_store(flags + tile, (tile == 0 ? LB_INC : LB_AGG) | (b0 + agg));
-        uint64_t excl = b0;
+        if (l == 0) lb_store(flags + tile, (tile == 0 ? LB_INC : LB_AGG) | agg);
+        uint64_t excl = 0;
         if (tile > 0) {
             int64_t p = (int64_t)tile - 1;   // the window covers tiles p, p - 1, ..., p - 63
             for (;;) {
@@ -1648,8 +1491,8 @@ __global__ __launch_bounds__(256) void k_scan_lb(const uint32_t *__restrict__ in
             out[r] = run;
             if (TILES) {
                 const uint64_t b = run + vals[i];
-                if (b > out_cap) atomicMin((unsigned long long *)err, (unsigned long long)(((row_base + r) << 8) | VCFCD_E_NOSPACE));
-                for (uint64_t t = (run + CT - 1) / CT; t * CT < b; t++) tile_first[t] = (uint32_t)(row_base + r);
+                if (b > out_cap) atomicMin((unsigned long long *)err, (unsigned long long)((r << 8) | VCFCD_E_NOSPACE));
+                for (uint64_t t = (run + CT - 1) / CT; t * CT < b; t++) tile_first[t] = (uint32_t)r;
             }
             if (r + 1 == n) out[n] = run + vals[i];
         }
@@ -1672,48 +1515,15 @@ VcfcWorkspaceLayout vcfc_encode_workspace_layout(uint64_t n, uint64_t total_line
     const uint64_t nt = (n + SCAN_TILE - 1) / SCAN_TILE + 1;
     L.lb = o;
     L.retry_count = o + 8;
-    L.lb_bytes = 16 + 16 * nt + 12 * VCFC_PIECES_MAX;   // + per-piece tickets and flag windows
+    L.lb_bytes = 16 + 16 * nt;
     o = al(o + L.lb_bytes);
     L.tile_first = o; o = al(o + 4 * (vcfc_record_bound(n, total_line_bytes) / CT + 2));
     L.prim = o; o = al(o + (uint64_t)VCFC_PRIM * n);
     L.slots = o; o = al(o + total_line_bytes + total_line_bytes / 2 + 64 * (n + 1));
     L.dbg = o;
-#ifdef VCFC_ROW_TIMES
-    o += 16 * n;
-#endif
+    o += VCFC_DIAG_WS_BYTES(n);
     L.total = o;
     return L;
-}
-
-// Pieces (VCFC_PIECES, default 1): the batch's rows in P consecutive
-// pieces; piece j's size scan and compaction run on a second stream while
-// piece j + 1 encodes, so the compaction's HBM traffic fills the encoder's
-// tail and its issue-bound stretches instead of following it.
-static int encode_pieces() {
-    const char *e = getenv("VCFC_PIECES");
-    const int v = e ? atoi(e) : 1;
-    return v < 1 ? 1 : v > (int)VCFC_PIECES_MAX ? (int)VCFC_PIECES_MAX : v;
-}
-
-// per-thread second stream and events of the piece pipeline (one device)
-struct PieceStreams {
-    int dev = -1;
-    hipStream_t s2 = nullptr;
-    hipEvent_t ev[VCFC_PIECES_MAX + 1] = {};
-};
-static hipError_t piece_streams(PieceStreams *&ps) {
-    static thread_local PieceStreams t;
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return e;
-    if (t.dev != dev) {
-        if ((e = hipStreamCreateWithFlags(&t.s2, hipStreamNonBlocking)) != hipSuccess) return e;
-        for (auto &x : t.ev)
-            if ((e = hipEventCreateWithFlags(&x, hipEventDisableTiming)) != hipSuccess) return e;
-        t.dev = dev;
-    }
-    ps = &t;
-    return hipSuccess;
 }
 
 hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t s, hipEvent_t *ev) {
@@ -1722,59 +1532,15 @@ hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t s, hipEvent_t
     if (a.n == 0) return hipMemsetAsync(a.rec_off, 0, 8, s);
     const uint64_t nt = (a.n + SCAN_TILE - 1) / SCAN_TILE;   // scan tiles
     // lb: tickets (slot scan, size scan), retry counter, slot-scan flags
-    // (nt + 1), size-scan flags (nt + 1 + one spare per piece), piece tickets
+    // (nt + 1), size-scan flags (nt + 1)
     uint32_t *tickets = reinterpret_cast<uint32_t *>(a.lb);
     uint64_t *flags_a = reinterpret_cast<uint64_t *>(a.lb + 16), *flags_b = flags_a + nt + 1;
-    uint32_t *ptickets = reinterpret_cast<uint32_t *>(flags_b + nt + 1 + VCFC_PIECES_MAX);
-    if ((e = hipMemsetAsync(a.lb, 0, 16 + 16 * (nt + 1) + 12 * VCFC_PIECES_MAX, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(a.lb, 0, 16 + 16 * (nt + 1), s)) != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[0], s);
-#ifdef VCFC_SCAN3
-    e = launch_scan<1>(a.line_len, a.n, a.partials, a.slot_off, s);
-    if (e != hipSuccess) return e;
-#else
     hipLaunchKernelGGL((k_scan_lb<1, false>), dim3((unsigned)nt), dim3(SCAN_THREADS), 0, s, a.line_len, a.n, tickets,
-                       flags_a, a.slot_off, nullptr, 0, nullptr, nullptr, 0);
+                       flags_a, a.slot_off, nullptr, 0, nullptr);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-#endif
     if (ev) (void)hipEventRecord(ev[1], s);
-    // a grid of 8 waves per SIMD striding over the output tiles (uniform work)
-    const uint64_t tiles = vcfc_record_bound(a.n, a.line_bytes_hint) / CT + 1;
-    const uint64_t cblocks = tiles < 8192 ? (tiles + 3) / 4 : 2048;
-#if !defined(VCFC_SCAN3) && !defined(VCFC_ROW_COMPACT)
-    int P = encode_pieces();
-    if ((uint64_t)P * SCAN_TILE > a.n) P = 1;   // a piece holds at least one scan tile
-    if (P > 1) {
-        PieceStreams *ps = nullptr;
-        if ((e = piece_streams(ps)) != hipSuccess) return e;
-        for (int j = 0; j < P; j++) {
-            // piece bounds on scan tiles: piece j's flags start at tile R_j / SCAN_TILE + j
-            const uint64_t lo = a.n * (uint64_t)j / (uint64_t)P / SCAN_TILE * SCAN_TILE;
-            const uint64_t hi = j + 1 == P ? a.n : a.n * (uint64_t)(j + 1) / (uint64_t)P / SCAN_TILE * SCAN_TILE;
-            const uint64_t m = hi - lo, mt = (m + SCAN_TILE - 1) / SCAN_TILE;
-            hipLaunchKernelGGL(k_encode_fast, dim3((unsigned)((m + K1_WAVES - 1) / K1_WAVES)), dim3(64 * K1_WAVES), 0, s,
-                               a, lo, hi);
-            hipLaunchKernelGGL(k_encode_general, dim3((unsigned)general_blocks(m)), dim3(64 * K1_WAVES), 0, s, a, lo,
-                               hi);
-            if ((e = hipGetLastError()) != hipSuccess) return e;
-            if ((e = hipEventRecord(ps->ev[j], s)) != hipSuccess) return e;
-            if ((e = hipStreamWaitEvent(ps->s2, ps->ev[j], 0)) != hipSuccess) return e;
-            hipLaunchKernelGGL((k_scan_lb<0, true>), dim3((unsigned)mt), dim3(SCAN_THREADS), 0, ps->s2, a.rec_size + lo,
-                               m, ptickets + j, flags_b + lo / SCAN_TILE + j, a.rec_off + lo, a.tile_first, a.out_cap,
-                               a.err, j ? a.rec_off + lo : nullptr, lo);
-            hipLaunchKernelGGL(k_compact_out, dim3((unsigned)cblocks), dim3(256), 0, ps->s2, a.prim, a.slots,
-                               a.slot_off, a.rec_off, hi, a.tile_first, a.out, a.out_cap, lo, j + 1 == P);
-            if ((e = hipGetLastError()) != hipSuccess) return e;
-        }
-        if (ev) {
-            (void)hipEventRecord(ev[2], s);   // encode done; the compaction of the last piece follows
-            (void)hipEventRecord(ev[3], s);
-        }
-        if ((e = hipEventRecord(ps->ev[P], ps->s2)) != hipSuccess) return e;
-        if ((e = hipStreamWaitEvent(s, ps->ev[P], 0)) != hipSuccess) return e;
-        if (ev) (void)hipEventRecord(ev[4], s);
-        return hipSuccess;
-    }
-#endif
     hipLaunchKernelGGL(k_encode_fast, dim3((unsigned)((a.n + K1_WAVES - 1) / K1_WAVES)), dim3(64 * K1_WAVES), 0, s, a,
                        (uint64_t)0, a.n);
     if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -1782,36 +1548,15 @@ hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t s, hipEvent_t
                        (uint64_t)0, a.n);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[2], s);
-#if defined(VCFC_SCAN3) || defined(VCFC_ROW_COMPACT)
-    e = launch_scan<0>(a.rec_size, a.n, a.partials, a.rec_off, s);
-    if (e != hipSuccess) return e;
-#else
     hipLaunchKernelGGL((k_scan_lb<0, true>), dim3((unsigned)nt), dim3(SCAN_THREADS), 0, s, a.rec_size, a.n,
-                       tickets + 1, flags_b, a.rec_off, a.tile_first, a.out_cap, a.err, nullptr, 0);
+                       tickets + 1, flags_b, a.rec_off, a.tile_first, a.out_cap, a.err);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-#endif
     if (ev) (void)hipEventRecord(ev[3], s);
-#ifdef VCFC_ROW_COMPACT
-    // (A/B builds) row-ordered compaction: records of rows longer than 64 KiB
-    // on average (biobank-wide rows) get a whole wave each
-#ifndef VCFC_WIDE_ROW
-#define VCFC_WIDE_ROW (64ull << 10)
-#endif
-    if (a.line_bytes_hint > VCFC_WIDE_ROW * a.n)
-        hipLaunchKernelGGL(k_compact<64>, dim3((unsigned)((a.n + 3) / 4)), dim3(256), 0, s, a.prim, a.slots,
-                           a.slot_off, a.rec_off, a.n, a.out, a.out_cap, a.err);
-    else
-        hipLaunchKernelGGL(k_compact<16>, dim3((unsigned)((a.n + 15) / 16)), dim3(256), 0, s, a.prim, a.slots,
-                           a.slot_off, a.rec_off, a.n, a.out, a.out_cap, a.err);
-#else
-#ifdef VCFC_SCAN3
-    hipLaunchKernelGGL(k_tile_first, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, s, a.rec_off, a.n, a.out_cap,
-                       a.tile_first, a.err);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-#endif
+    // a grid of 8 waves per SIMD striding over the output tiles (uniform work)
+    const uint64_t tiles = vcfc_record_bound(a.n, a.line_bytes_hint) / CT + 1;
+    const uint64_t cblocks = tiles < 8192 ? (tiles + 3) / 4 : 2048;
     hipLaunchKernelGGL(k_compact_out, dim3((unsigned)cblocks), dim3(256), 0, s, a.prim, a.slots, a.slot_off,
-                       a.rec_off, a.n, a.tile_first, a.out, a.out_cap, (uint64_t)0, true);
-#endif
+                       a.rec_off, a.n, a.tile_first, a.out, a.out_cap);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[4], s);
     return hipSuccess;

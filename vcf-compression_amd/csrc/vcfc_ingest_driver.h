@@ -552,6 +552,10 @@ inline int compress_device(const uint8_t *d_in, uint64_t N, uint8_t *d_out, uint
         if (vcfc_line_index(d_c, n, d_ix1, L1, x, s) != hipSuccess || !d2h(hsmall, d_small, 8) || !sync())
             return ST_E_HIP;
         const uint64_t n_lines = hsmall[0];
+        // line numbers inside a chunk are 32-bit (k_line_place): a chunk of
+        // 2^32 lines or more is refused (a chunk size set on the context
+        // splits such an input)
+        if (n_lines >= (1ull << 32) - 1) return ST_E_ARG;
         const VcfcLineIndexLayout L = vcfc_line_index_layout(n, n_lines);
         uint8_t *d_ix2 = static_cast<uint8_t *>(M.dev(Memory::D_IX2, L.total2));
         uint8_t *d_lines = static_cast<uint8_t *>(M.dev(Memory::D_LINES, 32 * (n_lines + 1)));
@@ -572,7 +576,17 @@ inline int compress_device(const uint8_t *d_in, uint64_t N, uint8_t *d_out, uint
         if (hsmall[3]) return ST_E_ARG;   // a line of 4 GiB or more
         const uint64_t n_data = hsmall[1], n_pass = hsmall[2];
         // ---- '#' lines: to the host, checked in order ----
-        std::vector<PassLine> pass;
+        // Each '#' line lies in d_c followed by its '\n' -- exactly the bytes
+        // the reference writes (line + "\n") -- so it is placed by a D2D copy;
+        // the host only checks the text.  The lines come to the host in one
+        // D2H of the span from the first to the last (a real header is one
+        // contiguous block), or one D2H per line when the span is much longer
+        // than the lines (interleaved '#' lines far apart).
+        struct DevPass {
+            uint64_t before, off, len;   // data lines before it; offset in d_c, length with the '\n'
+            uint32_t no;
+        };
+        std::vector<DevPass> pass;
         int64_t hdr_err = -1;
         uint64_t hdr_before = 0, pass_bytes = 0;
         bool interleaved = false;
@@ -582,28 +596,36 @@ inline int compress_device(const uint8_t *d_in, uint64_t N, uint8_t *d_out, uint
             if (!d2h(po.data(), x.pass_off, 8 * n_pass) || !d2h(pl.data(), x.pass_len, 4 * n_pass) ||
                 !d2h(pn.data(), x.pass_no, 4 * n_pass) || !d2h(pb.data(), x.pass_before, 8 * n_pass) || !sync())
                 return ST_E_HIP;
-            for (uint64_t k = 0; k < n_pass; k++) {
-                PassLine p;
-                p.before = pb[k];
-                p.no = pn[k];
-                p.text.resize(pl[k] + 1);
-                if (pl[k] && !d2h(p.text.data(), d_c + po[k], pl[k])) return ST_E_HIP;
-                p.text[pl[k]] = '\n';
-                pass.push_back(std::move(p));
+            uint64_t text_bytes = 0;
+            for (uint64_t k = 0; k < n_pass; k++) text_bytes += pl[k];
+            const uint64_t span = po[n_pass - 1] + pl[n_pass - 1] - po[0];
+            const bool one_copy = span <= 2 * text_bytes + (1u << 20);
+            std::vector<uint8_t> text(one_copy ? span : text_bytes);
+            std::vector<uint64_t> at(n_pass);   // line k's text at text.data() + at[k]
+            if (one_copy) {
+                if (span && !d2h(text.data(), d_c + po[0], span)) return ST_E_HIP;
+                for (uint64_t k = 0; k < n_pass; k++) at[k] = po[k] - po[0];
+            } else {
+                uint64_t t = 0;
+                for (uint64_t k = 0; k < n_pass; k++) {
+                    at[k] = t;
+                    if (pl[k] && !d2h(text.data() + t, d_c + po[k], pl[k])) return ST_E_HIP;
+                    t += pl[k];
+                }
             }
             if (!sync()) return ST_E_HIP;
             for (uint64_t k = 0; k < n_pass; k++) {
-                const PassLine &p = pass[k];
-                const uint64_t len = p.text.size() - 1;
-                if (!(len >= 2 && p.text[1] == '#') && !header_ok(p.text.data(), len)) {
-                    hdr_err = p.no;
-                    hdr_before = p.before;
-                    pass.resize(k);
+                const uint8_t *tx = text.data() + at[k];
+                const uint64_t len = pl[k];
+                if (!(len >= 2 && tx[1] == '#') && !header_ok(tx, len)) {
+                    hdr_err = pn[k];
+                    hdr_before = pb[k];
                     break;
                 }
+                pass.push_back(DevPass{pb[k], po[k], len + 1, pn[k]});
             }
-            for (const PassLine &p : pass) {
-                pass_bytes += p.text.size();
+            for (const DevPass &p : pass) {
+                pass_bytes += p.len;
                 interleaved = interleaved || p.before != 0;
             }
         }
@@ -659,23 +681,34 @@ inline int compress_device(const uint8_t *d_in, uint64_t N, uint8_t *d_out, uint
             stop = true;
             while (!pass.empty() && pass.back().before > good) pass.pop_back();   // '#' lines after the failing row
         }
-        // ---- place the '#' lines (and, interleaved, the record runs) ----
+        // ---- place the '#' lines (and, interleaved, the record runs); runs
+        // of '#' lines adjacent in the input and in the output are one copy ----
         uint64_t at = 0;   // records placed so far
-        for (const PassLine &p : pass) {
+        uint64_t run_src = 0, run_dst = 0, run_len = 0;
+        auto flush_run = [&]() {
+            const bool ok = !run_len ||
+                            hipMemcpyAsync(d_out + run_dst, d_c + run_src, run_len, hipMemcpyDeviceToDevice, s) == hipSuccess;
+            run_len = 0;
+            return ok;
+        };
+        for (const DevPass &p : pass) {
             uint64_t upto;
             if (!rec_at(std::min<uint64_t>(p.before, good), &upto)) return ST_E_HIP;
             if (upto > at) {
+                if (!flush_run()) return ST_E_HIP;
                 if (o + upto - at > out_cap) return ST_E_NOSPACE;
                 if (interleaved && hipMemcpyAsync(d_out + o, d_recs + at, upto - at, hipMemcpyDeviceToDevice, s) != hipSuccess)
                     return ST_E_HIP;
                 o += upto - at;
                 at = upto;
             }
-            if (o + p.text.size() > out_cap) return ST_E_NOSPACE;
-            if (hipMemcpyAsync(d_out + o, p.text.data(), p.text.size(), hipMemcpyHostToDevice, s) != hipSuccess)
-                return ST_E_HIP;
-            o += p.text.size();
+            if (o + p.len > out_cap) return ST_E_NOSPACE;
+            if (run_len && (run_src + run_len != p.off || run_dst + run_len != o) && !flush_run()) return ST_E_HIP;
+            if (!run_len) { run_src = p.off; run_dst = o; }
+            run_len += p.len;
+            o += p.len;
         }
+        if (!flush_run()) return ST_E_HIP;
         uint64_t rec_end;
         if (!rec_at(good, &rec_end)) return ST_E_HIP;
         if (rec_end > at) {
@@ -684,7 +717,7 @@ inline int compress_device(const uint8_t *d_in, uint64_t N, uint8_t *d_out, uint
                 return ST_E_HIP;
             o += rec_end - at;
         }
-        if (!sync()) return ST_E_HIP;   // the '#' line texts are host vectors
+        if (!sync()) return ST_E_HIP;
         *out_len = o;
         if (stop) {
             if (err_line) *err_line = (int64_t)(line_base + (uint64_t)bad_line + 1);
