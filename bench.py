@@ -50,13 +50,17 @@ def parse():
                     help="rows in the CPU-baseline sample (default: about 1.2 GB of lines)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify-rows", type=int, default=64, help="rows checked against the CPU path")
-    ap.add_argument("--mode", choices=["encode", "biobank", "decode", "query", "ingest", "devfile", "sparse"],
+    ap.add_argument("--mode", choices=["encode", "biobank", "decode", "query", "ingest", "devfile", "sparse",
+                                       "distfile"],
                     default="encode",
                     help="encode = the headline (BASELINE metric, configs[1]); biobank = configs[3] "
                          "(100k samples, one 100k-row batch of a 5M-row shard per GPU); decode = row f1; "
                          "query = row f2; ingest = row f4 (end-to-end file compress, configs[2]); "
                          "devfile = compress() of the configs[1] file already in HBM (line index + encode); "
-                         "sparse = rows a7-a9 + f3 (sparsify, sparse-file query)")
+                         "sparse = rows a7-a9 + f3 (sparsify, sparse-file query); distfile = the sharded "
+                         "file -> file compress (row e: every rank its byte range, outputs held and placed at "
+                         "the all-gathered offsets), --ingest-rows rows per rank")
+    ap.add_argument("--dist-dir", default="/tmp/vcfc_distfile", help="--mode distfile: where the files go")
     ap.add_argument("--rows-total", type=int, default=None,
                     help="--mode biobank: encode the rank's whole share of this many rows (5M = configs[3]) "
                          "as back-to-back --rows batches, every record digested and sampled rows re-encoded "
@@ -743,10 +747,153 @@ def bench_biobank_shard(args):
         dist.destroy_process_group()
 
 
+def bench_distfile(args):
+    """Row (e) end to end: the sharded `compress` of one VCF file into one
+    .vcfc file, as vcf-compression_amd/dist_compress.py runs it (one process
+    per GPU).  Every rank contributes --ingest-rows chr22-shaped rows (weak
+    scaling) to one input file (written untimed, so it sits in the page
+    cache); a step is the whole job: every rank streams its line-aligned
+    byte range through the ingest pipeline (reader threads, pinned H2D, GPU
+    line index + encode, D2H), rank 0 writes in place, the other ranks hold
+    their output in host memory, one all-gather of the byte counts gives the
+    offsets, the held bytes are written there once; a fresh output file per
+    step.  Time = max over ranks of the wall time between barriers.  After
+    timing, every rank checks its rows' slice of the output file against its
+    own GPU-encoded records (and rank 0 the header)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import vcfc
+    import workload
+    import dist_compress as D
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    rehearsal = os.environ.get("VCFC_BENCH_REHEARSAL") == "1"
+    dev = torch.device("cuda:%d" % (0 if rehearsal else local))
+    torch.cuda.set_device(dev)
+    cdev = torch.device("cpu") if rehearsal else dev
+    if world > 1:
+        dist.init_process_group("gloo" if rehearsal else "nccl", **({} if rehearsal else {"device_id": dev}))
+
+    def allgather(vals):
+        if world == 1:
+            return [list(vals)]
+        t = torch.tensor(vals, dtype=torch.int64, device=cdev)
+        o = torch.empty(world * len(vals), dtype=torch.int64, device=cdev)
+        dist.all_gather_into_tensor(o, t)
+        return o.view(world, len(vals)).cpu().tolist()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    n, S = args.ingest_rows, args.samples
+    rows = workload.DeviceRows(torch, vcfc, n, S, args.law, seed=2000 + rank, device=dev, row0=rank * n)
+    ws_bytes = vcfc.workspace_size(n, rows.line_bytes)
+    cap = vcfc.encode_bound(n, rows.line_bytes)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    recs = torch.empty(cap, dtype=torch.uint8, device=dev)
+    rec = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    err = torch.empty(1, dtype=torch.int64, device=dev)
+    vcfc.encode_rows_device(rows.buf.data_ptr(), rows.line_off.data_ptr(), rows.line_len.data_ptr(), n,
+                            rows.line_bytes, recs.data_ptr(), cap, rec.data_ptr(), ws.data_ptr(), ws_bytes,
+                            err.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize(dev)
+    assert int(err.cpu().numpy().view(np.uint64)[0]) == vcfc.NO_ERROR
+    my_rec = recs[:int(rec[n].item())].cpu().numpy().tobytes()
+    del ws, recs
+    header = sample_header(S)
+    g = allgather([rows.total_bytes, len(my_rec), rows.gt_bytes])
+    in_off = len(header) + sum(x[0] for x in g[:rank])
+    out_off = len(header) + sum(x[1] for x in g[:rank])
+    gt_all = sum(x[2] for x in g)
+    ip, op = os.path.join(args.dist_dir, "in.vcf"), os.path.join(args.dist_dir, "out.vcfc")
+    if rank == 0:
+        os.makedirs(args.dist_dir, exist_ok=True)
+        with open(ip, "wb") as f:
+            f.write(header)
+    barrier()
+    body = rows.buf[:rows.total_bytes].cpu().numpy()
+    fd = os.open(ip, os.O_WRONLY)
+    try:
+        mv, o = memoryview(body), 0
+        while o < len(body):
+            o += os.pwrite(fd, mv[o:o + (1 << 30)], in_off + o)
+    finally:
+        os.close(fd)
+    del body, rows
+    torch.cuda.empty_cache()
+    barrier()
+    ctx = vcfc.Context(0 if rehearsal else local)
+
+    def hold(path, off, length):
+        return ctx.compress_range_held(path, off, length, mem_bound=D.HOLD_BYTES, spill_dir=args.dist_dir)
+
+    def step():
+        if rank == 0:
+            if os.path.exists(op):
+                os.unlink(op)
+            open(op, "wb").close()
+        barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        st, total, line = D.compress_shard(ip, op, rank, world, ctx.compress_range, hold, allgather)
+        torch.cuda.synchronize(dev)
+        barrier()
+        dt = time.perf_counter() - t0
+        if st:
+            raise RuntimeError("sharded compress failed: status %d line %d" % (st, line))
+        return dt, total
+
+    for _ in range(args.warmup):
+        step()
+    tot_s = 0.0
+    for _ in range(args.steps):
+        dt, total = step()
+        tot_s += dt
+    t = torch.tensor([tot_s / args.steps], dtype=torch.float64, device=cdev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    sec = float(t[0].item())
+    # the output file: header (rank 0) + each rank's records at its offset
+    with open(op, "rb") as f:
+        ok = True
+        if rank == 0:
+            ok = f.read(len(header)) == header
+        f.seek(out_off)
+        ok = ok and f.read(len(my_rec)) == my_rec
+        size_ok = os.path.getsize(op) == len(header) + sum(x[1] for x in g)
+    okt = allgather([int(ok and size_ok)])
+    ctx.close()
+    res = {"metric": "input GT bytes/sec, sharded VCF file -> .vcfc file (row e end to end)",
+           "value": round(gt_all / sec / 1e9, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(sec * 1e3, 2), "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "u8", "data": "synthetic (written from HBM; input file in the page cache)",
+           "config": {"workload": "%s %d samples x %d variants per GPU, one file of %d rows"
+                                  % (law_name(args.law), S, n, n * world),
+                      "input_bytes": len(header) + sum(x[0] for x in g),
+                      "output_bytes": len(header) + sum(x[1] for x in g),
+                      "hold_bytes_per_rank_max": D.HOLD_BYTES,
+                      "parallelism": "byte-range shards x%d, all-gather of shard sizes%s"
+                                     % (world, " (rehearsal: gloo, one GPU)" if rehearsal else "")},
+           "timing": "wall time between barriers per step: read + H2D + line index + encode + D2H + write "
+                     "(rank 0 in place, other ranks held then placed at the all-gathered offset), max over ranks",
+           "output_identical_to_gpu_records": all(x[0] == 1 for x in okt)}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+        if not res["output_identical_to_gpu_records"]:
+            sys.exit(1)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     if args.mode == "biobank" and args.rows_total:
         return bench_biobank_shard(args)
+    if args.mode == "distfile":
+        return bench_distfile(args)
     if args.mode not in ("encode", "biobank"):
         import torch
         import vcfc

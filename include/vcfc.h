@@ -150,6 +150,24 @@ int vcfc_compress_device(vcfc_ctx *ctx, const uint8_t *d_in, uint64_t n, uint8_t
 int vcfc_compress_range(vcfc_ctx *ctx, const char *in_path, uint64_t off, uint64_t len, int out_fd,
                         uint64_t out_off, uint64_t *out_bytes, int64_t *err_line, uint64_t *lines);
 
+/* vcfc_compress_range with the output held for a later placement: the
+ * rank's offset in the output file is the exclusive prefix of the ranks' byte
+ * counts, known only after their all-gather.  The first mem_bound bytes stay
+ * in host memory, the rest go to an unlinked temporary file in spill_dir
+ * (NULL: /tmp).  vcfc_held_place writes all held bytes at out_off of out_fd
+ * (memory blocks by pwrite, the spilled part by copy_file_range), so output
+ * that fits in memory is written once, to its final place.  *held is set even
+ * on a failing line (it holds the output of the lines before it); free it
+ * with vcfc_held_free. */
+typedef struct vcfc_held vcfc_held;
+int vcfc_compress_range_held(vcfc_ctx *ctx, const char *in_path, uint64_t off, uint64_t len, uint64_t mem_bound,
+                             const char *spill_dir, vcfc_held **held, uint64_t *out_bytes, int64_t *err_line,
+                             uint64_t *lines);
+int vcfc_held_place(const vcfc_held *held, int out_fd, uint64_t out_off);
+/* bytes held in host memory / in the spill file */
+void vcfc_held_sizes(const vcfc_held *held, uint64_t *mem_bytes, uint64_t *spill_bytes);
+void vcfc_held_free(vcfc_held *held);
+
 /* ---- decoder: decompress2_fd (reference src/compress.cpp:1214-1257,
  * decompress2_data_line :741-986) ----------------------------------------
  * .vcfc bytes -> VCF text, byte-identical to the reference's `main

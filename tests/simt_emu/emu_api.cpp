@@ -5,6 +5,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <vector>
+#include <algorithm>
 #include "vcfc_device.h"
 #include "vcfc_decode_driver.h"
 #include "emu.h"
@@ -183,4 +184,19 @@ hipError_t vcfc_synth_device(uint8_t *buf, const uint64_t *line_off, uint64_t n,
 extern "C" int emu_synth(uint8_t *buf, const uint64_t *line_off, uint64_t n, const uint8_t *prefix,
                          const uint64_t *prefix_off, const float *row_af, uint32_t S, int law, uint64_t seed) {
     return (int)vcfc_synth_device(buf, line_off, n, prefix, prefix_off, row_af, S, law, seed, nullptr);
+}
+
+// vcfc_ing::Held (the held output of a sharded compress rank): append `n`
+// bytes in pieces of `piece`, with the first mem_bound bytes in memory and
+// the rest spilled to a file in `dir`; then place them at out_off of out_fd.
+extern "C" int emu_held(const uint8_t *data, uint64_t n, uint64_t piece, uint64_t mem_bound, const char *dir,
+                        int out_fd, uint64_t out_off, uint64_t *mem_bytes, uint64_t *spill_bytes) {
+    vcfc_ing::Held h;
+    h.mem_bound = mem_bound;
+    h.spill_dir = dir;
+    for (uint64_t o = 0; o < n; o += piece)
+        if (!h.append(data + o, std::min<uint64_t>(piece, n - o))) return 7;
+    *mem_bytes = h.mem;
+    *spill_bytes = h.spilled;
+    return h.place(out_fd, out_off) ? 0 : 7;
 }

@@ -1,5 +1,5 @@
 """GPU: the sharded compress (SURVEY §8 e; dist_compress.compress_shard over
-vcfc_compress_range) with 1/2/3 ranks as separate processes, all on cuda:0
+vcfc_compress_range / vcfc_compress_range_held) with 1/2/3 ranks as separate processes, all on cuda:0
 (gloo for the all-gather: RCCL refuses two ranks on one device).  Each rank
 streams its line-aligned byte range through the ingest pipeline (small chunks,
 so ranges span many chunks); the stitched file equals the reference's own
@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 sys.path.insert(0, os.path.join(G.REPO, "vcf-compression_amd"))
 
 
-def _worker(rank, world, port, in_path, out_path, chunk, q):
+def _worker(rank, world, port, in_path, out_path, chunk, mem_bound, q):
     import torch
     import torch.distributed as dist
     sys.path.insert(0, os.path.join(G.REPO, "vcf-compression_amd"))
@@ -34,14 +34,17 @@ def _worker(rank, world, port, in_path, out_path, chunk, q):
         out = [None] * world
         dist.all_gather_object(out, vals)
         return out
-    res = D.compress_shard(in_path, out_path, rank, world, ctx.compress_range, allgather)
+    def hold(p, off, length):   # output held in memory up to mem_bound, the rest spilled
+        return ctx.compress_range_held(p, off, length, mem_bound=mem_bound,
+                                       spill_dir=os.path.dirname(out_path))
+    res = D.compress_shard(in_path, out_path, rank, world, ctx.compress_range, hold, allgather)
     ctx.close()
     dist.barrier()
     dist.destroy_process_group()
     q.put((rank,) + tuple(res))
 
 
-def _run(world, data, port, chunk=65536):
+def _run(world, data, port, chunk=65536, mem_bound=1 << 30):
     with tempfile.TemporaryDirectory(dir="/tmp") as d:
         ip, op = os.path.join(d, "in.vcf"), os.path.join(d, "out.vcfc")
         with open(ip, "wb") as f:
@@ -49,21 +52,23 @@ def _run(world, data, port, chunk=65536):
         open(op, "wb").close()
         ctx = mp.get_context("spawn")
         q = ctx.Queue()
-        ps = [ctx.Process(target=_worker, args=(r, world, port, ip, op, chunk, q)) for r in range(world)]
+        ps = [ctx.Process(target=_worker, args=(r, world, port, ip, op, chunk, mem_bound, q)) for r in range(world)]
         for p in ps:
             p.start()
         for p in ps:
             p.join(180)
             assert p.exitcode == 0
         res = sorted(q.get() for _ in range(world))
-        leftovers = [x for x in os.listdir(d) if x.startswith(".vcfc-part")]
+        leftovers = [x for x in os.listdir(d) if x.startswith(".vcfc-")]
         assert not leftovers, leftovers
         return res, open(op, "rb").read()
 
 
-@pytest.mark.parametrize("world", [1, 2, 3])
-def test_gpu_sharded_compress_equals_reference(world):
-    res, out = _run(world, G.gz("random_100x10000.vcf.gz"), 29800 + world)
+@pytest.mark.parametrize("world,mem_bound", [(1, 1 << 30), (2, 1 << 30), (3, 1 << 30), (2, 0), (3, 100_003)])
+def test_gpu_sharded_compress_equals_reference(world, mem_bound):
+    """mem_bound 0: every held byte spilled; 100_003: held partly in memory."""
+    port = 29820 + 3 * world + (1 if mem_bound == 0 else 2 if mem_bound == 100_003 else 0)
+    res, out = _run(world, G.gz("random_100x10000.vcf.gz"), port, mem_bound=mem_bound)
     assert all(r[1] == 0 for r in res)
     assert out == G.gz("random_100x10000.vcfc.gz")
 
@@ -78,6 +83,6 @@ def test_gpu_sharded_compress_fuzz_and_error_lines():
         ls[k] = bad_line
         bad = b"\n".join(ls)
         st1, out1, line1 = G.oracle_compress(bad)
-        res, out = _run(3, bad, 29812 + k % 7, chunk=4096)
+        res, out = _run(3, bad, 29812 + k % 7, chunk=4096, mem_bound=50_000)
         assert st1 != 0 and all(r[1] == st1 and r[3] == line1 for r in res), (res, st1, line1)
         assert out == out1

@@ -193,8 +193,13 @@ def test_logical_shards_stitch_on_one_gpu(vcfc, world):
                 def allgather(vals):
                     slots[rank] = vals
                     bar.wait()
-                    return list(slots)
-                res[rank] = D.compress_shard(ip, op, rank, world, ctx.compress_range, allgather)
+                    out = list(slots)
+                    bar.wait()   # (the next all-gather reuses the slots)
+                    return out
+
+                def hold(p, off, length):
+                    return ctx.compress_range_held(p, off, length, spill_dir=d)
+                res[rank] = D.compress_shard(ip, op, rank, world, ctx.compress_range, hold, allgather)
 
         ts = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
         for t in ts:

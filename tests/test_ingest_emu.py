@@ -153,3 +153,32 @@ def test_short_lines_overflow_the_segment_slot():
     vcf = head + D.header(20) + body
     for chunk in (1 << 14, 1 << 20):
         check(vcf, chunk, "short lines")
+
+
+@pytest.mark.parametrize("mem_bound,piece", [(0, 1000), (12_345, 777), (10 ** 9, 4096), (65_536, 65_536)])
+def test_held_output_places_every_byte(mem_bound, piece):
+    """vcfc_ing::Held (dist_compress's rank output held until its offset is
+    known): bytes in memory up to mem_bound, the rest in an unlinked spill
+    file; place() writes them all at the offset, in order, once."""
+    import ctypes
+    import os
+    import tempfile
+    data = os.urandom(300_001)
+    L = E.lib()
+    u64, vp = ctypes.c_uint64, ctypes.c_void_p
+    L.emu_held.argtypes = [ctypes.c_char_p, u64, u64, u64, ctypes.c_char_p, ctypes.c_int, u64,
+                           ctypes.POINTER(u64), ctypes.POINTER(u64)]
+    with tempfile.TemporaryDirectory() as d:
+        op = os.path.join(d, "out")
+        with open(op, "wb") as f:
+            f.write(b"x" * 17)
+        fd = os.open(op, os.O_WRONLY)
+        m, s = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        try:
+            st = L.emu_held(data, len(data), piece, mem_bound, d.encode(), fd, 17, ctypes.byref(m), ctypes.byref(s))
+        finally:
+            os.close(fd)
+        assert st == 0
+        assert m.value == min(mem_bound, len(data)) and m.value + s.value == len(data)
+        assert open(op, "rb").read() == b"x" * 17 + data
+        assert os.listdir(d) == ["out"]   # the spill file was unlinked at once

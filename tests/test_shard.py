@@ -29,6 +29,33 @@ def _oracle_range(in_path, off, length, fd, out_off):
     return st, len(out), line, lines
 
 
+class _MemHeld:
+    """vcfc.Held stand-in: the oracle's output of a range, placed by pwrite."""
+
+    def __init__(self, b):
+        self.b = b
+
+    def place(self, fd, off):
+        mv, o = memoryview(self.b), 0
+        while o < len(self.b):
+            o += os.pwrite(fd, mv[o:], off + o)
+        return 0
+
+    def free(self):
+        self.b = None
+
+
+def _oracle_hold(in_path, off, length):
+    """vcfc.Context.compress_range_held with the oracle standing in for the
+    GPU: (status, bytes, failing line in the range, lines in the range, held)."""
+    with open(in_path, "rb") as f:
+        f.seek(off)
+        buf = f.read(length)
+    st, out, line = G.oracle_compress(buf)
+    lines = buf.count(b"\n") + (1 if buf and not buf.endswith(b"\n") else 0)
+    return st, len(out), line, lines, _MemHeld(out)
+
+
 def _worker(rank, world, port, in_path, out_path, q):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -38,7 +65,7 @@ def _worker(rank, world, port, in_path, out_path, q):
         out = [None] * world
         dist.all_gather_object(out, vals)
         return out
-    st, total, line = D.compress_shard(in_path, out_path, rank, world, _oracle_range, allgather)
+    st, total, line = D.compress_shard(in_path, out_path, rank, world, _oracle_range, _oracle_hold, allgather)
     dist.barrier()
     dist.destroy_process_group()
     q.put((rank, st, total, line))
@@ -101,35 +128,6 @@ def test_gloo_stitch_fuzz_and_error_line():
     assert st1 == 1 and all(r[1] == 1 and r[3] == line1 for r in res) and out == out1
 
 
-def test_copy_to_survives_short_writes(monkeypatch):
-    """A shard's spill is placed completely even when every pwrite moves only
-    part of the buffer and copy_file_range is unavailable (os.pwrite does not
-    loop by itself; one call moves < 2 GiB on Linux)."""
-    data = os.urandom(300_001)
-    with tempfile.TemporaryDirectory() as d:
-        sp, op = os.path.join(d, "spill"), os.path.join(d, "out")
-        with open(sp, "wb") as f:
-            f.write(data)
-        with open(op, "wb") as f:
-            f.write(b"x" * 17)
-        real = os.pwrite
-
-        def short(fd, b, off):
-            return real(fd, bytes(b)[:777], off)
-
-        def nocfr(*a):
-            raise OSError(38, "ENOSYS")
-        monkeypatch.setattr(os, "pwrite", short)
-        monkeypatch.setattr(os, "copy_file_range", nocfr)
-        sfd, ofd = os.open(sp, os.O_RDONLY), os.open(op, os.O_WRONLY)
-        try:
-            D.copy_to(sfd, ofd, len(data), 17)
-        finally:
-            os.close(sfd)
-            os.close(ofd)
-        assert open(op, "rb").read() == b"x" * 17 + data
-
-
 def test_rank_failure_travels_through_the_allgather():
     """A rank whose encoder raises (no GPU, I/O) reports E_IO through the
     all-gather instead of leaving the other ranks waiting; every rank returns
@@ -140,20 +138,22 @@ def test_rank_failure_travels_through_the_allgather():
         with open(ip, "wb") as f:
             f.write(data)
         open(op, "wb").close()
-        slots = {}
+        slots, calls = {}, {0: 0, 1: 0}
 
         def fake_gather(r):
-            def g(vals):
-                slots[r] = vals
-                return [slots[k] for k in sorted(slots)]
+            def g(vals):   # the k-th all-gather of rank r sees the k-th of the ranks before it
+                k = calls[r]
+                calls[r] += 1
+                slots[(r, k)] = vals
+                return [slots[(q, k)] for q in sorted(q for q, kk in slots if kk == k)]
             return g
 
         def boom(*a):
             raise RuntimeError("device lost")
-        # rank 1 of 2 runs first here, so its all-gather sees rank 0's values after
-        # rank 0 ran; run rank 0 with the oracle, then rank 1 failing
-        r0 = D.compress_shard(ip, op, 0, 2, _oracle_range, fake_gather(0))
-        r1 = D.compress_shard(ip, op, 1, 2, boom, fake_gather(1))
+        # run rank 0 with the oracle, then rank 1 failing (its all-gathers see
+        # rank 0's values)
+        r0 = D.compress_shard(ip, op, 0, 2, _oracle_range, _oracle_hold, fake_gather(0))
+        r1 = D.compress_shard(ip, op, 1, 2, _oracle_range, boom, fake_gather(1))
         assert r1[0] == D.E_IO and r1[2] == -1
         pts = D.split_points(len(data), 2, lambda o, n: data[o:o + n])
         assert open(op, "rb").read() == G.oracle_compress(data[:pts[1]])[1]

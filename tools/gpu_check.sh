@@ -15,7 +15,7 @@ for s in $STEPS; do
   echo "== $s $(date +%T)" | tee -a "$O/progress.txt"
   case $s in
     smoke) timeout -k 10 420 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 || { echo "smoke failed rc=$?"; tail -30 "$O/smoke.log"; exit 1; } ;;
-    tests) timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > "$O/pytest_gpu.log" 2>&1 || { echo "tests failed rc=$?"; tail -40 "$O/pytest_gpu.log"; exit 1; } ;;
+    tests) timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 400 --timeout-method thread --durations 15 > "$O/pytest_gpu.log" 2>&1 || { echo "tests failed rc=$?"; tail -40 "$O/pytest_gpu.log"; exit 1; } ;;
     bench) timeout -k 10 600 python bench.py > "$O/bench.json" 2> "$O/bench.err" || { echo "bench failed rc=$?"; tail -30 "$O/bench.err"; exit 1; } ; cat "$O/bench.json" ;;
     bench0) timeout -k 10 600 python bench.py --law 0 --no-cpu-baseline > "$O/bench_law0.json" 2> "$O/bench_law0.err" || { echo "bench0 failed"; tail -30 "$O/bench_law0.err"; exit 1; } ; cat "$O/bench_law0.json" ;;
     biobank) timeout -k 10 900 python bench.py --mode biobank --steps 5 --warmup 1 > "$O/bench_biobank.json" 2> "$O/bench_biobank.err" || { echo "biobank failed"; tail -30 "$O/bench_biobank.err"; exit 1; } ; cat "$O/bench_biobank.json" ;;
@@ -43,6 +43,8 @@ for s in $STEPS; do
            n=$(echo $P | cut -d' ' -f1)
            (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --pmc $P --kernel-trace --output-format csv -d "$O/pmcx_$n" -o run -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS} > "$O/pmcx_$n.log" 2>&1) || { echo "pmcx $n failed rc=$?"; tail -30 "$O/pmcx_$n.log"; exit 1; }
          done ;;
+    distfile) timeout -k 10 600 python bench.py --mode distfile --steps 3 --warmup 1 > "$O/bench_distfile.json" 2> "$O/bench_distfile.err" || { echo "distfile failed"; tail -30 "$O/bench_distfile.err"; exit 1; } ; cat "$O/bench_distfile.json" ;;
+    distfile2) VCFC_BENCH_REHEARSAL=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29621 bench.py --mode distfile --steps 3 --warmup 1 --dist-dir /tmp/vcfc_distfile2 > "$O/bench_distfile2.json" 2> "$O/bench_distfile2.err" || { echo "distfile2 failed"; tail -30 "$O/bench_distfile2.err"; exit 1; } ; cat "$O/bench_distfile2.json" ;;
     ptest) timeout -k 10 1000 python -u -m pytest ${PT_ARGS} -x -v -p no:cacheprovider --timeout 400 --timeout-method thread > "$O/pytest_sel.log" 2>&1 || { echo "ptest failed rc=$?"; tail -60 "$O/pytest_sel.log"; exit 1; } ; tail -5 "$O/pytest_sel.log" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

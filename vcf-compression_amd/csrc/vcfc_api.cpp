@@ -723,6 +723,52 @@ int vcfc_compress_range(vcfc_ctx *c, const char *in_path, uint64_t off, uint64_t
     return s;
 }
 
+struct vcfc_held : vcfc_ing::Held {};
+
+int vcfc_compress_range_held(vcfc_ctx *c, const char *in_path, uint64_t off, uint64_t len, uint64_t mem_bound,
+                             const char *spill_dir, vcfc_held **held, uint64_t *out_bytes, int64_t *err_line,
+                             uint64_t *lines) {
+    if (!c || !in_path || !held || !out_bytes) return VCFC_E_ARG;
+    *held = nullptr;
+    *out_bytes = 0;
+    if (err_line) *err_line = -1;
+    if (lines) *lines = 0;
+    if (hipSetDevice(c->device) != hipSuccess) return VCFC_E_HIP;
+    int fd = open(in_path, O_RDONLY);
+    if (fd < 0) return VCFC_E_IO;
+    struct stat st;
+    if (fstat(fd, &st) != 0 || off > (uint64_t)st.st_size || len > (uint64_t)st.st_size - off) {
+        close(fd);
+        return VCFC_E_ARG;
+    }
+    posix_fadvise(fd, (off_t)off, (off_t)len, POSIX_FADV_SEQUENTIAL);
+    vcfc_held *h = new (std::nothrow) vcfc_held;
+    if (!h) { close(fd); return VCFC_E_IO; }
+    h->mem_bound = mem_bound;
+    if (spill_dir) h->spill_dir = spill_dir;
+    auto sink = [&](const uint8_t *p, uint64_t k) { return h->append(p, k); };
+    FdSource src(fd, len, off);
+    CtxIngestMemory M(c);
+    const vcfc_ing::Config cfg = ingest_config(c, len);
+    const int s = vcfc_ing::compress_stream(src, sink, M, c->stream, cfg, err_line, lines);
+    close(fd);
+    *held = h;
+    *out_bytes = h->bytes();
+    return s;
+}
+
+int vcfc_held_place(const vcfc_held *h, int out_fd, uint64_t out_off) {
+    if (!h || out_fd < 0) return VCFC_E_ARG;
+    return h->place(out_fd, out_off) ? VCFC_OK : VCFC_E_IO;
+}
+
+void vcfc_held_sizes(const vcfc_held *h, uint64_t *mem_bytes, uint64_t *spill_bytes) {
+    if (mem_bytes) *mem_bytes = h ? h->mem : 0;
+    if (spill_bytes) *spill_bytes = h ? h->spilled : 0;
+}
+
+void vcfc_held_free(vcfc_held *h) { delete h; }
+
 // ---- decoder: decompress2_fd, reference
 // src/compress.cpp:1214-1257 ------------------------------------------------
 

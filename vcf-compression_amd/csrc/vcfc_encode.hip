@@ -106,6 +106,10 @@ __device__ __forceinline__ void ring_put(Ring &r, uint32_t pos, uint32_t b) {
 // (non-temporal: k_compact reads the staging back only after the whole
 // batch, so keeping it out of L2's way helps the input stream -- about 1 %,
 // profiles/r01/ab/ab_nt_stores.txt)
+// (temporal stores, i.e. staging kept in L2 / the 256 MiB Infinity Cache for
+// k_compact: k_compact unchanged at 0.283 ms, k_encode +0.4 %; the staging's
+// 0.68 GB are written amid the 10 GB input stream, so it does not stay
+// resident -- profiles/r03/ab/ab_staging_cache_policy.txt)
 __device__ __forceinline__ void ring_stage(Ring &r, uint32_t f, uint4 v) {
     if (r.fpos < VCFC_PRIM) vw::gstore16_nt(r.prim, f, v);
     else vw::gstore16_nt(r.slot, f - VCFC_PRIM, v);
@@ -196,6 +200,7 @@ struct Chunk {
 // cache policy of the encoder's line loads: plain (non-temporal loads are
 // 30 % slower: the prefix / genotype chunk overlap and the look-ahead rely on
 // L2 hits, profiles/r01/ab/ab_nt_loads.txt)
+// (genotype stream alone non-temporal: +14 %, ab_staging_cache_policy.txt)
 constexpr int PRE_AUX = 0, GT_AUX = 0;
 
 // The look-ahead dword after a lane's bytes is the next lane's first dword:

@@ -30,8 +30,13 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <fcntl.h>
+#include <unistd.h>
 #include <functional>
+#include <memory>
 #include <mutex>
+#include <new>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -53,6 +58,79 @@ struct Source {
 };
 // In-order output; false = I/O error (or no space).
 using Sink = std::function<bool(const uint8_t *, uint64_t)>;
+
+// Output held for a later placement (a rank of a sharded compress whose file
+// offset is known only after the all-gather of the ranks' byte counts): the
+// first mem_bound bytes in host memory (64 MiB blocks), the rest appended to
+// a spill file (unlinked at once; only its fd is kept).  place() writes the
+// held bytes at the given file offset: one pwrite per memory block, the spill
+// part copied in-kernel (copy_file_range) or by pread/pwrite -- so the bytes
+// that fit in memory are written once, to their final place.
+struct Held {
+    static constexpr uint64_t BLOCK = 64ull << 20;
+    std::vector<std::unique_ptr<uint8_t[]>> blocks;
+    uint64_t mem_bound = 0, mem = 0, spilled = 0;
+    std::string spill_dir;
+    int spill_fd = -1;
+    ~Held() {
+        if (spill_fd >= 0) close(spill_fd);
+    }
+    uint64_t bytes() const { return mem + spilled; }
+    bool append(const uint8_t *p, uint64_t k) {
+        while (k && mem < mem_bound) {
+            if (mem / BLOCK >= blocks.size()) {
+                blocks.emplace_back(new (std::nothrow) uint8_t[BLOCK]);
+                if (!blocks.back()) return false;
+            }
+            const uint64_t at = mem % BLOCK;
+            const uint64_t take = std::min<uint64_t>({k, BLOCK - at, mem_bound - mem});
+            memcpy(blocks[mem / BLOCK].get() + at, p, take);
+            p += take; k -= take; mem += take;
+        }
+        if (!k) return true;
+        if (spill_fd < 0) {
+            std::string path = (spill_dir.empty() ? std::string("/tmp") : spill_dir) + "/.vcfc-held-XXXXXX";
+            std::vector<char> t(path.begin(), path.end());
+            t.push_back('\0');
+            spill_fd = mkstemp(t.data());
+            if (spill_fd < 0) return false;
+            unlink(t.data());
+        }
+        while (k) {
+            const ssize_t w = pwrite(spill_fd, p, std::min<uint64_t>(k, 1ull << 30), (off_t)spilled);
+            if (w <= 0) return false;
+            p += w; k -= (uint64_t)w; spilled += (uint64_t)w;
+        }
+        return true;
+    }
+    bool place(int fd, uint64_t off) const {
+        auto put = [&](const uint8_t *b, uint64_t k, uint64_t at) {
+            while (k) {
+                const ssize_t w = pwrite(fd, b, std::min<uint64_t>(k, 1ull << 30), (off_t)at);
+                if (w <= 0) return false;
+                b += w; k -= (uint64_t)w; at += (uint64_t)w;
+            }
+            return true;
+        };
+        for (uint64_t q = 0; q * BLOCK < mem; q++)
+            if (!put(blocks[q].get(), std::min(BLOCK, mem - q * BLOCK), off + q * BLOCK)) return false;
+        uint64_t done = 0;
+        while (done < spilled) {   // in-kernel copy where the filesystems allow it
+            loff_t si = (loff_t)done, di = (loff_t)(off + mem + done);
+            const ssize_t c = copy_file_range(spill_fd, &si, fd, &di, spilled - done, 0);
+            if (c <= 0) break;
+            done += (uint64_t)c;
+        }
+        std::vector<uint8_t> tmp;
+        while (done < spilled) {
+            tmp.resize(std::min<uint64_t>(spilled - done, 64ull << 20));
+            const ssize_t r = pread(spill_fd, tmp.data(), tmp.size(), (off_t)done);
+            if (r <= 0 || !put(tmp.data(), (uint64_t)r, off + mem + done)) return false;
+            done += (uint64_t)r;
+        }
+        return true;
+    }
+};
 
 // Device and pinned host buffers, owned by the caller; contents not kept
 // between calls.

@@ -6,10 +6,12 @@ compress() (reference src/compress.cpp:205-257) is stateless per line -- the
 schema it tracks is never read by the encoder -- so any split at a line
 boundary can be compressed independently and the outputs concatenated in
 order.  Each rank streams its slice through the ingest pipeline on its own GPU
-(vcfc.Context.compress_range: reader threads, pinned H2D, GPU line index +
-encode), all-gathers (bytes, status, failing line, lines) -- RCCL on GPU
-ranks, gloo in the CPU tests -- and places its output at the exclusive
-prefix of the byte counts.
+(reader threads, pinned H2D, GPU line index + encode): rank 0 writes its
+output in place, every other rank holds its output in host memory
+(vcfc.Context.compress_range_held); one all-gather of (bytes, status, failing
+line, lines) -- RCCL on GPU ranks, gloo in the CPU tests -- gives each rank
+its offset, the exclusive prefix of the byte counts, where it writes the held
+bytes once.
 
 Run: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \\
          vcf-compression_amd/dist_compress.py [sparsify] in out
@@ -19,9 +21,11 @@ halo record each side, one all-gather of the plans' verdicts).
 """
 import os
 import sys
-import tempfile
 
 E_IO = 7   # include/vcfc.h VCFC_E_IO
+# output a rank holds in host memory until its offset is known (the rest
+# spills to a temporary file beside the output): VCFC_HOLD_GB, default 32
+HOLD_BYTES = int(float(os.environ.get("VCFC_HOLD_GB", "32")) * (1 << 30))
 
 
 def split_points(data_len, world, read_at):
@@ -50,52 +54,29 @@ def exclusive_offsets(counts):
     return offs, acc
 
 
-def copy_to(src_fd, dst_fd, n, dst_off):
-    """Copy bytes [0, n) of src_fd to dst_fd at dst_off: copy_file_range (in
-    the kernel; a reflink where the filesystem has them), else a pread/pwrite
-    loop.  Both loop until every byte is placed (one call moves < 2 GiB)."""
-    done = 0
-    try:
-        while done < n:
-            k = os.copy_file_range(src_fd, dst_fd, n - done, done, dst_off + done)
-            if k <= 0:
-                raise OSError("copy_file_range made no progress")
-            done += k
-        return
-    except (OSError, AttributeError):
-        pass
-    while done < n:
-        b = os.pread(src_fd, min(n - done, 64 << 20), done)
-        if not b:
-            raise OSError("short read of a shard's spill file")
-        mv = memoryview(b)
-        while len(mv):
-            w = os.pwrite(dst_fd, mv, dst_off + done)
-            if w <= 0:
-                raise OSError("pwrite made no progress")
-            mv = mv[w:]
-            done += w
-
-
-def compress_shard(in_path, out_path, rank, world, compress_range, allgather):
+def compress_shard(in_path, out_path, rank, world, compress_range, hold, allgather):
     """One rank of a sharded compress.
 
     compress_range(in_path, off, length, fd, out_off) -> (status, bytes
     written, 1-based failing line in the range or -1, lines in the range)
-    streams the rank's line-aligned byte range through the ingest pipeline
-    (vcfc.Context.compress_range) and writes its output to fd from out_off on;
-    allgather(list_of_ints) -> per-rank lists.  Rank 0's output starts the
-    file, so it writes in place; every other rank spills to a temporary file
-    beside the output and, once one all-gather has given it its offset (the
-    exclusive prefix of the byte counts), copies the spill there.  No rank
-    reads outside its own range, and no slice is held in memory.
+    streams a line-aligned byte range through the ingest pipeline
+    (vcfc.Context.compress_range) straight into fd at out_off: rank 0, whose
+    output starts the file, uses it.  hold(in_path, off, length) -> (status,
+    bytes, failing line, lines, held) does the same with the output held in
+    host memory (spilling past a bound, vcfc_compress_range_held): every
+    other rank uses it, and once one all-gather of (bytes, status, failing
+    line, lines) has given it its offset -- the exclusive prefix of the byte
+    counts -- places the held bytes there with held.place(fd, off).  Output
+    that fits in memory is written once, to its final place; no rank reads
+    outside its own range.  A second all-gather carries the placements'
+    statuses.  allgather(list_of_ints) -> per-rank lists.
 
     Returns (status, total bytes, global failing line or -1) -- the same on
     every rank.  The output file equals the single-process output: on a
     failure, everything before the first failing line in file order (the
     reference stops there, src/compress.cpp:205-257).  Errors that are not
-    about the VCF (HIP, I/O) travel through the same all-gather, so no rank
-    is left waiting in the collective."""
+    about the VCF (HIP, I/O) travel through the same all-gathers, so no rank
+    is left waiting in a collective."""
     size = os.path.getsize(in_path)
     with open(in_path, "rb") as f:
         def read_at(off, n):
@@ -104,16 +85,14 @@ def compress_shard(in_path, out_path, rank, world, compress_range, allgather):
         pts = split_points(size, world, read_at)
     lo, hi = pts[rank], pts[rank + 1]
     fd = os.open(out_path, os.O_WRONLY | os.O_CREAT, 0o644)
-    pfd, part = -1, None
+    held = None
     try:
         try:
             if rank == 0:
                 st, nb, eline, lines = compress_range(in_path, lo, hi - lo, fd, 0)
             else:
-                pfd, part = tempfile.mkstemp(prefix=".vcfc-part%d-" % rank,
-                                             dir=os.path.dirname(os.path.abspath(out_path)))
-                st, nb, eline, lines = compress_range(in_path, lo, hi - lo, pfd, 0)
-        except Exception as e:   # still take part in the collective
+                st, nb, eline, lines, held = hold(in_path, lo, hi - lo)
+        except Exception as e:   # still take part in the collectives
             print("vcfc rank %d: %s" % (rank, e), file=sys.stderr)
             st, nb, eline, lines = E_IO, 0, -1, 0
         g = allgather([int(nb), int(st), int(eline), int(lines)])
@@ -128,16 +107,22 @@ def compress_shard(in_path, out_path, rank, world, compress_range, allgather):
             gline = sum(x[3] for x in g[:first_bad]) + eb if eb >= 0 else -1
         else:
             status, gline = 0, -1
-        if rank > 0 and rank <= first_bad and counts[rank]:
-            copy_to(pfd, fd, counts[rank], offs[rank])
-        if rank == world - 1:
-            os.ftruncate(fd, total)
+        pst = 0
+        try:
+            if rank > 0 and rank <= first_bad and counts[rank]:
+                pst = held.place(fd, offs[rank]) if held is not None else E_IO
+            if rank == world - 1:
+                os.ftruncate(fd, total)
+        except Exception as e:
+            print("vcfc rank %d: %s" % (rank, e), file=sys.stderr)
+            pst = E_IO
+        p = allgather([int(pst)])
+        if any(x[0] for x in p) and status == 0:
+            status = next(x[0] for x in p if x[0])
     finally:
         os.close(fd)
-        if pfd >= 0:
-            os.close(pfd)
-        if part:
-            os.unlink(part)
+        if held is not None:
+            held.free()
     return status, total, gline
 
 
@@ -200,6 +185,12 @@ def main():
             return vcfc.E_HIP, 0, -1, 0
         return ctx.compress_range(path, off, length, fd, out_off)
 
+    def hold(path, off, length):
+        if ctx is None:
+            return vcfc.E_HIP, 0, -1, 0, None
+        return ctx.compress_range_held(path, off, length, mem_bound=HOLD_BYTES,
+                                       spill_dir=os.path.dirname(os.path.abspath(out_path)))
+
     def allgather(vals):
         if world == 1:
             return [vals]
@@ -222,7 +213,7 @@ def main():
         st = sparsify_shards(rank, world, shard, whole, allgather)
         line = -1
     else:
-        st, total, line = compress_shard(in_path, out_path, rank, world, compress_range, allgather)
+        st, total, line = compress_shard(in_path, out_path, rank, world, compress_range, hold, allgather)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

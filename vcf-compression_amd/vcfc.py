@@ -36,7 +36,8 @@ EXPORTS = [
     "vcfc_decode_records_device", "vcfc_parse_query", "vcfc_query_buffer", "vcfc_query_file",
     "vcfc_query_match_device", "vcfc_decode_selected_device", "vcfc_sparse_query_file",
     "vcfc_sparsify_shard", "vcfc_ctx_set_ingest_chunk", "vcfc_record_hash_device",
-    "vcfc_compress_range", "vcfc_compress_device",
+    "vcfc_compress_range", "vcfc_compress_device", "vcfc_compress_range_held", "vcfc_held_place",
+    "vcfc_held_sizes", "vcfc_held_free",
 ]
 
 
@@ -69,6 +70,13 @@ def lib():
     L.vcfc_record_hash_device.argtypes = [vp, vp, u64, vp, vp]
     L.vcfc_compress_range.argtypes = [vp, ctypes.c_char_p, u64, u64, ctypes.c_int, u64, ctypes.POINTER(u64),
                                       ctypes.POINTER(i64), ctypes.POINTER(u64)]
+    L.vcfc_compress_range_held.argtypes = [vp, ctypes.c_char_p, u64, u64, u64, ctypes.c_char_p, ctypes.POINTER(vp),
+                                           ctypes.POINTER(u64), ctypes.POINTER(i64), ctypes.POINTER(u64)]
+    L.vcfc_held_place.argtypes = [vp, ctypes.c_int, u64]
+    L.vcfc_held_sizes.argtypes = [vp, ctypes.POINTER(u64), ctypes.POINTER(u64)]
+    L.vcfc_held_sizes.restype = None
+    L.vcfc_held_free.argtypes = [vp]
+    L.vcfc_held_free.restype = None
     L.vcfc_compress_data_line.argtypes = [vp, ctypes.c_char_p, u64, ctypes.c_int, vp, u64, ctypes.POINTER(u64)]
     L.vcfc_encode_bound.restype = u64
     L.vcfc_encode_bound.argtypes = [u64, u64]
@@ -146,6 +154,27 @@ def parse_coordinate_string(q):
                3: "Failed to parse int from end position: %s" % qb[dash + 1:].decode(errors="replace")}.get(st)
         raise ValueError(msg or strerror(st))
     return VcfCoordinateQuery(qb[:ref_len.value], bool(has_range.value), start.value, end.value)
+
+
+class Held:
+    """Output of Context.compress_range_held, placed once its offset is known."""
+
+    def __init__(self, h):
+        self._h = h
+
+    def place(self, fd, off):
+        """Write every held byte at file offset `off` of fd; returns the status."""
+        return lib().vcfc_held_place(self._h, fd, off) if self._h else E_ARG
+
+    def sizes(self):
+        m, sp = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        lib().vcfc_held_sizes(self._h, ctypes.byref(m), ctypes.byref(sp))
+        return m.value, sp.value
+
+    def free(self):
+        if self._h:
+            lib().vcfc_held_free(self._h)
+            self._h = None
 
 
 class Context:
@@ -236,6 +265,17 @@ class Context:
         st = lib().vcfc_compress_range(self._h, in_path.encode(), off, length, out_fd, out_off, ctypes.byref(nb),
                                        ctypes.byref(line), ctypes.byref(lines))
         return st, nb.value, line.value, lines.value
+
+    def compress_range_held(self, in_path, off, length, mem_bound=16 << 30, spill_dir=None):
+        """compress_range with the output held (host memory up to mem_bound
+        bytes, the rest in a spill file) until its file offset is known.
+        Returns (status, bytes, failing line in the range or -1, lines in the
+        range, Held); does not raise."""
+        nb, line, lines, h = ctypes.c_uint64(0), ctypes.c_int64(-1), ctypes.c_uint64(0), ctypes.c_void_p()
+        st = lib().vcfc_compress_range_held(self._h, in_path.encode(), off, length, mem_bound,
+                                            spill_dir.encode() if spill_dir else None, ctypes.byref(h),
+                                            ctypes.byref(nb), ctypes.byref(line), ctypes.byref(lines))
+        return st, nb.value, line.value, lines.value, Held(h.value)
 
     def decompress_buffer(self, data, cap=None):
         """.vcfc bytes -> VCF bytes, as decompress2_fd (reference
