@@ -208,3 +208,24 @@ def test_logical_shards_stitch_on_one_gpu(vcfc, world):
             t.join(120)
         assert all(r is not None and r[0] == 0 for r in res), res
         assert open(op, "rb").read() == want
+
+
+@pytest.mark.parametrize("seed", [51, 52, 53, 54])
+def test_variable_token_rows(ctx, seed):
+    """k_encode_var on the GPU: rows of odd-length tokens (haploid beside
+    diploid, '.', GT:DP:GQ, 41-byte tokens, all-1-byte rows, long runs broken
+    by 1-byte escapes) plus rows it must hand on (even-length tokens, empty
+    fields, a trailing TAB, CR, a failure in the third chunk), through
+    compress_buffer: byte-exact against the oracle."""
+    import random
+    import test_kernel_emu as T
+    rnd = random.Random(seed)
+    lines = T._var_rows(rnd, 120, ["hap", "dot", "long", "ones", "runs", "gdg"])
+    lines += [T.PFX_V + b"0\t1|1\t10\t0|0", T.PFX_V + b"0\t\t1|1\t0", T.PFX_V + b"1\t0|0\t",
+              T.PFX_V + b"\t".join([b"0"] * 2000 + [b"10", b"11", b"1"])]
+    rnd.shuffle(lines)
+    hdr = b"##fileformat=VCFv4.2\n#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\tS0\n"
+    data = hdr + b"\n".join(lines) + b"\n"
+    st, want, _ = G.oracle_compress(data)
+    assert st == 0
+    assert ctx.compress_buffer(data) == want

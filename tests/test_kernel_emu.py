@@ -276,3 +276,91 @@ def test_output_capacity_short():
         st2, out2, ro2, err2 = E.emu_encode(bytes(buf), np.array(offs, np.uint64), np.array(lens, np.uint32), cap=cap)
         assert err2 == (cut_row << 8) | 4, (cut_row, hex(err2))
         assert out2[:int(ro[cut_row])] == out[:int(ro[cut_row])]
+
+
+PFX_V = b"X\t100\trs1\tA\tG\t50\tPASS\tAC=1\tGT\t"
+
+
+def _var_rows(rnd, n, kinds):
+    """Rows of odd-length tokens (the variable-token kernel's shape)."""
+    rows = []
+    for i in range(n):
+        kind = kinds[i % len(kinds)]
+        S = rnd.choice([1, 2, 3, 17, 63, 64, 65, 200, 511, 512, 513, 1023, 1024, 1025, 1500, 2600])
+        toks = []
+        p00 = rnd.choice([0.0, 0.5, 0.9, 0.99, 1.0])
+        for j in range(S):
+            if kind == "hap":       # haploid beside diploid
+                toks.append(rnd.choice([b"0", b"1"]) if (j * 7 + i) % 3 == 0 else
+                            (b"0|0" if rnd.random() < p00 else rnd.choice([b"0|1", b"1|0", b"1|1", b"0|0"])))
+            elif kind == "dot":     # "." for missing
+                toks.append(b"." if rnd.random() < 0.2 else (b"0|0" if rnd.random() < p00 else
+                                                                  rnd.choice([b"0|1", b"1|1", b"2|1"])))
+            elif kind == "long":    # GT:DP:GQ and other odd lengths
+                toks.append(rnd.choice([b"0|0:35:99", b"0|1:17:12", b"1|1:123:9", b"0|0", b"1", b"./.",
+                                        b"0|0:1", b"0" * 41]))
+            elif kind == "gdg":     # escapes of 1, 5, 9 and 41 bytes only (the escape-chunk step)
+                toks.append(rnd.choice([b"0|0:35:99", b"0|1:17:12", b"1|1:123:9", b"0|0:1", b"1", b"0" * 41]))
+            elif kind == "ones":    # every token one byte
+                toks.append(rnd.choice([b"0", b"1", b"."]))
+            else:                   # plain runs with long 1-byte stretches
+                toks.append(b"0|0" if (j // 200) % 2 == 0 else b"1")
+        rows.append(PFX_V + b"\t".join(toks))
+    return rows
+
+
+@pytest.mark.parametrize("seed", [51, 52, 53])
+def test_variable_token_rows(seed):
+    """k_encode_var: rows whose tokens all have odd length (1, 3, 5, 9, 41
+    bytes) -- haploid beside diploid, '.', GT:DP:GQ, all-1-byte rows, long
+    0|0 runs broken by 1-byte escapes -- byte-exact against the oracle at
+    every alignment of the buffer; only rows mixing tokens longer than 3
+    bytes with 3-byte ones may be left to k_encode_general."""
+    rnd = random.Random(seed)
+    lines = _var_rows(rnd, 72, ["hap", "dot", "long", "ones", "runs", "gdg"])
+    want = [G.oracle_encode_line(x) for x in lines]
+    assert all(w[0] == 0 for w in want)
+    for lead in (0, 1, 2, 3, 7, 13):
+        st, out, ro, err = run(lines, lead)
+        assert err == (1 << 64) - 1
+        for i, (_, rec) in enumerate(want):
+            assert out[int(ro[i]):int(ro[i + 1])] == rec, (seed, lead, i)
+        # only rows with a token longer than 3 bytes may go on to
+        # k_encode_general (those mixing them with 3-byte tokens)
+        longer = sum(1 for x in lines if max(len(t) for t in x[len(PFX_V):].split(b"\t")) > 3)
+        assert E.LAST_RETRIES[0] <= longer, (E.LAST_RETRIES[0], longer)
+
+
+def test_variable_token_rows_fall_back():
+    """Rows the variable-token kernel must hand on (even-length tokens, empty
+    fields, a trailing TAB, CR) are encoded by k_encode_general, and the
+    others of the batch stay exact."""
+    rnd = random.Random(77)
+    good = _var_rows(rnd, 8, ["hap", "long"])
+    bad = [PFX_V + b"0\t1|1\t10\t0|0", PFX_V + b"0\t\t1|1\t0", PFX_V + b"1\t0|0\t", PFX_V + b"0|0\t1\t0\r",
+           PFX_V + b"0\t" * 600 + b"00",
+           PFX_V + b"\t".join([b"0"] * 2000 + [b"10", b"11", b"1"])]   # fails in its third chunk
+    lines = [x for pair in zip(good, bad + bad[:2]) for x in pair]
+    st, out, ro, err = run(lines)
+    assert err == (1 << 64) - 1
+    for i, x in enumerate(lines):
+        assert out[int(ro[i]):int(ro[i + 1])] == G.oracle_encode_line(x)[1], i
+    longer = sum(1 for x in good if max(len(t) for t in x[len(PFX_V):].split(b"\t")) > 3)
+    assert 8 <= E.LAST_RETRIES[0] <= 8 + longer
+
+
+def test_law2_synthetic_rows():
+    """The synthetic law-2 rows (bench.py --law 2; kinds haploid, GT:DP:GQ,
+    missing, unphased, '.'): byte-exact, and none of them reaches
+    k_encode_general (GT:DP:GQ rows take the variable-token kernel's escape
+    chunks)."""
+    rows = E.emu_synth_rows(40, 700, 2, seed=9)
+    buf, lo, ll = rows
+    st, out, ro, err = E.emu_encode(buf, lo, ll)
+    assert err == (1 << 64) - 1
+    gdg = 0
+    for i in range(len(lo)):
+        line = bytes(buf[int(lo[i]):int(lo[i]) + int(ll[i])])
+        gdg += b"GT:DP:GQ" in line
+        assert out[int(ro[i]):int(ro[i + 1])] == G.oracle_encode_line(line)[1], i
+    assert gdg > 0 and E.LAST_RETRIES[0] == 0

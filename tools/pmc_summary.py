@@ -12,7 +12,7 @@ from collections import defaultdict
 def load(root, ksub=None):
     vals = defaultdict(lambda: defaultdict(list))
     dur = defaultdict(list)
-    for f in glob.glob(os.path.join(root, "pmc*_*", "run_counter_collection.csv")):
+    for f in glob.glob(os.path.join(root, "pmc*", "run_counter_collection.csv")):
         seen = set()
         for r in csv.DictReader(open(f)):
             name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]

@@ -29,6 +29,7 @@
 // the REQ bytes: `linebuf.append(buf)` stops at a NUL, compress.cpp:798),
 // then S four-byte words "a|b\t" with the last TAB replaced by LF.
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <vcfc_wave.h>   // angle brackets: tests/simt_emu shadows it
 #include "vcfc_device.h"
 
@@ -455,7 +456,10 @@ __device__ __forceinline__ void write_one(const VcfcDecodeArgs &a, uint64_t i, u
     constexpr uint32_t PL = TB / 64;   // slots per lane
     for (uint32_t q = 0; q < PL; q += 4) *reinterpret_cast<uint4 *>(W + PL * l + q) = make_uint4(0, 0, 0, 0);
     uint32_t j0 = 0, carry = 0;   // tile start; word of the item holding token j0
-    auto tile_out = [&](uint32_t n_tok) {
+    // LAST: the line's last tile (n_tok tokens, its LF replacing the last
+    // TAB, partial stores); the others are whole tiles of TB tokens
+    auto tile_out = [&](auto last_tag, uint32_t n_tok) {
+        constexpr bool LAST = decltype(last_tag)::value;
         vw::wave_sync();
         uint32_t w[PL];
 #pragma unroll
@@ -477,19 +481,23 @@ __device__ __forceinline__ void write_one(const VcfcDecodeArgs &a, uint64_t i, u
 #pragma unroll
         for (uint32_t q = 0; q < PL; q++) w[q] = w[q] ? w[q] : enter;
         const uint32_t t0 = j0 + PL * l;
-        if (j0 + n_tok == S) {   // the line's last tile: its LF replaces the last TAB
-#pragma unroll
-            for (uint32_t q = 0; q < PL; q++)
-                if (t0 + q + 1 == S) w[q] = (w[q] & 0x00FFFFFFu) | 0x0A000000u;
-        }
-        if (t0 + PL <= j0 + n_tok) {
+        if (!LAST) {
 #pragma unroll
             for (uint32_t q = 0; q < PL; q += 4)
                 // (non-temporal: -0.3 % in an A/B, ab_dec_nt.txt)
                 vw::gstore16_nt(tok, 4ull * (t0 + q), make_uint4(w[q], w[q + 1], w[q + 2], w[q + 3]));
         } else {
+#pragma unroll
             for (uint32_t q = 0; q < PL; q++)
-                if (t0 + q < j0 + n_tok) *reinterpret_cast<uint32_t *>(tok + 4ull * (t0 + q)) = w[q];
+                if (t0 + q + 1 == S) w[q] = (w[q] & 0x00FFFFFFu) | 0x0A000000u;
+            if (t0 + PL <= j0 + n_tok) {
+#pragma unroll
+                for (uint32_t q = 0; q < PL; q += 4)
+                    vw::gstore16_nt(tok, 4ull * (t0 + q), make_uint4(w[q], w[q + 1], w[q + 2], w[q + 3]));
+            } else {
+                for (uint32_t q = 0; q < PL; q++)
+                    if (t0 + q < j0 + n_tok) *reinterpret_cast<uint32_t *>(tok + 4ull * (t0 + q)) = w[q];
+            }
         }
         carry = vw::readlane(w[PL - 1], 63);
         vw::wave_sync();
@@ -526,12 +534,13 @@ __device__ __forceinline__ void write_one(const VcfcDecodeArgs &a, uint64_t i, u
                 const uint32_t o = ws[j] - j0;
                 W[o < TB ? o : TB] = w[j];
             }
-            if (st.got < j0 + TB || j0 + TB > S) break;   // the tile is not complete yet
-            tile_out(TB);
+            // the tile is not complete yet, or it is the line's last
+            if (st.got < j0 + TB || j0 + TB >= S) break;
+            tile_out(std::false_type(), TB);
             j0 += TB;
         }
     }
-    if (j0 < S) tile_out(S - j0);
+    if (j0 < S) tile_out(std::true_type(), S - j0);
     // a light plan assumed this record simple: check it (tokens past S were
     // never stored; the line's bytes are rewritten by the exact rerun)
     if ((st.bad || st.got != S || req_bad) && l == 0)

@@ -142,6 +142,20 @@ __device__ __forceinline__ void ring_flush(Ring &r, bool final) {
     vw::wave_sync();
 }
 
+// Bytes a lane wrote past the ring end (into the 64-byte tail) belong at the
+// ring start.  At most one lane of a step straddles the end (the lanes after
+// it start from a masked position); the wave moves its tail bytes with one
+// byte per lane instead of that lane copying them one by one.
+__device__ __forceinline__ void ring_unwrap(Ring &r, uint32_t end) {   // end: the lane's unmasked end position
+    const uint64_t wb = vw::ballot(end > RING);
+    if (wb) {
+        const uint32_t n = vw::readlane(end, (uint32_t)__builtin_ctzll(wb)) - RING;   // <= RING_TAIL
+        const uint32_t l = vw::lane_id();
+        const uint8_t v = r.lds[RING + l];
+        if (l < n) r.lds[l] = v;
+    }
+}
+
 // Finish a record: header words go straight to the staging (lane 0 also
 // wrote its first 16 bytes during the flush, so program order keeps them).
 __device__ void ring_finish(Ring &r, uint32_t req) {
@@ -235,7 +249,10 @@ struct FastState {
 };
 
 // Prefix phase for chunk c: 0 = no sample yet, 1 = first sample starts in
-// this chunk (its tokens still to do), 2 = not the fast shape.
+// this chunk (its tokens still to do), 2 = not the fast shape.  VAR (the
+// variable-token kernel): the genotype region need only hold odd-length
+// tokens (f.T = its 2-byte half-slots instead of its tokens).
+template <bool VAR>
 __device__ __forceinline__ int fast_prefix_step(const Chunk &cur, uint32_t c, uint32_t lead, uint32_t len,
                                                 FastState &f, Ring &r) {
     const uint32_t l = vw::lane_id();
@@ -309,9 +326,16 @@ __device__ __forceinline__ int fast_prefix_step(const Chunk &cur, uint32_t c, ui
     f.gt0 = (int32_t)x9;
     r.wpos = 8u + x9;
     const uint32_t glen = len - x9;
-    if (((glen + 1) & 3u) != 0) return 2;
-    f.T = (glen + 1) >> 2;
     f.phi = (lead + x9) & 3u;
+    if (VAR) {
+        // odd-length tokens and single TABs: glen + 1 is even, and every
+        // token starts on an even offset from token 0
+        if (((glen + 1) & 1u) != 0) return 2;
+        f.T = (glen + 1) >> 1;
+    } else {
+        if (((glen + 1) & 3u) != 0) return 2;
+        f.T = (glen + 1) >> 2;
+    }
     if (f.T >= (1u << 23) - 2 * MOD_BIAS) return 2;   // mod_cap is exact below 2^23
     return 1;
 }
@@ -540,12 +564,7 @@ __device__ __forceinline__ void clean8(const uint32_t (&d)[TPL8], int32_t t0, in
             }
             s2 &= s2 - 1u;
         }
-        const bool wrap = base + n2 > RING;
-        if (vw::ballot(wrap)) {
-            if (wrap) {
-                for (uint32_t q = RING; q < base + n2; q++) r.lds[q - RING] = r.lds[q];
-            }
-        }
+        ring_unwrap(r, base + n2);
     }
     r.wpos += vw::readlane(incl2, 63);
     f.pcls = (vw::readlane(cbH, 63) >> 24) & 3u;
@@ -677,12 +696,7 @@ __device__ __forceinline__ void esc8(const uint32_t (&d)[TPL8], int32_t t0, int3
         o += 4u * (uint32_t)e;
         njp = s ? -j : njp;
     }
-    const bool wrap = base + cnt > RING;
-    if (vw::ballot(wrap)) {
-        if (wrap) {
-            for (uint32_t q = RING; q < base + cnt; q++) r.lds[q - RING] = r.lds[q];
-        }
-    }
+    ring_unwrap(r, base + cnt);
     r.wpos += vw::readlane(incl2, 63);
     f.pcls = (vw::readlane(cbH, 63) >> 24) & 7u;
     f.prs = vw::umax(vw::readlane(incl, 63), f.prs);
@@ -811,7 +825,7 @@ __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring
     Chunk b = load_chunk(rsA, 0, lo16);
     int st;
     for (;;) {
-        st = (int)vw::readfirst((uint32_t)fast_prefix_step(look_ahead(b), c, lead, len, f, r));
+        st = (int)vw::readfirst((uint32_t)fast_prefix_step<false>(look_ahead(b), c, lead, len, f, r));
         if (st != 0) break;
         c = vw::readfirst(c + 1);
         if (c >= nch) return false;   // < 10 fields
@@ -875,6 +889,332 @@ __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring
     }
     r.wpos += extra + 1;
     ring_finish(r, (uint32_t)gt0);
+    *rec_bytes = r.wpos;
+    return true;
+}
+
+
+// ---------------------------------------------------------------------------
+// Variable-token path (k_encode_var): rows the fast kernel hands back whose
+// genotype tokens all have odd length and are separated by single TABs --
+// haploid "0" beside diploid "0|1", "." for missing samples, "0|1:35:99"
+// (GT:DP:GQ).  Then every token starts an even number of bytes after token 0,
+// so the genotype region is a sequence of 2-byte half-slots: a token is a
+// start half and continuation halves up to the half whose second byte is its
+// TAB.  One wave streams 2 KiB chunks (lane l: half-slots [16 l, 16 l + 16)),
+// three in flight, with fixed-trip per-half work:
+//   - TAB masks give the token starts; a start whose 4 bytes read "a|b\t"
+//     (a, b in {0,1}) is a plain token of class 2a + b, any other an escape;
+//   - classes fill forward to the continuation halves (segmented doubling),
+//     so a half's predecessor class is the class of the half before it;
+//   - run starts, the entering run (wave max-scan) and its offset mod cap
+//     follow esc8's rules over token indices (a wave add-scan of starts);
+//   - emission per half: [lead][0xE1 at an escape start][both bytes of an
+//     escape half].  An escape's last half carries its trailing TAB, so a
+//     start after an escape emits no lead byte (the reference's '\t' after
+//     an escape, compress.cpp:181-184, is that TAB); the row's last half
+//     drops its second byte (the line end).
+// Bytes leave as one unaligned dword store per half, issued from the lane's
+// last half to its first with each dword holding the bytes that follow it,
+// so only a lane's last emitting half writes past its end (<= 3 bytes, into
+// the next lanes' first bytes); a final store rewrites every lane's first
+// min(count, 4) bytes.  Rows of other shapes stay flagged for
+// k_encode_general.
+constexpr uint32_t HPC = 1024;   // half-slots per 2 KiB chunk
+
+struct VarState : FastState {
+    uint32_t ntok;   // tokens started so far
+};
+
+struct Chunk8v {
+    uint4 a, b;
+    uint32_t y, y2;   // lane 63: the 8 bytes after the chunk (others: from the next lane by DPP)
+};
+__device__ __forceinline__ Chunk8v load_chunk8v(vw::brsrc rs, uint32_t C, uint32_t lo32) {
+    Chunk8v k;
+    const uint32_t off = C * CHUNK8 + lo32;
+    const uint32_t la = la_off(lo32, 63 * BPL8);
+    k.a = vw::bload16(rs, off, GT_AUX);
+    k.b = vw::bload16(rs, off + 16u, GT_AUX);
+    k.y = vw::bload4(rs, off + 32u + la, GT_AUX);
+    k.y2 = vw::bload4(rs, off + 36u + la, GT_AUX);
+    return k;
+}
+
+// 4-bit zero-byte mask -> its even bytes (0, 2) / odd bytes (1, 3) as 2 bits
+__device__ __forceinline__ uint32_t even2(uint32_t z) { return (z & 1u) | ((z >> 1) & 2u); }
+__device__ __forceinline__ uint32_t odd2(uint32_t z) { return ((z >> 1) & 1u) | ((z >> 2) & 2u); }
+
+// Flush in 512-byte granules: a half burst (lanes 0..31) to reach a 1 KiB
+// boundary, full bursts, then a half burst, so < 512 bytes stay pending and
+// the next chunk (<= 49 bytes per lane, < 3.2 KiB) fits the 4 KiB ring.  No
+// burst straddles the staging regions (fpos stays a multiple of 512 and a
+// full burst starts on a 1 KiB boundary).
+__device__ __forceinline__ void ring_half_burst(Ring &r, uint32_t l) {
+    if (l < 32) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(r.lds + ((r.fpos + 16u * l) & RMASK));
+        ring_stage(r, r.fpos + 16u * l, v);
+    }
+    r.fpos += BURST / 2;
+}
+__device__ __forceinline__ void ring_flush_var(Ring &r) {
+    const uint32_t l = vw::lane_id();
+    r.wpos = vw::readfirst(r.wpos);
+    r.fpos = vw::readfirst(r.fpos);
+    vw::wave_sync();
+    if ((r.fpos & (BURST / 2)) && r.wpos - r.fpos >= BURST / 2) ring_half_burst(r, l);
+    if (r.wpos - r.fpos >= BURST) {
+        ring_burst(r, l);
+        if (r.wpos - r.fpos >= BURST) {
+            ring_burst(r, l);
+            if (r.wpos - r.fpos >= BURST) ring_burst(r, l);
+        }
+    }
+    if (r.wpos - r.fpos >= BURST / 2) ring_half_burst(r, l);
+    vw::wave_sync();
+}
+
+// One 2 KiB chunk C of a variable-token row.  false: not this shape (the
+// row goes to k_encode_general; nothing of it is kept).
+__device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState &f, Ring &r) {
+    const uint32_t l = vw::lane_id();
+    const uint32_t NH = f.T, phi = f.phi;
+    // dwords realigned to token 0: d[j] = token-relative bytes [2048 C + 32 l + 4 j, +4); d[8] the next lane's first
+    const uint32_t ya = vw::shl1(cur.a.x, cur.y), yb = vw::shl1(cur.a.y, cur.y2);
+    const uint32_t w[10] = {cur.a.x, cur.a.y, cur.a.z, cur.a.w, cur.b.x, cur.b.y, cur.b.z, cur.b.w, ya, yb};
+    uint32_t d[9];
+#pragma unroll
+    for (int j = 0; j < 9; j++) d[j] = vw::alignbyte(w[j + 1], w[j], phi);
+    const int32_t lastrel = (int32_t)NH - 1 - (int32_t)(C * HPC + 16u * l);   // the row's last half, lane-relative
+    const uint32_t vm = lastrel >= 15 ? 0xFFFFu : lastrel < 0 ? 0u : (2u << lastrel) - 1u;   // valid halves
+    // TAB masks over halves 0..17: tb0 = first byte TAB (never valid), tb1 = second byte TAB (a token's end);
+    // plain 3-byte candidates: bytes "a|b" from the half, a, b in {0,1}; a, b bits
+    uint32_t tb0 = 0, tb1 = 0;
+#pragma unroll
+    for (int j = 0; j < 9; j++) {
+        const uint32_t z = zero_bytes4(d[j] ^ 0x09090909u);
+        tb0 |= even2(z) << (2 * j);
+        tb1 |= odd2(z) << (2 * j);
+    }
+    if (lastrel >= 0 && lastrel <= 17) tb1 |= 1u << lastrel;   // the row's last half ends its token (line end)
+    if (vw::ballot((tb0 & vm) != 0)) return false;           // an empty field, or a token of even length
+    // token starts: after a half whose second byte is a TAB (lane 0: the chunk carry)
+    const uint32_t pin = vw::shr1((tb1 >> 15) & 1u, f.carryT);
+    const uint32_t S = ((tb1 << 1) | pin) & vm;
+    const uint32_t L3 = S & ~tb1 & (tb1 >> 1);                 // 3-byte tokens (plain or not)
+    const uint32_t nt = (uint32_t)__builtin_popcount(S);
+    const uint32_t tinc = vw::scan_add(nt);
+    if ((f.pcls == CLS_ESC || f.pcls == CLS_NONE) && vw::ballot(L3 != 0) == 0) {
+        // Escape chunk: no 3-byte token starts here and the token entering
+        // the chunk is an escape (or this is token 0: no lead byte), so
+        // every half belongs to an escape (1 byte, or 5 and more: GT:DP:GQ):
+        // each emits its bytes, a start 0xE1 first -- the input with 0xE1
+        // before every token.
+        const bool lastin = lastrel >= 0 && lastrel < 16;
+        const uint32_t cnt = nt + 2u * (uint32_t)__builtin_popcount(vm) - (lastin ? 1u : 0u);
+        const uint32_t incl2 = vw::scan_add(cnt);
+        const uint32_t base = (r.wpos + incl2 - cnt) & RMASK;
+        uint8_t *const lb0 = r.lds + base;
+        uint8_t *const dm = r.lds + RING_DUMMY;
+        // byte stores (unaligned dword stores from every lane wait ~100x
+        // longer to issue: SQ_WAIT_INST_LDS, profiles/r03/pmc/pmc_var_kind1*)
+        uint32_t o = 0;
+#pragma unroll
+        for (int h = 0; h < 16; h++) {
+            const uint32_t es = (S >> h) & 1u;
+            const uint32_t np = (vm >> h) & 1u ? ((int32_t)h == lastrel ? 1u : 2u) : 0u;
+            const uint32_t pay = d[h >> 1] >> (16 * (h & 1));
+            *(es ? lb0 + o : dm) = (uint8_t)0xE1u;
+            o += es;
+            *(np ? lb0 + o : dm) = (uint8_t)pay;
+            *(np == 2u ? lb0 + o + 1 : dm) = (uint8_t)(pay >> 8);
+            o += np;
+        }
+        ring_unwrap(r, base + cnt);
+        r.wpos += vw::readlane(incl2, 63);
+        const uint32_t tot = vw::readlane(tinc, 63);
+        f.ntok += tot;
+        if (tot) f.prs = f.ntok;   // every escape starts a run: the last token's
+        f.pcls = CLS_ESC;
+        f.carryT = vw::readlane((tb1 >> 15) & 1u, 63);
+        ring_flush_var(r);
+        return true;
+    }
+    // tokens longer than 3 bytes beside 3-byte ones (or after a plain token)
+    // are left to k_encode_general
+    if (vw::ballot((S & ~tb1 & ~(tb1 >> 1)) != 0)) return false;
+    // plain 3-byte candidates: bytes "a|b" from the half, a, b in {0,1}; a, b bits
+    constexpr uint32_t Z3 = 0x00307C30u;   // "0|0"
+    uint32_t p3 = 0, am = 0, bm = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const uint32_t e = d[j], o = vw::alignbyte(d[j + 1], d[j], 2);
+        p3 |= ((((e ^ Z3) & 0x00FEFFFEu) == 0 ? 1u : 0u) | (((o ^ Z3) & 0x00FEFFFEu) == 0 ? 2u : 0u)) << (2 * j);
+        am |= ((e & 1u) | ((o & 1u) << 1)) << (2 * j);
+        bm |= (((e >> 16) & 1u) | (((o >> 16) & 1u) << 1)) << (2 * j);
+    }
+    const uint32_t PL = S & p3 & ~tb1 & (tb1 >> 1);           // plain: exactly 3 bytes "a|b"
+    const uint32_t X0 = PL & bm, X1 = PL & am, XE = S & ~PL;  // class bits at the starts (bit 2: escape)
+    if (f.pcls == CLS_NONE) {
+        // first chunk: token 0 continues a virtual run of its own class begun at token 0 (see clean8)
+        f.pcls = vw::readlane(((X1 & 1u) << 1) | (X0 & 1u), 0);
+        f.prs = 1;
+    }
+    // class entering the lane: that of the last start in an earlier lane, else the chunk carry
+    const uint32_t hs = S ? 31u - (uint32_t)__builtin_clz(S) : 0u;
+    const uint32_t lastc = (((XE >> hs) & 1u) << 2) | (((X1 >> hs) & 1u) << 1) | ((X0 >> hs) & 1u);
+    const uint32_t pek = vw::shr1z(vw::scan_max(S ? ((l + 1u) << 3) | lastc : 0u));
+    const uint32_t cin = pek ? (pek & 7u) : f.pcls;
+    // fill each start's class forward over its continuation halves
+    uint32_t c0 = X0, c1 = X1, ce = XE, has = S;
+#pragma unroll
+    for (int k = 1; k < 16; k <<= 1) {
+        c0 |= (c0 << k) & ~has;
+        c1 |= (c1 << k) & ~has;
+        ce |= (ce << k) & ~has;
+        has |= has << k;
+    }
+    const uint32_t pre = ~has & 0xFFFFu;   // halves before the lane's first start: the entering token's
+    c0 = (c0 | ((cin & 1u) ? pre : 0u)) & 0xFFFFu;
+    c1 = (c1 | ((cin & 2u) ? pre : 0u)) & 0xFFFFu;
+    ce = (ce | ((cin & 4u) ? pre : 0u)) & 0xFFFFu;
+    // predecessor class of each half (half 0: the entering class)
+    const uint32_t q0 = (c0 << 1) | (cin & 1u), q1 = (c1 << 1) | ((cin >> 1) & 1u), qe = (ce << 1) | ((cin >> 2) & 1u);
+    const uint32_t RS = S & ((c0 ^ q0) | (c1 ^ q1) | (ce ^ qe) | ce);   // run starts (escapes always)
+    const uint32_t EH = ce & vm;                                         // halves of escape tokens
+    // token indices, the run entering the lane and its offset mod cap
+    const uint32_t t0 = f.ntok + tinc - nt;
+    const uint32_t hr = RS ? 31u - (uint32_t)__builtin_clz(RS) : 0u;
+    const uint32_t lane_rs = RS ? t0 + (uint32_t)__builtin_popcount(S & ((1u << hr) - 1u)) + 1u : 0u;
+    const uint32_t incl = vw::scan_max(lane_rs);
+    const uint32_t rin = vw::umax(vw::shr1z(incl), f.prs);
+    const bool is00 = cin == 0;
+    const uint32_t cap = is00 ? 127u : 31u;
+    const uint32_t mp = mod_cap((t0 + MOD_BIAS) - rin, is00);   // offset of token t0 - 1 in its run, mod cap
+    const uint32_t lr = RS ? (uint32_t)__builtin_ctz(RS) : 16u;  // the first run start
+    const uint32_t j1 = RS ? (uint32_t)__builtin_popcount(S & ((1u << lr) - 1u)) : nt;
+    const uint32_t jf = cap - 2u - mp;                           // token completing a chunk of cap
+    const bool full = cin < CLS_ESC && jf < j1;
+    uint32_t rr = mp + j1;
+    rr = umin32(rr, rr - cap);
+    const bool lead1 = j1 < nt && cin < CLS_ESC && rr != cap - 1u;
+    const uint32_t b1v = cls_mask_f(cin) | (rr + 1u);
+    // the lane's byte count from the masks: lead bytes (the first run start's
+    // if lead1, every later run start's unless its predecessor is an escape),
+    // 0xE1 per escape start, two bytes per escape half (one for the row's last)
+    const uint32_t lrbit = RS & (0u - RS);
+    const uint32_t LEAD = ((RS & ~lrbit) & ~qe) | (lead1 ? lrbit : 0u);
+    const bool lastin = lastrel >= 0 && lastrel < 16 && ((EH >> lastrel) & 1u);
+    const uint32_t cnt = (full ? 1u : 0u) + (uint32_t)__builtin_popcount(LEAD) + (uint32_t)__builtin_popcount(XE) +
+                         2u * (uint32_t)__builtin_popcount(EH) - (lastin ? 1u : 0u);
+    const uint32_t incl2 = vw::scan_add(cnt);
+    const uint32_t base = (r.wpos + incl2 - cnt) & RMASK;
+    uint8_t *const lb0 = r.lds + base;
+    uint8_t *const dm = r.lds + RING_DUMMY;   // shared dummy word (see esc8)
+    // Per half, in token order: [lead][0xE1][payload], one byte store each
+    // (stores that emit nothing go to the shared dummy word)
+    uint32_t o = 0;
+    if (full) *lb0 = (uint8_t)(cls_mask_f(cin) | cap);
+    o += full ? 1u : 0u;
+    uint32_t tk = 0, ptk = 0;   // token index (in the lane) of half h; of the run start before it
+#pragma unroll
+    for (int h = 0; h < 16; h++) {
+        const uint32_t hl = (LEAD >> h) & 1u, es = (XE >> h) & 1u, eh = (EH >> h) & 1u;
+        const uint32_t pc = (((q1 >> h) & 1u) << 1) | ((q0 >> h) & 1u);    // predecessor class (plain when hl)
+        const uint32_t lb = (uint32_t)h == lr ? b1v : (cls_mask_f(pc) | (tk - ptk));
+        ptk = (RS >> h) & 1u ? tk : ptk;
+        tk += (S >> h) & 1u;
+        const uint32_t np = eh ? ((int32_t)h == lastrel ? 1u : 2u) : 0u;
+        const uint32_t pay = d[h >> 1] >> (16 * (h & 1));
+        *(hl ? lb0 + o : dm) = (uint8_t)lb;
+        o += hl;
+        *(es ? lb0 + o : dm) = (uint8_t)0xE1u;
+        o += es;
+        *(np ? lb0 + o : dm) = (uint8_t)pay;
+        *(np == 2u ? lb0 + o + 1 : dm) = (uint8_t)(pay >> 8);
+        o += np;
+    }
+    ring_unwrap(r, base + cnt);
+    r.wpos += vw::readlane(incl2, 63);
+    f.ntok += vw::readlane(tinc, 63);
+    // carries: the class of the chunk's last valid half, whether it ended a token, the last run start
+    const uint32_t hl = lastrel >= 15 ? 15u : lastrel < 0 ? 0u : (uint32_t)lastrel;
+    const uint32_t lcls = (((ce >> hl) & 1u) << 2) | (((c1 >> hl) & 1u) << 1) | ((c0 >> hl) & 1u);
+    const uint64_t endl = vw::ballot(lastrel >= 0 && lastrel < 16);
+    const uint32_t src = endl ? (uint32_t)__builtin_ctzll(endl) : 63u;
+    f.pcls = vw::readlane(lcls, src);
+    f.carryT = vw::readlane((tb1 >> 15) & 1u, 63);
+    f.prs = vw::umax(vw::readlane(incl, 63), f.prs);
+    ring_flush_var(r);
+    return true;
+}
+
+__device__ bool encode_var(const uint8_t *__restrict__ line, uint32_t len, Ring &r, uint32_t *rec_bytes) {
+    const uint32_t l = vw::lane_id();
+    const uint32_t lead = (uint32_t)(reinterpret_cast<uintptr_t>(line) & 15);
+    const uint8_t *A = line - lead;
+    const uint32_t span = lead + len;
+    if (len == 0) return false;
+    const uint32_t nch = (span + CHUNK - 1) / CHUNK;
+    const uint32_t lo16 = BPL * l;
+    VarState f;
+    f.nf = 0; f.carryT = 1; f.gt0 = -1; f.T = 0; f.phi = 0; f.pcls = CLS_NONE; f.prs = 0; f.esc = 0; f.ntok = 0;
+    r.wpos = 8;
+    r.fpos = 0;
+    // prefix phase: as encode_fast
+    const vw::brsrc rsA = vw::make_rsrc(A, (span + 3u) & ~3u);
+    uint32_t c = 0;
+    Chunk b = load_chunk(rsA, 0, lo16);
+    int st;
+    for (;;) {
+        st = (int)vw::readfirst((uint32_t)fast_prefix_step<true>(look_ahead(b), c, lead, len, f, r));
+        if (st != 0) break;
+        c = vw::readfirst(c + 1);
+        if (c >= nch) return false;
+        b = load_chunk(rsA, c, lo16);
+    }
+    if (st == 2) return false;
+    f.carryT = 1;   // token 0 starts the genotype region
+    ring_flush_var(r);   // < 512 bytes pending before the first chunk
+    const uint32_t phi = f.phi, NH = f.T;
+    const vw::brsrc rsG = vw::make_rsrc(line + f.gt0 - phi, (phi + len - (uint32_t)f.gt0 + 3u) & ~3u);
+    const uint32_t ncG = (NH + HPC - 1) / HPC;
+    const uint32_t lo32 = BPL8 * l;
+    // three chunks in flight, a single loop exit (see encode_fast)
+    Chunk8v b0 = load_chunk8v(rsG, 0, lo32);
+    Chunk8v b1 = load_chunk8v(rsG, 1, lo32);
+    Chunk8v b2 = load_chunk8v(rsG, 2, lo32);
+    vw::pin_loads();
+    uint32_t C = 0;
+    bool ok = true;
+    for (;;) {
+        ok = vw::readfirst(gt_var8(b0, C, f, r));
+        b0 = load_chunk8v(rsG, C + 3, lo32);
+        vw::pin_loads();
+        if (ok && C + 1 < ncG) ok = vw::readfirst(gt_var8(b1, C + 1, f, r));
+        b1 = load_chunk8v(rsG, C + 4, lo32);
+        vw::pin_loads();
+        if (ok && C + 2 < ncG) ok = vw::readfirst(gt_var8(b2, C + 2, f, r));
+        b2 = load_chunk8v(rsG, C + 5, lo32);
+        vw::pin_loads();
+        C = vw::readfirst(C + 3);
+        if (!ok || C >= ncG) break;
+    }
+    if (!ok) return false;
+    // row end: pending chunk of the last run, then '\n'
+    const uint32_t T = f.ntok, pcls = f.pcls, prs = f.prs;
+    uint32_t extra = 0, pb = 0;
+    if (pcls < CLS_ESC) {
+        const uint32_t off = mod_cap(T - prs, pcls == 0);
+        if (off != (pcls == 0 ? 126u : 30u)) { extra = 1; pb = cls_mask_f(pcls) | (off + 1); }
+    }
+    if (l == 0) {
+        if (extra) ring_put(r, r.wpos, pb);
+        ring_put(r, r.wpos + extra, 0x0Au);
+    }
+    r.wpos += extra + 1;
+    ring_flush_var(r);   // (< 512 pending: the final partial burst stays inside one staging region)
+    ring_finish(r, (uint32_t)f.gt0);
     *rec_bytes = r.wpos;
     return true;
 }
@@ -963,12 +1303,7 @@ __device__ uint32_t encode_general(const uint8_t *__restrict__ line, uint32_t le
                     *(in ? lb + o : dm) = (uint8_t)byte_of(cur.a, (uint32_t)i);
                     o += in ? 1u : 0u;
                 }
-                const bool wrap = base + o > RING;
-                if (vw::ballot(wrap)) {
-                    if (wrap) {
-                        for (uint32_t q = RING; q < base + o; q++) r.lds[q - RING] = r.lds[q];
-                    }
-                }
+                ring_unwrap(r, base + o);
                 r.wpos += vw::readlane(inc2, 63);
                 const uint32_t nst = vw::readlane(finc, 63);
                 nf += nst;
@@ -1100,12 +1435,7 @@ __device__ uint32_t encode_general(const uint8_t *__restrict__ line, uint32_t le
                 rm &= rm - 1u;
             }
         }
-        const bool wrap = base + o > RING;
-        if (vw::ballot(wrap)) {
-            if (wrap) {
-                for (uint32_t q = RING; q < base + o; q++) r.lds[q - RING] = r.lds[q];
-            }
-        }
+        ring_unwrap(r, base + o);
         r.wpos += vw::readlane(inc2, 63);
         // carries
         nf += vw::readlane(finc, 63);
@@ -1204,6 +1534,27 @@ __global__ __launch_bounds__(256) void k_encode_general(VcfcEncodeArgs a, uint64
             a.rec_size[row] = st == VCFCD_OK ? bytes : 0u;
             if (st != VCFCD_OK) atomicMin((unsigned long long *)a.err, (unsigned long long)((row << 8) | st));
         }
+    }
+}
+
+// Variable-token kernel: the rows the fast kernel flagged, GEN_ROWS per wave
+// (a flag load per 32 rows, so a batch without such rows costs next to
+// nothing); rows of another shape stay flagged for k_encode_general.
+__global__ __launch_bounds__(256) void k_encode_var(VcfcEncodeArgs a, uint64_t row_lo, uint64_t row_hi) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[K1_WAVES * RING_STRIDE];
+    const uint32_t wave = vw::readfirst(threadIdx.x >> 6);
+    const uint32_t l = vw::lane_id();
+    const uint64_t row0 = row_lo + ((uint64_t)blockIdx.x * K1_WAVES + wave) * GEN_ROWS;
+    const bool flagged = l < GEN_ROWS && row0 + l < row_hi && a.rec_size[row0 + l] == VCFCD_RETRY;
+    uint64_t todo = vw::ballot(flagged);
+    while (todo) {
+        const uint64_t row = row0 + (uint64_t)__builtin_ctzll(todo);
+        todo &= todo - 1;
+        Ring r;
+        if (!row_setup(a, row, lds + wave * RING_STRIDE, r)) continue;
+        uint32_t bytes = 0;
+        const bool ok = encode_var(a.buf + a.line_off[row], a.line_len[row], r, &bytes);
+        if (l == 0 && ok) a.rec_size[row] = bytes;
     }
 }
 
@@ -1547,6 +1898,9 @@ hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t s, hipEvent_t
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[1], s);
     hipLaunchKernelGGL(k_encode_fast, dim3((unsigned)((a.n + K1_WAVES - 1) / K1_WAVES)), dim3(64 * K1_WAVES), 0, s, a,
+                       (uint64_t)0, a.n);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_encode_var, dim3((unsigned)general_blocks(a.n)), dim3(64 * K1_WAVES), 0, s, a,
                        (uint64_t)0, a.n);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(k_encode_general, dim3((unsigned)general_blocks(a.n)), dim3(64 * K1_WAVES), 0, s, a,
