@@ -61,6 +61,8 @@ def parse():
                          "file -> file compress (row e: every rank its byte range, outputs held and placed at "
                          "the all-gathered offsets), --ingest-rows rows per rank")
     ap.add_argument("--dist-dir", default="/tmp/vcfc_distfile", help="--mode distfile: where the files go")
+    ap.add_argument("--dev-chunk", type=int, default=0,
+                    help="--mode devfile: chunk bytes of the device-resident compress (0: the whole file)")
     ap.add_argument("--rows-total", type=int, default=None,
                     help="--mode biobank: encode the rank's whole share of this many rows (5M = configs[3]) "
                          "as back-to-back --rows batches, every record digested and sampled rows re-encoded "
@@ -484,6 +486,8 @@ def bench_devfile(args, torch, vcfc, workload):
     d_out = torch.empty(cap, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize(dev)   # the call runs on the context's own stream
     ctx = vcfc.Context(0)
+    if args.dev_chunk:
+        ctx.set_ingest_chunk(args.dev_chunk)
     for _ in range(args.warmup):
         st, k, _ = ctx.compress_device(d_file.data_ptr(), N, d_out.data_ptr(), cap)
         assert st == 0 and k == want_len, (st, k, want_len)
@@ -501,7 +505,9 @@ def bench_devfile(args, torch, vcfc, workload):
            "data": "synthetic (generated in HBM; header + data lines as one device buffer)",
            "config": {"workload": "%s %d samples x %d variants, %.2f GB file in HBM (BASELINE configs[1])"
                                   % (law_name(args.law), S, n, N / 1e9),
-                      "file_bytes": N, "output_bytes": want_len, "chunk": "the whole file (one line index, one encode)"},
+                      "file_bytes": N, "output_bytes": want_len,
+                      "chunk": ("%d bytes of whole lines per line index + encode" % args.dev_chunk) if args.dev_chunk
+                               else "the whole file (one line index, one encode)"},
            "roofline": {"kernel": "line index + encoder (whole step)", "bound": "hbm",
                         "achieved": round((2 * N + want_len) / (ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round((2 * N + want_len) / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),

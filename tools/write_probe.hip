@@ -1,0 +1,64 @@
+// write_probe.hip -- write-bandwidth ceiling for the decoder's output shape
+// (not product code; a measurement tool).  Every pattern writes the same
+// 10.19 GB (1M lines of 10,189 B, the config-2 decode output):
+//   w0  grid-stride 16-B plain stores over the whole buffer
+//   w1  grid-stride 16-B non-temporal stores
+//   w2  one wave per line, 1 KiB per store instruction (16 B per lane),
+//       non-temporal -- the decoder's tile stores, lines back to back
+//   w3  as w2, plain stores
+// Build: hipcc --offload-arch=gfx950 -O3 -o build/write_probe tools/write_probe.hip
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e_), __LINE__); return 1; } } while (0)
+
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+constexpr uint64_t LINE = 10189, NLINE = 1000000, TOTAL = LINE * NLINE;
+
+template <bool NT>
+__global__ __launch_bounds__(256) void w_grid(v4u *buf, uint64_t n16) {
+    const v4u v = {0x09307C30u, 0x09307C30u, 0x09307C30u, 0x09307C30u};
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * 256) {
+        if (NT) __builtin_nontemporal_store(v, buf + i); else buf[i] = v;
+    }
+}
+
+template <bool NT>
+__global__ __launch_bounds__(256) void w_line(uint8_t *buf) {
+    const uint32_t l = threadIdx.x & 63;
+    const uint64_t row = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= NLINE) return;
+    const uint64_t o0 = row * LINE, a0 = (o0 + 15) & ~15ull, e = o0 + LINE;
+    const v4u v = {0x09307C30u, 0x09307C30u, 0x09307C30u, 0x09307C30u};
+    for (uint64_t o = a0 + 16 * l; o + 16 <= e; o += 1024) {
+        v4u *p = reinterpret_cast<v4u *>(buf + o);
+        if (NT) __builtin_nontemporal_store(v, p); else *p = v;
+    }
+}
+
+int main() {
+    uint8_t *buf;
+    CK(hipMalloc(&buf, TOTAL + 64));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const char *names[4] = {"w0 grid plain", "w1 grid nt", "w2 line nt", "w3 line plain"};
+    for (int p = 0; p < 4; p++) {
+        float best = 1e9;
+        for (int it = 0; it < 12; it++) {
+            CK(hipEventRecord(e0));
+            if (p == 0) hipLaunchKernelGGL(w_grid<false>, dim3(8192), dim3(256), 0, 0, (v4u *)buf, TOTAL / 16);
+            if (p == 1) hipLaunchKernelGGL(w_grid<true>, dim3(8192), dim3(256), 0, 0, (v4u *)buf, TOTAL / 16);
+            if (p == 2) hipLaunchKernelGGL(w_line<true>, dim3(NLINE / 4), dim3(256), 0, 0, buf);
+            if (p == 3) hipLaunchKernelGGL(w_line<false>, dim3(NLINE / 4), dim3(256), 0, 0, buf);
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            if (it >= 2 && ms < best) best = ms;
+        }
+        printf("{\"pattern\": \"%s\", \"ms\": %.4f, \"GB/s\": %.1f}\n", names[p], best, TOTAL / (best * 1e6));
+    }
+    return 0;
+}

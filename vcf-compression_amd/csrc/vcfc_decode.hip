@@ -484,8 +484,11 @@ __device__ __forceinline__ void write_one(const VcfcDecodeArgs &a, uint64_t i, u
         if (!LAST) {
 #pragma unroll
             for (uint32_t q = 0; q < PL; q += 4)
-                // (non-temporal: -0.3 % in an A/B, ab_dec_nt.txt)
-                vw::gstore16_nt(tok, 4ull * (t0 + q), make_uint4(w[q], w[q + 1], w[q + 2], w[q + 3]));
+                // plain stores: 2.645 -> 2.49 ms against non-temporal ones in
+                // an A/B (profiles/r03/ab/ab_dec_plain.txt; tools/write_probe.hip:
+                // one wave per 10 KB line writes 10.19 GB in 2.07 ms plain,
+                // 2.25 ms non-temporal)
+                vw::gstore16(tok, 4ull * (t0 + q), make_uint4(w[q], w[q + 1], w[q + 2], w[q + 3]));
         } else {
 #pragma unroll
             for (uint32_t q = 0; q < PL; q++)
@@ -493,7 +496,7 @@ __device__ __forceinline__ void write_one(const VcfcDecodeArgs &a, uint64_t i, u
             if (t0 + PL <= j0 + n_tok) {
 #pragma unroll
                 for (uint32_t q = 0; q < PL; q += 4)
-                    vw::gstore16_nt(tok, 4ull * (t0 + q), make_uint4(w[q], w[q + 1], w[q + 2], w[q + 3]));
+                    vw::gstore16(tok, 4ull * (t0 + q), make_uint4(w[q], w[q + 1], w[q + 2], w[q + 3]));
             } else {
                 for (uint32_t q = 0; q < PL; q++)
                     if (t0 + q < j0 + n_tok) *reinterpret_cast<uint32_t *>(tok + 4ull * (t0 + q)) = w[q];

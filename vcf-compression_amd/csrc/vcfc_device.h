@@ -16,6 +16,14 @@
 // rec_size value of a row the fast kernel leaves to the general kernel
 #define VCFCD_RETRY 0xFFFFFFFFu
 
+// Alignment: buf, the lines in it and out may start at any byte.  The
+// kernels address them with 16-byte loads and stores at the base's own
+// alignment (k_nl_scan reads a chunk from d_in + pos, k_compact_out stores
+// 16-B blocks at out + 16k, out = d_out + header bytes in compress_device);
+// gfx950 global and buffer memory instructions take unaligned addresses (ROCm
+// runs the GPU with SH_MEM_CONFIG's unaligned mode), an unaligned base only
+// costs the split accesses.  tests/test_gpu_ingest.py and test_kernel_emu.py
+// run unaligned bases and chunk starts (all 16 alignments of the buffer).
 struct VcfcEncodeArgs {
     // input: concatenated VCF data lines (device memory)
     const uint8_t *buf;

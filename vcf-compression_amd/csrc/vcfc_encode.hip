@@ -1674,7 +1674,9 @@ __global__ __launch_bounds__(256) void k_compact_out(const uint8_t *__restrict__
             if (o + 16 <= lim) {
                 // non-temporal: the records leave the chip (D2H, a file, the
                 // next stage), and the next batch's encode keeps L2 / MALL to
-                // itself (-0.8 % per step in an A/B, ab_compact_nt.txt)
+                // itself (-0.8 % per step in an A/B, ab_compact_nt.txt; round 3
+                // again: plain stores +1 % k_compact on law 1, +5 % on law 2,
+                // profiles/r03/ab/ab_compact_plain.txt)
                 vw::gstore16_nt(out, o, v);
             } else {
                 const uint32_t w[4] = {v.x, v.y, v.z, v.w};
