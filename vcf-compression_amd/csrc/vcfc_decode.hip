@@ -38,7 +38,7 @@ namespace {
 constexpr int DEC_WAVES = 4;   // records per 256-thread block
 constexpr uint32_t SB = 2048;              // sample bytes staged per piece (k_dec_write)
 constexpr uint32_t SBUF = SB + 48;         // + look-ahead, 16-B alignment slack, last block's overhang
-constexpr uint32_t TB = 256;   // token words per LDS tile (k_dec_write): 4 per lane (512: 1.9x, ab_dec_tile512.txt)
+constexpr uint32_t TB = 256;   // token words per LDS tile (k_dec_write): 4 per lane (512: +13 %, profiles/r03/ab/ab_dec_tile512.txt)
 
 // per-record status after planning
 constexpr uint32_t DS_SIMPLE = 0;   // line = REQ' + 4S bytes, item fill
