@@ -35,7 +35,8 @@ def lib():
                                    u64, ctypes.c_int, u64]
         L.emu_record_hash.argtypes = [vp, vp, u64, vp]
         L.emu_compress_device.argtypes = [ctypes.c_char_p, u64, vp, u64, ctypes.POINTER(u64),
-                                          ctypes.POINTER(ctypes.c_int64), u64, u64]
+                                          ctypes.POINTER(ctypes.c_int64), u64, u64, ctypes.c_int,
+                                          ctypes.POINTER(u64)]
         L.emu_synth.argtypes = [vp, vp, u64, vp, vp, vp, ctypes.c_uint32, ctypes.c_int, u64]
         _lib = L
     return _lib
@@ -149,15 +150,19 @@ def emu_compress(vcf, chunk=4096, read_threads=2, cap=None, max_chunk=0):
     return st, out[:n.value].tobytes(), el.value
 
 
-def emu_compress_device(vcf, chunk=4096, cap=None, max_chunk=0):
+def emu_compress_device(vcf, chunk=4096, cap=None, max_chunk=0, hop=True, redo=None):
     """compress() of device-resident bytes (vcfc_ing::compress_device) on the
-    emulator: (status, bytes, err_line)."""
+    emulator: (status, bytes, err_line).  hop: the hop line index when the
+    header gives S; redo (a list): gets the count of chunks indexed again."""
     cap = cap or 2 * len(vcf) + 4096
     out = np.zeros(cap, dtype=np.uint8)
     n = ctypes.c_uint64(0)
     el = ctypes.c_int64(-1)
+    r = ctypes.c_uint64(0)
     st = lib().emu_compress_device(vcf, len(vcf), out.ctypes.data, cap, ctypes.byref(n), ctypes.byref(el), chunk,
-                                   max_chunk)
+                                   max_chunk, 1 if hop else 0, ctypes.byref(r))
+    if redo is not None:
+        redo.append(r.value)
     return st, out[:n.value].tobytes(), el.value
 
 

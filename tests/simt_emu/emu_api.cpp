@@ -164,11 +164,14 @@ extern "C" int emu_compress(const uint8_t *in, uint64_t n, uint8_t *out, uint64_
 // compress() of "device-resident" bytes (host memory on the emulator)
 // through vcfc_ing::compress_device, with small chunks.
 extern "C" int emu_compress_device(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len,
-                                   int64_t *err_line, uint64_t chunk, uint64_t max_chunk) {
+                                   int64_t *err_line, uint64_t chunk, uint64_t max_chunk, int hop,
+                                   uint64_t *hop_redo) {
     HostIngestMemory M;
     vcfc_ing::Config cfg;
     cfg.chunk = chunk;
     if (max_chunk) cfg.max_chunk = max_chunk;
+    cfg.hop_index = hop != 0;
+    cfg.hop_redo = hop_redo;
     return vcfc_ing::compress_device(in, n, out, cap, out_len, M, nullptr, cfg, err_line);
 }
 

@@ -10,6 +10,9 @@
 #define VCFCD_E_LT8COLS 1
 #define VCFCD_E_8COLS 2
 #define VCFCD_E_NOSPACE 4
+// a row holding a '\n' byte, seen only when VcfcEncodeArgs::nl_check is set:
+// the hop line index (vcfc_line_index with S_hint) mispredicted a line end
+#define VCFCD_E_NEWLINE 9
 
 // error word: min over failing rows of (row << 8 | code); ~0 = no error
 #define VCFCD_NO_ERROR (~0ull)
@@ -47,6 +50,10 @@ struct VcfcEncodeArgs {
     uint8_t *slots;            // per-row overflow slots: record bytes [VCFC_PRIM, ...) at slots + slot_off[row]
     uint64_t slots_cap;
     uint64_t *dbg;             // diagnostic builds only (tools/diag hooks); else null
+    // rows from the hop line index: a row holding a '\n' fails with
+    // VCFCD_E_NEWLINE (k_encode_var scans the rows k_encode_fast hands back;
+    // k_encode_fast accepts none)
+    uint32_t nl_check = 0;
 };
 
 // Record staging: the first VCFC_PRIM bytes of every record go to a dense
@@ -176,9 +183,12 @@ struct VcfcLineIndexLayout {
     uint64_t nl, is_data, is_pass, data_rank, pass_rank, partials2, total2;   // phase 2 workspace
 };
 VcfcLineIndexLayout vcfc_line_index_layout(uint64_t chunk_bytes, uint64_t n_lines);
-// phase 1: '\n' count of buf[0, n) (last byte '\n'); counts[0] = lines
+// phase 1: '\n' count of buf[0, n) (last byte '\n'); counts[0] = lines.
+// S_hint (the header's sample count, 0: none) selects the hop index
+// (k_nl_hop: data line ends predicted from S and checked) over the full
+// '\n' scan; its result must be confirmed by the encoder (VcfcEncodeArgs::nl_check).
 hipError_t vcfc_line_index(const uint8_t *buf, uint64_t n, uint8_t *ws, const VcfcLineIndexLayout &L,
-                           const VcfcLineIndex &x, hipStream_t s);
+                           const VcfcLineIndex &x, hipStream_t s, uint32_t S_hint = 0);
 // phase 2 (n_lines = counts[0]): '\n' positions, data / pass line arrays; counts[1], counts[2]
 hipError_t vcfc_line_index_place(const uint8_t *buf, uint64_t n, uint64_t n_lines, const uint8_t *ws1, uint8_t *ws2,
                                  const VcfcLineIndexLayout &L, const VcfcLineIndex &x, hipStream_t s);

@@ -294,7 +294,22 @@ __device__ __forceinline__ int fast_prefix_step(const Chunk &cur, uint32_t c, ui
         const int32_t d = (int32_t)x9 - x0;
         below = d <= 0 ? 0u : d >= (int32_t)BPL ? ~0u : ((1u << d) - 1u);
     }
-    if (vw::ballot((et & below) != 0)) return 2;
+    // a '\n' in the row (the hop line index's guess went wrong, see
+    // VcfcEncodeArgs::nl_check): not the fast shape
+    uint32_t lf = 0;
+#pragma unroll
+    for (int k = 0; k < (int)TPL; k++) lf |= zero_bytes4(cur.w(k) ^ 0x0A0A0A0Au) << (4 * k);
+    // the fast shape: in this chunk's genotype bytes the TABs sit exactly at
+    // x9 + 4k + 3 -- rows of other token lengths (haploid "0", GT:DP:GQ, '.')
+    // leave here, before the genotype phase puts 6 KiB of loads in flight
+    bool odd = false;
+    if (!VAR && hb) {
+        const int32_t rel = x0 - (int32_t)x9;
+        const uint32_t ph = (uint32_t)(3 - rel) & 3u;   // lane bytes i with (rel + i) % 4 == 3
+        const uint32_t ge = rel >= 0 ? FULLM : (-rel >= (int32_t)BPL ? 0u : (FULLM & ~((1u << -rel) - 1u)));
+        odd = ((m ^ ((0x1111u << ph) & FULLM)) & ge & vm) != 0;
+    }
+    if (vw::ballot((et & below) != 0 || (lf & vm) != 0 || odd)) return 2;
     // prefix bytes -> ring[8 + x]: realign the lane's bytes to ring dwords
     // (ring position of lane byte i is bo + i + 8 - lead); bytes outside
     // [0, x9) land below 8 (header, rewritten) or at >= wpos (free,
@@ -365,7 +380,8 @@ __device__ bool gt_general(const Chunk &cur, int32_t tf, FastState &f, Ring &r) 
         cl[j] = !v[j] ? CLS_NONE : isc ? cls_classed(d[j]) : CLS_ESC;
         if (cl[j] == CLS_ESC) {
             // an escape, or the row's last token (no TAB after it): full check
-            const uint32_t x = d[j] ^ 0x09090909u;
+            // (bytes 0..2 masked to 0xFC: 0x08-0x0B, TAB and '\n' among them, reject)
+            const uint32_t x = (d[j] ^ 0x09090909u) & 0xFFFCFCFCu;
             const uint32_t zb = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
             const bool last = (uint32_t)(t0 + j) + 1 == T;
             bad |= (zb & 0x00808080u) != 0 || ((zb >> 31) == 0 && !last);
@@ -703,8 +719,9 @@ __device__ __forceinline__ void esc8(const uint32_t (&d)[TPL8], int32_t t0, int3
     ring_flush(r, false);
 }
 
-// every slot of the lane is "xyz\t" with x, y, z not TAB (the last token: no
-// TAB needed; slots past it ignored)
+// every slot of the lane is "xyz\t" with x, y, z none of 0x08-0x0B (not TAB,
+// not '\n': a row holding one is the hop index's wrong guess; the other two go
+// the general way) -- the last token: no TAB needed; slots past it ignored
 template <bool EDGE>
 __device__ __forceinline__ bool shape3(const uint32_t (&d)[TPL8], int32_t t0, uint32_t T) {
     if (!EDGE) {
@@ -715,7 +732,7 @@ __device__ __forceinline__ bool shape3(const uint32_t (&d)[TPL8], int32_t t0, ui
 #pragma unroll
         for (int j = 0; j < (int)TPL8; j++) {
             const uint32_t t = d[j] ^ 0x09090909u;
-            const uint32_t u = t | 0xFF000000u;
+            const uint32_t u = (t & 0x00FCFCFCu) | 0xFF000000u;
             at |= t;
             az |= (u - 0x01010101u) & ~u;
         }
@@ -724,8 +741,8 @@ __device__ __forceinline__ bool shape3(const uint32_t (&d)[TPL8], int32_t t0, ui
     bool bad = false;
 #pragma unroll
     for (int j = 0; j < (int)TPL8; j++) {
-        const uint32_t x = d[j] ^ 0x09090909u;
-        const uint32_t zb = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);   // 0x80 per TAB byte
+        const uint32_t x = (d[j] ^ 0x09090909u) & 0xFFFCFCFCu;
+        const uint32_t zb = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);   // 0x80 per TAB byte (0x08-0x0B in bytes 0..2)
         if (EDGE) {
             const int32_t t = t0 + j;
             const uint32_t want = (uint32_t)t + 1u == T ? 0u : 0x80000000u;
@@ -1537,6 +1554,29 @@ __global__ __launch_bounds__(256) void k_encode_general(VcfcEncodeArgs a, uint64
     }
 }
 
+// a '\n' among the row's bytes (VcfcEncodeArgs::nl_check): 4 KiB per round
+__device__ bool row_has_nl(const uint8_t *__restrict__ line, uint32_t len) {
+    const uint32_t l = vw::lane_id();
+    const uint32_t lead = (uint32_t)(reinterpret_cast<uintptr_t>(line) & 15);
+    const uint32_t span = lead + len;
+    const vw::brsrc rs = vw::make_rsrc(line - lead, (span + 3u) & ~3u);
+    for (uint32_t c = 0; c < span; c = vw::readfirst(c + 4096u)) {
+        uint4 v[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) v[k] = vw::bload16(rs, c + 1024u * k + 16u * l, 0);
+        bool hit = false;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {
+            const int32_t o = (int32_t)(c + 1024u * k + 16u * l);
+            const uint32_t m = zero_bytes4(v[k].x ^ 0x0A0A0A0Au) | (zero_bytes4(v[k].y ^ 0x0A0A0A0Au) << 4) |
+                               (zero_bytes4(v[k].z ^ 0x0A0A0A0Au) << 8) | (zero_bytes4(v[k].w ^ 0x0A0A0A0Au) << 12);
+            hit |= (m & mask_range16((int32_t)lead - o, (int32_t)span - o)) != 0;
+        }
+        if (vw::ballot(hit)) return true;
+    }
+    return false;
+}
+
 // Variable-token kernel: the rows the fast kernel flagged, GEN_ROWS per wave
 // (a flag load per 32 rows, so a batch without such rows costs next to
 // nothing); rows of another shape stay flagged for k_encode_general.
@@ -1552,6 +1592,13 @@ __global__ __launch_bounds__(256) void k_encode_var(VcfcEncodeArgs a, uint64_t r
         todo &= todo - 1;
         Ring r;
         if (!row_setup(a, row, lds + wave * RING_STRIDE, r)) continue;
+        if (a.nl_check && row_has_nl(a.buf + a.line_off[row], a.line_len[row])) {
+            if (l == 0) {   // not encoded: the caller indexes the lines again
+                a.rec_size[row] = 0;
+                atomicMin((unsigned long long *)a.err, (unsigned long long)((row << 8) | VCFCD_E_NEWLINE));
+            }
+            continue;
+        }
         uint32_t bytes = 0;
         const bool ok = encode_var(a.buf + a.line_off[row], a.line_len[row], r, &bytes);
         if (l == 0 && ok) a.rec_size[row] = bytes;

@@ -147,6 +147,8 @@ struct Config {
     uint64_t max_chunk = 3ull << 30; // growth limit (line offsets in a chunk are 32-bit; a record's
                                      // LEN header holds < 2^30 anyway, reference src/utils.hpp:160)
     int read_threads = 8;
+    bool hop_index = true;           // compress_device: the hop line index (S from "#CHROM")
+    uint64_t *hop_redo = nullptr;    // compress_device: chunks indexed again after a wrong hop guess
 };
 
 // compress()'s header-line check (src/compress.cpp:230-235): split_string
@@ -160,6 +162,25 @@ inline bool header_ok(const uint8_t *p, uint64_t len) {
         while (q < len && p[q] != '\t') q++;
     }
     return terms >= 8;
+}
+
+// Samples of the "#CHROM" line held whole in p[0, len) (TABs - 8), 0 if none:
+// only a guess for the hop line index, never trusted for the output.
+inline uint32_t header_samples(const uint8_t *p, uint64_t len) {
+    static const char key[] = "#CHROM\t";
+    for (uint64_t q = 0; q + 7 <= len;) {
+        const uint8_t *e = static_cast<const uint8_t *>(memchr(p + q, '\n', len - q));
+        if (!e) return 0;
+        const uint64_t end = (uint64_t)(e - p);
+        if (end - q >= 7 && memcmp(p + q, key, 7) == 0) {
+            uint64_t tabs = 0;
+            for (uint64_t k = q; k < end; k++) tabs += p[k] == '\t';
+            return tabs >= 9 && tabs - 8 < (1u << 24) ? (uint32_t)(tabs - 8) : 0u;
+        }
+        if (p[q] != '#') return 0;   // the header ended
+        q = end + 1;
+    }
+    return 0;
 }
 
 namespace detail {
@@ -595,6 +616,20 @@ inline int compress_device(const uint8_t *d_in, uint64_t N, uint8_t *d_out, uint
             return ST_E_ARG;
         }
     }
+    // The sample count S from the "#CHROM" line (in the first MiB) lets the
+    // line index hop over a data line's genotypes (vcfc_line_index S_hint);
+    // a chunk whose hop index the encoder finds wrong (VCFCD_E_NEWLINE) is
+    // indexed again from every byte.  VCFC_HOP=0: always every byte.
+    uint32_t S_hint = 0;
+    {
+        const char *hv = getenv("VCFC_HOP");
+        if (cfg.hop_index && !(hv && hv[0] == '0')) {
+            std::vector<uint8_t> h(std::min<uint64_t>(N, 1u << 20));
+            if (!d2h(h.data(), d_in, h.size()) || !sync()) return ST_E_HIP;
+            S_hint = header_samples(h.data(), h.size());
+        }
+        if (trace) fprintf(stderr, "compress_device: S_hint=%u\n", S_hint);
+    }
     uint64_t pos = 0, o = 0, line_base = 0;
     constexpr uint64_t WIN = 1ull << 16;
     std::vector<uint8_t> win;
@@ -621,13 +656,15 @@ inline int compress_device(const uint8_t *d_in, uint64_t N, uint8_t *d_out, uint
         }
         const uint8_t *d_c = d_in + pos;
         if (trace) fprintf(stderr, "compress_device: chunk [%llu, +%llu)\n", (unsigned long long)pos, (unsigned long long)n);
-        // ---- line index (as compress_stream) ----
+        uint32_t hop = S_hint;
+      index_again:
+        // ---- line index (as compress_stream; hop: see S_hint) ----
         const VcfcLineIndexLayout L1 = vcfc_line_index_layout(n, 0);
         uint8_t *d_ix1 = static_cast<uint8_t *>(M.dev(Memory::D_IX1, L1.total1));
         if (!d_ix1) return ST_E_HIP;
         VcfcLineIndex x;
         x.counts = d_small;
-        if (vcfc_line_index(d_c, n, d_ix1, L1, x, s) != hipSuccess || !d2h(hsmall, d_small, 8) || !sync())
+        if (vcfc_line_index(d_c, n, d_ix1, L1, x, s, hop) != hipSuccess || !d2h(hsmall, d_small, 8) || !sync())
             return ST_E_HIP;
         const uint64_t n_lines = hsmall[0];
         // line numbers inside a chunk are 32-bit (k_line_place): a chunk of
@@ -651,7 +688,14 @@ inline int compress_device(const uint8_t *d_in, uint64_t N, uint8_t *d_out, uint
         if (vcfc_line_index_place(d_c, n, n_lines, d_ix1, d_ix2, L, x, s) != hipSuccess || !d2h(hsmall, d_small, 32) ||
             !sync())
             return ST_E_HIP;
-        if (hsmall[3]) return ST_E_ARG;   // a line of 4 GiB or more
+        if (hsmall[3]) {   // a line of 4 GiB or more (or a hop across lines)
+            if (hop) {
+                if (cfg.hop_redo) ++*cfg.hop_redo;
+                hop = 0;
+                goto index_again;
+            }
+            return ST_E_ARG;
+        }
         const uint64_t n_data = hsmall[1], n_pass = hsmall[2];
         // ---- '#' lines: to the host, checked in order ----
         // Each '#' line lies in d_c followed by its '\n' -- exactly the bytes
@@ -737,9 +781,17 @@ inline int compress_device(const uint8_t *d_in, uint64_t N, uint8_t *d_out, uint
             a.out = d_recs; a.out_cap = cap; a.rec_off = d_rec_off;
             vcfc_encode_args_workspace(a, ws, W);
             a.err = d_small + 4;
+            a.nl_check = hop != 0;
             if (vcfc_encode_device(a, s) != hipSuccess || !d2h(hsmall + 4, d_small + 4, 8) || !sync())
                 return ST_E_HIP;
             const uint64_t errw = hsmall[4];
+            if (errw != VCFCD_NO_ERROR && (errw & 0xFF) == VCFCD_E_NEWLINE) {
+                if (trace) fprintf(stderr, "compress_device: hop index missed a line end (row %llu)\n",
+                                   (unsigned long long)(errw >> 8));
+                if (cfg.hop_redo) ++*cfg.hop_redo;
+                hop = 0;
+                goto index_again;
+            }
             if (errw != VCFCD_NO_ERROR) {
                 good = errw >> 8;
                 st = (int)(errw & 0xFF);
