@@ -37,6 +37,7 @@ def lib():
         L.emu_compress_device.argtypes = [ctypes.c_char_p, u64, vp, u64, ctypes.POINTER(u64),
                                           ctypes.POINTER(ctypes.c_int64), u64, u64, ctypes.c_int,
                                           ctypes.POINTER(u64)]
+        L.emu_line_index.argtypes = [ctypes.c_char_p, u64, ctypes.c_uint32, vp, vp, u64, vp]
         L.emu_synth.argtypes = [vp, vp, u64, vp, vp, vp, ctypes.c_uint32, ctypes.c_int, u64]
         _lib = L
     return _lib
@@ -164,6 +165,19 @@ def emu_compress_device(vcf, chunk=4096, cap=None, max_chunk=0, hop=True, redo=N
     if redo is not None:
         redo.append(r.value)
     return st, out[:n.value].tobytes(), el.value
+
+
+def emu_line_index(vcf, S_hint=0):
+    """The GPU line index of vcf (ending in '\n') on the emulator: (counts
+    [lines, data lines, pass lines, long], data line offsets, lengths)."""
+    cap = vcf.count(b"\n") + 1
+    off = np.zeros(cap, dtype=np.uint64)
+    ln = np.zeros(cap, dtype=np.uint32)
+    cnt = np.zeros(4, dtype=np.uint64)
+    st = lib().emu_line_index(vcf, len(vcf), S_hint, off.ctypes.data, ln.ctypes.data, cap, cnt.ctypes.data)
+    assert st == 0
+    k = int(cnt[1])
+    return [int(c) for c in cnt], off[:k].tolist(), ln[:k].tolist()
 
 
 def emu_synth_rows(n, samples, law, seed, row0=0):

@@ -203,3 +203,29 @@ extern "C" int emu_held(const uint8_t *data, uint64_t n, uint64_t piece, uint64_
     *spill_bytes = h.spilled;
     return h.place(out_fd, out_off) ? 0 : 7;
 }
+
+// The line index (csrc/vcfc_ingest.hip) of in[0, n) (last byte '\n'): the
+// data lines' offsets and lengths and the counts; S_hint != 0: the hop index.
+extern "C" int emu_line_index(const uint8_t *in, uint64_t n, uint32_t S_hint, uint64_t *off, uint32_t *len,
+                              uint64_t cap, uint64_t *counts) {
+    const VcfcLineIndexLayout L1 = vcfc_line_index_layout(n, 0);
+    std::vector<uint8_t> ws1(L1.total1 + 64);
+    std::vector<uint64_t> cnt(4, 0);
+    VcfcLineIndex x;
+    memset(&x, 0, sizeof x);
+    x.counts = cnt.data();
+    if (vcfc_line_index(in, n, ws1.data(), L1, x, nullptr, S_hint) != hipSuccess) return 1;
+    const uint64_t lines = cnt[0];
+    const VcfcLineIndexLayout L = vcfc_line_index_layout(n, lines);
+    std::vector<uint8_t> ws2(L.total2 + 64);
+    std::vector<uint64_t> lo(lines + 1), po(lines + 1), pb(lines + 1);
+    std::vector<uint32_t> ll(lines + 1), ln(lines + 1), pl(lines + 1), pn(lines + 1);
+    x.line_off = lo.data(); x.line_len = ll.data(); x.line_no = ln.data();
+    x.pass_off = po.data(); x.pass_len = pl.data(); x.pass_no = pn.data(); x.pass_before = pb.data();
+    if (vcfc_line_index_place(in, n, lines, ws1.data(), ws2.data(), L, x, nullptr) != hipSuccess) return 1;
+    memcpy(counts, cnt.data(), 32);
+    const uint64_t k = std::min<uint64_t>(cnt[1], cap);
+    memcpy(off, lo.data(), 8 * k);
+    memcpy(len, ll.data(), 4 * k);
+    return 0;
+}

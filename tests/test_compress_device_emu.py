@@ -170,3 +170,43 @@ def test_hop_index_wrong_guess_is_caught(kind):
     st2, out2, _ = E.emu_compress_device(vcf, chunk=1 << 16, hop=False, redo=redo)
     assert st == st2 == OK and out == out2
     assert redo == [1, 0]   # the guess went wrong once, and was caught
+
+
+def chr22_like(rnd, n_rows, S, prefix_jitter=40):
+    """Rows of S 3-byte tokens behind prefixes whose lengths vary by up to
+    prefix_jitter bytes (the hop index guesses each end from the previous
+    row's prefix length), some '##' lines and an empty line among them."""
+    lines = T.D.header(S).rstrip(b"\n").split(b"\n")
+    for i in range(n_rows):
+        info = b"AC=%d;AF=0.%d;NS=%s" % (rnd.randrange(100), rnd.randrange(10 ** 6), b"9" * rnd.randrange(prefix_jitter))
+        toks = [rnd.choice([b"0|0", b"0|0", b"0|1", b"1|0", b"1|1", b"0|2"]) for _ in range(S)]
+        lines.append(b"\t".join([b"22", b"%d" % (16050000 + 37 * i), b"rs%d" % rnd.randrange(10 ** 8), b"A", b"G",
+                                 b"100", b"PASS", info, b"GT"] + toks))
+        if i % 17 == 5:
+            lines.append(b"##mid=%d" % i)
+        if i == 11:
+            lines.append(b"")
+    return b"\n".join(lines) + b"\n"
+
+
+@pytest.mark.parametrize("S,jitter", [(300, 40), (700, 300), (64, 5)])
+def test_hop_index_equals_scan_index(S, jitter):
+    """Where no guess goes wrong the hop index gives the scan index's tables
+    exactly: guess windows that hit, miss (prefix lengths jumping by up to
+    300 bytes: the VERIFY round) and lines shorter than the first KiB."""
+    rnd = random.Random(S)
+    vcf = chr22_like(rnd, 150, S, jitter)
+    assert E.emu_line_index(vcf, S) == E.emu_line_index(vcf, 0)
+    for chunk in (1 << 15, 1 << 20):
+        check(vcf, chunk, "chr22-like S=%d" % S)
+
+
+@pytest.mark.parametrize("kind", ["tab", "escape", "var", "lines"])
+def test_hop_index_trap_counts_fewer_lines(kind):
+    """On the trap files the hop index misses the '\\n' of row A (so the
+    encoder's check is what makes test_hop_index_wrong_guess_is_caught pass)."""
+    vcf = hop_trap_file(kind, random.Random(kind))
+    S = vcf.split(b"\n")[1].count(b"\t") - 8
+    hop, scan = E.emu_line_index(vcf, S), E.emu_line_index(vcf, 0)
+    # A..B counted as one data line ('#' and empty lines between them swallowed)
+    assert hop[0][0] < scan[0][0] and hop[0][1] == scan[0][1] - 1

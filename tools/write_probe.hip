@@ -6,6 +6,9 @@
 //   w2  one wave per line, 1 KiB per store instruction (16 B per lane),
 //       non-temporal -- the decoder's tile stores, lines back to back
 //   w3  as w2, plain stores
+//   w4  as w3, each line's stores at its own (unaligned) start -- the
+//       decoder's tile stores at line + REQ' (any byte alignment)
+//   w5  as w4 with 4-B stores (a lane's four dwords one by one)
 // Build: hipcc --offload-arch=gfx950 -O3 -o build/write_probe tools/write_probe.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -37,14 +40,32 @@ __global__ __launch_bounds__(256) void w_line(uint8_t *buf) {
     }
 }
 
+template <bool DW>
+__global__ __launch_bounds__(256) void w_line_u(uint8_t *buf) {
+    const uint32_t l = threadIdx.x & 63;
+    const uint64_t row = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= NLINE) return;
+    const uint64_t o0 = row * LINE + 37, e = o0 + LINE - 64;
+    for (uint64_t o = o0 + 16 * l; o + 16 <= e; o += 1024) {
+        if (DW) {
+            uint32_t *p = reinterpret_cast<uint32_t *>(buf + o);
+            p[0] = 0x09307C30u; p[1] = 0x09307C30u; p[2] = 0x09307C30u; p[3] = 0x09307C30u;
+        } else {
+            const v4u v = {0x09307C30u, 0x09307C30u, 0x09307C30u, 0x09307C30u};
+            __builtin_memcpy(buf + o, &v, 16);
+        }
+    }
+}
+
 int main() {
     uint8_t *buf;
     CK(hipMalloc(&buf, TOTAL + 64));
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    const char *names[4] = {"w0 grid plain", "w1 grid nt", "w2 line nt", "w3 line plain"};
-    for (int p = 0; p < 4; p++) {
+    const char *names[6] = {"w0 grid plain", "w1 grid nt", "w2 line nt", "w3 line plain", "w4 line plain unaligned",
+                            "w5 line plain unaligned dwords"};
+    for (int p = 0; p < 6; p++) {
         float best = 1e9;
         for (int it = 0; it < 12; it++) {
             CK(hipEventRecord(e0));
@@ -52,6 +73,8 @@ int main() {
             if (p == 1) hipLaunchKernelGGL(w_grid<true>, dim3(8192), dim3(256), 0, 0, (v4u *)buf, TOTAL / 16);
             if (p == 2) hipLaunchKernelGGL(w_line<true>, dim3(NLINE / 4), dim3(256), 0, 0, buf);
             if (p == 3) hipLaunchKernelGGL(w_line<false>, dim3(NLINE / 4), dim3(256), 0, 0, buf);
+            if (p == 4) hipLaunchKernelGGL(w_line_u<false>, dim3(NLINE / 4), dim3(256), 0, 0, buf);
+            if (p == 5) hipLaunchKernelGGL(w_line_u<true>, dim3(NLINE / 4), dim3(256), 0, 0, buf);
             CK(hipEventRecord(e1));
             CK(hipEventSynchronize(e1));
             float ms;

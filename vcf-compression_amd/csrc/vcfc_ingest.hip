@@ -16,13 +16,14 @@
 //                 the segment's slot (per-lane masks, a wave prefix sum of
 //                 their popcounts)
 //   scan          segment bases (the encoder's exclusive scan)
-//   k_nl_place    one wave per segment: its positions from the slot to their
+//   k_nl_place    one lane per segment: its positions from the slot to their
 //                 place; a segment with more than NL_SLOT lines (average
 //                 line < 64 bytes: header lines) scans its bytes again
 //   k_line_kind   one lane per line: data / pass flags
 //   scan x2       data and pass ranks
 //   k_line_place  one lane per line: scatter into the output arrays
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <vcfc_wave.h>   // angle brackets: tests/simt_emu shadows it
 #include "vcfc_device.h"
 
@@ -32,6 +33,7 @@ constexpr uint32_t SEG = 16384;          // bytes per wave
 constexpr uint32_t WIN = 1024;           // bytes per wave step (16 per lane)
 constexpr uint32_t IX_WAVES = 4;
 constexpr uint32_t NL_SLOT = 128;        // '\n' positions kept per segment by k_nl_scan
+__device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
 
 // bit j: byte j of x is '\n' (exact per byte)
 __device__ __forceinline__ uint32_t nl_bits(uint32_t x) {
@@ -108,151 +110,203 @@ __global__ __launch_bounds__(256) void k_nl_scan(const uint8_t *buf, uint64_t n,
 
 // ---------------------------------------------------------------------------
 // Hop index (compress_device when the header gives the sample count S): the
-// same per-segment output as k_nl_scan without reading every byte.  One wave
-// walks the lines that start in a group of HOPG segments.  A data line whose
-// first 1 KiB holds its 9th TAB and no '\n' is predicted to end at
-// gt0 + 4 S - 1 (every token 3 bytes + TAB, gt0 = its first sample byte):
-// one 256-byte window loaded beside the first (at the previous line's prefix
-// length) checks that this byte is '\n' and the 31 bytes 4, 8, ..., 124
-// before it are TABs.  Every other line (header and '#' lines, empty lines,
-// other token lengths, a failed check) is scanned for its '\n'.  A group
-// finds its first line start by scanning from the byte before it.  So a
-// chr22-shaped file is read for ~1.2 KiB per line instead of every byte.
-// A line predicted across a '\n' it did not see (one that is shorter than
-// predicted and whose end lands on another line's '\n', with TABs at the 31
-// checked places) is caught by the encoder (k_encode_fast<true> rejects '\n'
-// in its tokens, k_nl_verify scans the rows it rejects), and the chunk is
-// indexed again by k_nl_scan.
-constexpr uint32_t HOPG = 8;          // 16 KiB segments per walker (128 KiB)
-constexpr uint32_t GW = 256;          // guess window (4 bytes per lane)
+// same per-segment output as k_nl_scan without reading every byte.  A wave
+// holds HOPW walkers of 16 lanes; walker w walks the lines that end in its
+// span of `wseg` segments, one round trip per line:
+//   LINE    the line's first MW bytes (256..1024: the previous line's prefix
+//           length + 96, rounded up) and a 256-byte guess window around where
+//           the line would end if its prefix were as long as the previous
+//           line's.  A '\n' in the first window is the end.  Else the 9th TAB
+//           gives gt0 (the first sample byte) and the end is predicted at
+//           e = gt0 + 4 S - 1 (every token 3 bytes + TAB): taken when byte e
+//           is '\n' and the 31 bytes 4, 8, ..., 124 before it are TABs; if
+//           the guess window missed e, VERIFY loads the 256 bytes ending at e
+//           next round.  No 9th TAB in MW < 1024 bytes: the line again with
+//           1 KiB.  '#' lines, prefixes over 1 KiB, a failed check: FIND.
+//   FIND    the next 1 KiB scanned for its first '\n' (also the walker's
+//           start: the first '\n' at or after its span's first byte - 1).
+// Loads are 16 B per lane over contiguous 256-byte rows (coalesced).  A
+// chr22-shaped file is read for ~0.5 KiB per line instead of every byte.
+// A line predicted across a '\n' it did not see (a shorter line whose guessed
+// end lands on a later line's '\n' with TABs at the 31 checked places) is
+// caught by the encoder (VcfcEncodeArgs::nl_check), and the chunk is indexed
+// again by k_nl_scan.
+constexpr uint32_t HOPW = 4;                   // walkers per wave
+constexpr uint64_t HOP_WALKERS = 32768;   // (devfile step: 16384 +1.2 %, 8192 +4.6 %)
+constexpr uint32_t GW = 256;                   // guess window (16 B per lane)
+constexpr uint32_t HOP_LINE = 0, HOP_VERIFY = 1, HOP_FIND = 2, HOP_DONE = 3;
 
-// first '\n' at or after q (q < n, buf[n - 1] == '\n'), 4 KiB per round
-__device__ uint64_t find_nl(const uint8_t *buf, uint64_t n, uint64_t q) {
-    const uint32_t l = vw::lane_id();
-    for (;;) {
-        if (q >= n) return n - 1;   // (buf[n - 1] is '\n')
-        uint32_t m[4];
-#pragma unroll
-        for (uint32_t k = 0; k < 4; k++) m[k] = nl_mask16(buf, n, q + 1024u * k + 16u * l);
-#pragma unroll
-        for (uint32_t k = 0; k < 4; k++) {
-            const uint64_t b = vw::ballot(m[k] != 0);
-            if (b) {
-                const uint32_t f = (uint32_t)__builtin_ctzll(b);
-                return q + 1024u * k + 16u * f + (uint32_t)__builtin_ctz(vw::readlane(m[k], f));
-            }
-        }
-        q += 4096;
-    }
-}
-
-// end ('\n') of the line starting at p (p < n); pl: the previous predicted
-// line's prefix length (updated)
-__device__ uint64_t line_end(const uint8_t *buf, uint64_t n, uint64_t p, uint32_t S, uint32_t &pl) {
-    const uint32_t l = vw::lane_id();
-    const uint64_t x = p + pl + 4ull * S - 1;      // the end if the prefix is as long as the last one
-    const uint64_t g0 = x >= GW / 2 ? x - GW / 2 : 0;
-    // the line's first 1 KiB and the guess window, both in flight
-    const uint32_t nm = nl_mask16(buf, n, p + 16u * l);
+// 16 bytes at p (bytes at or past n read as 0)
+__device__ __forceinline__ uint4 load16(const uint8_t *buf, uint64_t n, uint64_t p) {
+    if (p + 16 <= n) return *reinterpret_cast<const uint4 *>(buf + p);
     uint4 v = make_uint4(0, 0, 0, 0);
-    const uint64_t q = p + 16u * l;
-    if (q + 16 <= n) v = *reinterpret_cast<const uint4 *>(buf + q);
-    uint32_t gw = 0;
-    const uint64_t gq = g0 + 4u * l;
-    if (gq + 4 <= n) __builtin_memcpy(&gw, buf + gq, 4);
-    const uint32_t b0 = vw::readlane(v.x & 0xFFu, 0);
-    // the first '\n' in the window is the line end (an empty line: p itself)
-    const uint64_t nb = vw::ballot(nm != 0);
-    if (nb) {
-        const uint32_t f = (uint32_t)__builtin_ctzll(nb);
-        return p + 16u * f + (uint32_t)__builtin_ctz(vw::readlane(nm, f));
+    for (uint32_t j = 0; j < 16 && p + j < n; j++)
+        (j < 4 ? v.x : j < 8 ? v.y : j < 12 ? v.z : v.w) |= (uint32_t)buf[p + j] << (8 * (j & 3));
+    return v;
+}
+__device__ __forceinline__ uint32_t tab_mask_v(uint4 v) {   // ('\t' = '\n' ^ 0x03)
+    return nl_bits(v.x ^ 0x03030303u) | nl_bits(v.y ^ 0x03030303u) << 4 | nl_bits(v.z ^ 0x03030303u) << 8 |
+           nl_bits(v.w ^ 0x03030303u) << 12;
+}
+// inclusive sum over the lane's 16-lane walker
+__device__ __forceinline__ uint32_t walker_scan(uint32_t v) {
+    const uint32_t l = vw::lane_id();
+#pragma unroll
+    for (uint32_t d = 1; d < 16; d <<= 1) {
+        const uint32_t y = vw::shfl(v, (l - d) & 63u);
+        if ((l & 15u) >= d) v += y;
     }
-    if (S == 0 || b0 == '#' || p + 1024 > n) return find_nl(buf, n, p + 1024);
-    // the 9th TAB of the window
-    const uint32_t tm = (p + 16u * l + 16 <= n) ? (nl_bits(v.x ^ 0x03030303u) | nl_bits(v.y ^ 0x03030303u) << 4 |
-                                                   nl_bits(v.z ^ 0x03030303u) << 8 | nl_bits(v.w ^ 0x03030303u) << 12)
-                                                : 0u;   // ('\t' = '\n' ^ 0x03)
-    const uint32_t c = (uint32_t)__builtin_popcount(tm);
-    const uint32_t inc = vw::scan_add(c);
-    const bool has9 = inc - c < 9 && inc >= 9;
-    const uint64_t hb = vw::ballot(has9);
-    if (!hb) return find_nl(buf, n, p + 1024);      // prefix longer than 1 KiB: scan
-    const uint32_t k9 = (uint32_t)__builtin_ctzll(hb);
-    uint32_t mm = tm;
-    for (uint32_t k = inc - c; k < 8; k++) mm &= mm - 1;   // (lane k9 only; others' values unused)
-    const uint32_t t9 = vw::readlane(16u * l + (uint32_t)__builtin_ctz(mm | 0x10000u), k9);
-    const uint64_t gt0 = p + t9 + 1;
-    const uint64_t e = gt0 + 4ull * S - 1;
-    pl = (uint32_t)(gt0 - p);
-    if (e >= n) return find_nl(buf, n, p + 1024);
-    // the predicted end and the TABs before it, from the guess window (or one more load)
-    bool ok;
-    if (e >= g0 + 124 && e < g0 + GW && g0 + GW <= n) {
-        // lane j's dword holds bytes [g0 + 4 j, + 4): byte e - 4 i is byte ((e - g0) & 3) of lane (e - g0) / 4 - i
-        const uint32_t le = (uint32_t)(e - g0) >> 2, sh = 8u * ((uint32_t)(e - g0) & 3u);
-        const uint32_t byte = (gw >> sh) & 0xFFu;
-        const bool mine = l <= le && l + 31 >= le;       // lanes le - 31 .. le
-        const uint32_t want = l == le ? 0x0Au : 0x09u;
-        ok = vw::ballot(mine && byte != want) == 0;
-    } else {
-        uint32_t w = 0;
-        const bool mine = l < 32;
-        const uint64_t a = e - 4ull * l;                 // lane i: byte e - 4 i
-        if (mine && a < n && a >= gt0) w = buf[a];
-        const uint32_t want = l == 0 ? 0x0Au : 0x09u;
-        ok = S >= 32 && vw::ballot(mine && w != want) == 0;
-    }
-    if (ok) return e;
-    return find_nl(buf, n, p + 1024);
+    return v;
 }
 
 __global__ __launch_bounds__(256) void k_nl_hop(const uint8_t *buf, uint64_t n, uint64_t n_seg, uint32_t S,
-                                                uint32_t *seg_cnt, uint64_t *slot) {
-    const uint64_t g = (uint64_t)blockIdx.x * IX_WAVES + vw::readfirst(threadIdx.x >> 6);
-    const uint64_t seg0 = g * HOPG;
-    if (seg0 >= n_seg) return;
-    const uint32_t l = vw::lane_id();
-    const uint64_t lo = seg0 * SEG, hi = (seg0 + HOPG) * SEG < n ? (seg0 + HOPG) * SEG : n;
-    uint32_t cnt = 0;   // lane k < HOPG: '\n' count of segment seg0 + k
-    auto record = [&](uint64_t e) {   // lo <= e < hi, in order
-        const uint32_t k = (uint32_t)((e - lo) / SEG);
-        const uint32_t c = vw::readlane(cnt, k);
-        if (l == 0 && c < NL_SLOT) slot[(seg0 + k) * NL_SLOT + c] = e;
-        cnt += l == k ? 1u : 0u;
+                                                uint32_t wseg, uint32_t *seg_cnt, uint64_t *slot) {
+    const uint32_t l = vw::lane_id(), wl = l & 15u, w0 = l & ~15u, sh = l & 48u;   // w0: the walker's first lane
+    const uint64_t walker = ((uint64_t)blockIdx.x * IX_WAVES + (threadIdx.x >> 6)) * HOPW + (l >> 4);
+    const uint64_t sg0 = walker * wseg;                              // the walker's first segment
+    const uint64_t lo = sg0 * SEG, hi = umin64((sg0 + wseg) * SEG, n);
+    const uint32_t nseg = sg0 >= n_seg ? 0u : (uint32_t)umin64(wseg, n_seg - sg0);
+    uint32_t mode = nseg == 0 ? HOP_DONE : (lo == 0 ? HOP_LINE : HOP_FIND);
+    uint64_t p = 0, q = lo == 0 ? 0 : lo - 1, e = 0;
+    uint32_t pl = 0, rows = 4;          // previous prefix length; 256-byte rows of the next LINE window
+    uint32_t cur = 0, cc = 0;           // current segment (in the span) and its count
+    auto record = [&](uint64_t x) {     // (the walker's lanes; lo <= x < hi, in order)
+        const uint32_t k = (uint32_t)((x - lo) / SEG);
+        for (; cur < k; cur++, cc = 0)
+            if (l == w0) seg_cnt[sg0 + cur] = cc;
+        if (l == w0 && cc < NL_SLOT) slot[(sg0 + cur) * NL_SLOT + cc] = x;
+        cc++;
     };
-    uint64_t p = 0;
-    if (lo > 0) {
-        const uint64_t e = find_nl(buf, n, lo - 1);
-        if (e >= lo && e < hi) record(e);
-        p = e + 1;
+    auto wbits = [&](bool pr) { return (uint32_t)(vw::ballot(pr) >> sh) & 0xFFFFu; };
+    while (vw::ballot(mode != HOP_DONE)) {
+        // ---- loads: the main window (LINE: `rows` rows, FIND: 4), the guess window ----
+        const uint64_t base = mode == HOP_FIND ? q : p;
+        const uint32_t nr = mode == HOP_FIND ? 4u : mode == HOP_LINE ? rows : 0u;
+        uint4 v[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) v[k] = k < nr ? load16(buf, n, base + 256u * k + 16u * wl) : make_uint4(0, 0, 0, 0);
+        uint64_t g0 = 0;
+        if (mode == HOP_LINE) {
+            const uint64_t x = p + pl + 4ull * S - 1;   // the end if the prefix is as long as the last one
+            g0 = x >= GW / 2 + 62 ? x - (GW / 2 + 62) : 0;
+        } else if (mode == HOP_VERIFY) {
+            g0 = e + 1 >= GW ? e + 1 - GW : 0;
+        }
+        const bool gv = (mode == HOP_LINE || mode == HOP_VERIFY) && g0 + GW <= n;
+        const uint4 ga = gv ? *reinterpret_cast<const uint4 *>(buf + g0 + 16u * wl) : make_uint4(0, 0, 0, 0);
+        // ---- the first '\n' of the main window (row-major: row k, then lane) ----
+        uint64_t first = ~0ull;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {
+            const uint32_t m = nl_mask_v(v[k]);
+            const uint32_t b = wbits(m != 0);
+            const uint32_t f = b ? (uint32_t)__builtin_ctz(b) : 0u;
+            const uint32_t mf = vw::shfl(m, w0 + f);   // (collectives stay wave-uniform)
+            if (b && first == ~0ull) first = base + 256u * k + 16u * f + (uint32_t)__builtin_ctz(mf | 0x10000u);
+        }
+        bool found = false, check = false;
+        if (mode == HOP_FIND) {
+            if (first != ~0ull) { e = first; found = true; }
+            else if (q + 1024 >= n) { e = n - 1; found = true; }   // (buf[n - 1] is '\n')
+            else q += 1024;
+        }
+        // ---- LINE: the 9th TAB, the predicted end ----
+        uint32_t t9 = ~0u, acc = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {
+            const bool act = k < nr && mode == HOP_LINE && first == ~0ull && t9 == ~0u;
+            if (vw::ballot(act)) {   // (wave-uniform: walkers without work compute and drop)
+                const uint32_t tm = act ? tab_mask_v(v[k]) : 0u;
+                const uint32_t c = (uint32_t)__builtin_popcount(tm);
+                const uint32_t inc = walker_scan(c) + acc;
+                const bool has9 = act && inc - c < 9 && inc >= 9;
+                uint32_t mm = tm;
+                for (uint32_t r = inc - c; has9 && r < 8; r++) mm &= mm - 1;
+                const uint32_t hb = wbits(has9);
+                const uint32_t tl = 256u * k + 16u * wl + (uint32_t)__builtin_ctz(mm | 0x10000u);
+                const uint32_t t9n = vw::shfl(tl, w0 + (hb ? (uint32_t)__builtin_ctz(hb) : 0u));
+                if (hb) t9 = t9n;
+                acc = vw::shfl(inc, w0 + 15);
+            }
+        }
+        const uint32_t b0 = vw::shfl(v[0].x & 0xFFu, w0);
+        if (mode == HOP_LINE) {
+            if (first != ~0ull) { e = first; found = true; }
+            else if (S == 0 || b0 == '#') { mode = HOP_FIND; q = p + 256u * rows; }
+            else if (t9 == ~0u) {
+                if (rows < 4) rows = 4;                              // the line again with 1 KiB
+                else { mode = HOP_FIND; q = p + 1024; }
+            } else {
+                pl = t9 + 1;
+                const uint32_t want = pl + 96;
+                rows = want <= 256 ? 1u : want <= 512 ? 2u : 4u;
+                e = p + t9 + 4ull * S;   // gt0 + 4 S - 1
+                if (e >= n) { mode = HOP_FIND; q = p + 256u * nr; }
+                else if (gv && e >= g0 + 124 && e < g0 + GW) check = true;
+                else mode = HOP_VERIFY;
+            }
+        } else if (mode == HOP_VERIFY) {
+            if (gv && e >= g0 + 124) check = true;
+            else { mode = HOP_FIND; q = p; }
+        }
+        // ---- the check: byte e is '\n', bytes e - 4 i (i = 1..31) TABs ----
+        bool bad = false;
+        if (check) {
+            const uint32_t s8 = 8u * (uint32_t)((e - g0) & 3u);
+            const uint32_t gw[4] = {ga.x, ga.y, ga.z, ga.w};
+#pragma unroll
+            for (uint32_t j = 0; j < 4; j++) {
+                const uint64_t a = g0 + 16u * wl + 4u * j + ((e - g0) & 3u);
+                const uint32_t want = a == e ? 0x0Au : 0x09u;
+                bad |= a + 124 >= e && a <= e && ((gw[j] >> s8) & 0xFFu) != want;
+            }
+        }
+        const bool bw = wbits(bad) != 0;
+        if (check) {
+            if (!bw) found = true;
+            else { mode = HOP_FIND; q = p + 256u * nr; }   // (past the first window: no '\n' there)
+        }
+        // ---- the line end: record, next line ----
+        if (found) {
+            if (e >= hi) mode = HOP_DONE;
+            else {
+                if (e >= lo) record(e);
+                p = e + 1;
+                mode = p >= hi ? HOP_DONE : HOP_LINE;
+            }
+        }
     }
-    uint32_t pl = 0;
-    while (p < hi) {
-        const uint64_t e = line_end(buf, n, p, S, pl);   // (wave-uniform)
-        if (e >= hi) break;
-        record(e);
-        p = e + 1;
-    }
-    if (l < HOPG && seg0 + l < n_seg) seg_cnt[seg0 + l] = cnt;
+    for (; cur < nseg; cur++, cc = 0)
+        if (l == w0) seg_cnt[sg0 + cur] = cc;
 }
 
+// One wave per 64 segments, one lane per segment (most hold a few lines:
+// a wave per segment spent ~0.1 ms launching 622k waves for 8 MB of
+// positions); a segment with more lines than its slot holds is scanned
+// again by the whole wave, one such segment after the other.
 __global__ __launch_bounds__(256) void k_nl_place(const uint8_t *buf, uint64_t n, uint64_t n_seg, const uint32_t *seg_cnt,
                                                   const uint64_t *slot, const uint64_t *seg_base, uint64_t *nl) {
-    const uint64_t seg = (uint64_t)blockIdx.x * IX_WAVES + vw::readfirst(threadIdx.x >> 6);
-    if (seg >= n_seg) return;
     const uint32_t l = vw::lane_id();
-    const uint32_t c = seg_cnt[seg];
-    uint64_t *dst = nl + seg_base[seg];
+    const uint64_t seg0 = ((uint64_t)blockIdx.x * IX_WAVES + vw::readfirst(threadIdx.x >> 6)) * 64;
+    if (seg0 >= n_seg) return;
+    const uint64_t seg = seg0 + l;
+    const uint32_t c = seg < n_seg ? seg_cnt[seg] : 0u;
     if (c <= NL_SLOT) {
         const uint64_t *sl = slot + seg * NL_SLOT;
-        for (uint32_t k = l; k < c; k += 64) dst[k] = sl[k];
-        return;
+        uint64_t *dst = nl + (seg < n_seg ? seg_base[seg] : 0);
+        for (uint32_t k = 0; k < c; k++) dst[k] = sl[k];
     }
     // more lines than the slot holds: scan the segment again (at most c
     // positions: the hop index may have counted fewer than there are, and
     // the encoder then rejects the chunk's index)
-    uint32_t o = 0;
-    for (uint32_t w = 0; w < SEG; w += WIN) o += nl_window(buf, n, seg * SEG + w + 16 * l, dst, o, c);
+    for (uint64_t m = vw::ballot(c > NL_SLOT); m; m &= m - 1) {
+        const uint32_t f = (uint32_t)__builtin_ctzll(m);
+        const uint64_t sf = seg0 + f;
+        const uint32_t cf = vw::readlane(c, f);
+        uint64_t *dst = nl + seg_base[sf];
+        uint32_t o = 0;
+        for (uint32_t w = 0; w < SEG; w += WIN) o += nl_window(buf, n, sf * SEG + w + 16 * l, dst, o, cf);
+    }
 }
 
 __global__ __launch_bounds__(256) void k_line_kind(const uint8_t *buf, const uint64_t *nl, uint64_t n_lines,
@@ -328,9 +382,15 @@ hipError_t vcfc_line_index(const uint8_t *buf, uint64_t n, uint8_t *ws, const Vc
     if (n == 0) return hipMemsetAsync(x.counts, 0, 24, s);
     const uint64_t n_seg = (n + SEG - 1) / SEG;
     const dim3 sg((unsigned)((n_seg + IX_WAVES - 1) / IX_WAVES)), blk(64 * IX_WAVES);
-    if (S_hint)
-        hipLaunchKernelGGL(k_nl_hop, dim3((unsigned)((n_seg + HOPG * IX_WAVES - 1) / (HOPG * IX_WAVES))), blk, 0, s, buf,
-                           n, n_seg, S_hint, seg_cnt, slot);
+    if (S_hint >= 32) {
+        // spans of wseg segments: about HOP_WALKERS walkers, each over at
+        // least 2 segments
+        const uint64_t wseg = std::max<uint64_t>(2, (n_seg + HOP_WALKERS - 1) / HOP_WALKERS);
+        const uint64_t walkers = (n_seg + wseg - 1) / wseg;
+        const uint64_t per_block = (uint64_t)HOPW * IX_WAVES;
+        hipLaunchKernelGGL(k_nl_hop, dim3((unsigned)((walkers + per_block - 1) / per_block)), blk, 0, s, buf, n, n_seg,
+                           S_hint, (uint32_t)wseg, seg_cnt, slot);
+    }
     else
         hipLaunchKernelGGL(k_nl_scan, sg, blk, 0, s, buf, n, n_seg, seg_cnt, slot);
     if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -356,8 +416,8 @@ hipError_t vcfc_line_index_place(const uint8_t *buf, uint64_t n, uint64_t n_line
     if (n_lines == 0) return hipMemsetAsync(x.counts + 1, 0, 24, s);
     if ((e = hipMemsetAsync(x.counts + 3, 0, 8, s)) != hipSuccess) return e;
     const uint64_t n_seg = (n + SEG - 1) / SEG;
-    hipLaunchKernelGGL(k_nl_place, dim3((unsigned)((n_seg + IX_WAVES - 1) / IX_WAVES)), dim3(64 * IX_WAVES), 0, s, buf,
-                       n, n_seg, seg_cnt, slot, seg_base, nl);
+    hipLaunchKernelGGL(k_nl_place, dim3((unsigned)((n_seg + 64 * IX_WAVES - 1) / (64 * IX_WAVES))), dim3(64 * IX_WAVES), 0,
+                       s, buf, n, n_seg, seg_cnt, slot, seg_base, nl);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const dim3 g((unsigned)((n_lines + 255) / 256)), blk(256);
     hipLaunchKernelGGL(k_line_kind, g, blk, 0, s, buf, nl, n_lines, is_data, is_pass);

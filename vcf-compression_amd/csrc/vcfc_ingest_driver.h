@@ -627,6 +627,7 @@ inline int compress_device(const uint8_t *d_in, uint64_t N, uint8_t *d_out, uint
             std::vector<uint8_t> h(std::min<uint64_t>(N, 1u << 20));
             if (!d2h(h.data(), d_in, h.size()) || !sync()) return ST_E_HIP;
             S_hint = header_samples(h.data(), h.size());
+            if (S_hint < 32) S_hint = 0;   // (the check reads 32 tokens)
         }
         if (trace) fprintf(stderr, "compress_device: S_hint=%u\n", S_hint);
     }
