@@ -155,16 +155,17 @@ def cpu_baseline(rows, torch, args):
 
 def load_pmc(workload_key, name="pmc_k_encode.json"):
     """HBM bytes per launch from a committed rocprofv3 PMC summary
-    (profiles/<name>) when it was measured on this workload, else None."""
-    p = os.path.join(REPO, "profiles", name)
-    if not os.path.exists(p):
-        return None
-    try:
-        d = json.load(open(p))
+    (profiles/<name>, or profiles/<stem>_*.json for other workloads) when it
+    was measured on this workload, else None."""
+    import glob
+    stem = os.path.splitext(name)[0]
+    for p in [os.path.join(REPO, "profiles", name)] + sorted(glob.glob(os.path.join(REPO, "profiles", stem + "_*.json"))):
+        try:
+            d = json.load(open(p))
+        except Exception:
+            continue
         if d.get("workload") == workload_key:
             return d.get("hbm_bytes_per_launch")
-    except Exception:
-        return None
     return None
 
 

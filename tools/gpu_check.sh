@@ -52,6 +52,17 @@ for s in $STEPS; do
          done ;;
     shard) timeout -k 10 900 python bench.py --mode biobank --rows-total 5000000 --steps 1 --warmup 1 > "$O/bench_biobank_shard.json" 2> "$O/bench_biobank_shard.err" || { echo "shard failed"; tail -30 "$O/bench_biobank_shard.err"; exit 1; } ; cat "$O/bench_biobank_shard.json" ;;
     ptest) timeout -k 10 1000 python -u -m pytest ${PT_ARGS} -x -v -p no:cacheprovider --timeout 400 --timeout-method thread > "$O/pytest_sel.log" 2>&1 || { echo "ptest failed rc=$?"; tail -60 "$O/pytest_sel.log"; exit 1; } ; tail -5 "$O/pytest_sel.log" ;;
+    pmcenc) # encoder HBM bytes per launch for laws 1, 0, 2 (two passes each) -> pmc_k_encode*.json
+         for L in 1 0 2; do
+           for P in FETCH_SIZE WRITE_SIZE; do
+             (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc $P --kernel-trace --output-format csv -d "$O/pmcenc_l${L}_$P" -o run -- python3 "$R/bench.py" --law $L --steps 3 --warmup 1 --no-cpu-baseline > "$O/pmcenc_l${L}_$P.log" 2>&1) || { echo "pmcenc $L $P failed rc=$?"; tail -30 "$O/pmcenc_l${L}_$P.log"; exit 1; }
+           done
+         done
+         python3 tools/pmc_encode_json.py "$O/pmcenc_l1_FETCH_SIZE" "$O/pmcenc_l1_WRITE_SIZE" "chr22-shaped/2504x1000000" "$O/pmc_k_encode.json" "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes (tools/gpu_check.sh pmcenc, run $TAG)" > /dev/null &&
+         python3 tools/pmc_encode_json.py "$O/pmcenc_l0_FETCH_SIZE" "$O/pmcenc_l0_WRITE_SIZE" "random_vcf-law/2504x1000000" "$O/pmc_k_encode_law0.json" "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes (tools/gpu_check.sh pmcenc, run $TAG)" > /dev/null &&
+         python3 tools/pmc_encode_json.py "$O/pmcenc_l2_FETCH_SIZE" "$O/pmcenc_l2_WRITE_SIZE" "general-shapes (chrX haploid/GT:DP:GQ/missing)/2504x1000000" "$O/pmc_k_encode_law2.json" "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes (tools/gpu_check.sh pmcenc, run $TAG)" > /dev/null || { echo "pmc json failed"; exit 1; } ;;
+    benchdev) timeout -k 10 300 python bench.py --mode devfile > "$O/bench_devfile.json" 2> "$O/bench_devfile.err" || { echo "benchdev failed"; tail -30 "$O/bench_devfile.err"; exit 1; } ; cat "$O/bench_devfile.json" ;;
+    profdev) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/profdev" -o run -- python3 "$R/bench.py" --mode devfile --steps 5 --warmup 1 > "$O/profdev.log" 2>&1) || { echo "profdev failed rc=$?"; tail -30 "$O/profdev.log"; exit 1; } ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -21,7 +21,8 @@
 
 // Alignment: buf, the lines in it and out may start at any byte.  The
 // kernels address them with 16-byte loads and stores at the base's own
-// alignment (k_nl_scan reads a chunk from d_in + pos, k_compact_out stores
+// alignment (k_nl_scan reads a chunk from d_in + pos, k_nl_hop a line's
+// windows from any byte of it, k_compact_out stores
 // 16-B blocks at out + 16k, out = d_out + header bytes in compress_device);
 // gfx950 global and buffer memory instructions take unaligned addresses (ROCm
 // runs the GPU with SH_MEM_CONFIG's unaligned mode), an unaligned base only
