@@ -1031,21 +1031,23 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
         const uint32_t cnt = nt + 2u * (uint32_t)__builtin_popcount(vm) - (lastin ? 1u : 0u);
         const uint32_t incl2 = vw::scan_add(cnt);
         const uint32_t base = (r.wpos + incl2 - cnt) & RMASK;
-        uint8_t *const lb0 = r.lds + base;
-        uint8_t *const dm = r.lds + RING_DUMMY;
         // byte stores (unaligned dword stores from every lane wait ~100x
-        // longer to issue: SQ_WAIT_INST_LDS, profiles/r03/pmc/pmc_var_kind1*)
-        uint32_t o = 0;
+        // longer to issue: SQ_WAIT_INST_LDS, profiles/r03/pmc/pmc_var_kind1*;
+        // packed aligned dwords cost more VALU than they save, ab_var_packer.txt),
+        // addressed as in the mixed step below
+        const int32_t dmi = (int32_t)RING_DUMMY;
+        int32_t ro = (int32_t)base - dmi;
+        const uint32_t vm2 = vm & ~(lastin ? (1u << lastrel) : 0u);
 #pragma unroll
         for (int h = 0; h < 16; h++) {
-            const uint32_t es = (S >> h) & 1u;
-            const uint32_t np = (vm >> h) & 1u ? ((int32_t)h == lastrel ? 1u : 2u) : 0u;
+            const int32_t es = (int32_t)((S >> h) & 1u);
+            const int32_t e1 = (int32_t)((vm >> h) & 1u), e2 = (int32_t)((vm2 >> h) & 1u);
             const uint32_t pay = d[h >> 1] >> (16 * (h & 1));
-            *(es ? lb0 + o : dm) = (uint8_t)0xE1u;
-            o += es;
-            *(np ? lb0 + o : dm) = (uint8_t)pay;
-            *(np == 2u ? lb0 + o + 1 : dm) = (uint8_t)(pay >> 8);
-            o += np;
+            r.lds[(uint32_t)vw::mad24(es, ro, dmi)] = (uint8_t)0xE1u;
+            ro += es;
+            r.lds[(uint32_t)vw::mad24(e1, ro, dmi)] = (uint8_t)pay;
+            r.lds[(uint32_t)vw::mad24(e2, ro + 1, dmi)] = (uint8_t)(pay >> 8);
+            ro += e1 + e2;
         }
         ring_unwrap(r, base + cnt);
         r.wpos += vw::readlane(incl2, 63);
@@ -1126,30 +1128,33 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
                          2u * (uint32_t)__builtin_popcount(EH) - (lastin ? 1u : 0u);
     const uint32_t incl2 = vw::scan_add(cnt);
     const uint32_t base = (r.wpos + incl2 - cnt) & RMASK;
-    uint8_t *const lb0 = r.lds + base;
-    uint8_t *const dm = r.lds + RING_DUMMY;   // shared dummy word (see esc8)
-    // Per half, in token order: [lead][0xE1][payload], one byte store each
-    // (stores that emit nothing go to the shared dummy word)
-    uint32_t o = 0;
-    if (full) *lb0 = (uint8_t)(cls_mask_f(cin) | cap);
-    o += full ? 1u : 0u;
+    // Per half, in token order: [lead][0xE1][payload], one byte store each.
+    // A byte goes to dummy + f * (base + o - dummy) (f in {0, 1}: one
+    // v_mad_u32_u24, as esc8); the stores that emit nothing land on the
+    // shared dummy word.  Payload bytes: the first of every escape half, the
+    // second of every escape half but the row's last (its line end).
+    const int32_t dmi = (int32_t)RING_DUMMY;
+    int32_t ro = (int32_t)base - dmi;           // base + o - dummy
+    if (full) r.lds[base] = (uint8_t)(cls_mask_f(cin) | cap);
+    ro += full ? 1 : 0;
+    const uint32_t EH2 = EH & ~(lastrel >= 0 && lastrel < 16 ? (1u << lastrel) : 0u);
     uint32_t tk = 0, ptk = 0;   // token index (in the lane) of half h; of the run start before it
 #pragma unroll
     for (int h = 0; h < 16; h++) {
-        const uint32_t hl = (LEAD >> h) & 1u, es = (XE >> h) & 1u, eh = (EH >> h) & 1u;
+        const int32_t hl = (int32_t)((LEAD >> h) & 1u), es = (int32_t)((XE >> h) & 1u);
+        const int32_t e1 = (int32_t)((EH >> h) & 1u), e2 = (int32_t)((EH2 >> h) & 1u);
         const uint32_t pc = (((q1 >> h) & 1u) << 1) | ((q0 >> h) & 1u);    // predecessor class (plain when hl)
         const uint32_t lb = (uint32_t)h == lr ? b1v : (cls_mask_f(pc) | (tk - ptk));
         ptk = (RS >> h) & 1u ? tk : ptk;
         tk += (S >> h) & 1u;
-        const uint32_t np = eh ? ((int32_t)h == lastrel ? 1u : 2u) : 0u;
         const uint32_t pay = d[h >> 1] >> (16 * (h & 1));
-        *(hl ? lb0 + o : dm) = (uint8_t)lb;
-        o += hl;
-        *(es ? lb0 + o : dm) = (uint8_t)0xE1u;
-        o += es;
-        *(np ? lb0 + o : dm) = (uint8_t)pay;
-        *(np == 2u ? lb0 + o + 1 : dm) = (uint8_t)(pay >> 8);
-        o += np;
+        r.lds[(uint32_t)vw::mad24(hl, ro, dmi)] = (uint8_t)lb;
+        ro += hl;
+        r.lds[(uint32_t)vw::mad24(es, ro, dmi)] = (uint8_t)0xE1u;
+        ro += es;
+        r.lds[(uint32_t)vw::mad24(e1, ro, dmi)] = (uint8_t)pay;
+        r.lds[(uint32_t)vw::mad24(e2, ro + 1, dmi)] = (uint8_t)(pay >> 8);
+        ro += e1 + e2;
     }
     ring_unwrap(r, base + cnt);
     r.wpos += vw::readlane(incl2, 63);
