@@ -1138,17 +1138,35 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
     if (full) r.lds[base] = (uint8_t)(cls_mask_f(cin) | cap);
     ro += full ? 1 : 0;
     const uint32_t EH2 = EH & ~(lastrel >= 0 && lastrel < 16 ? (1u << lastrel) : 0u);
+    // The first run start's lead byte (b1v) is stored on its own: only
+    // payload bytes of the entering escape precede it (no lead or 0xE1 bit
+    // lies below the first run start); the loop's leads are the later starts'.
+    {
+        const uint32_t bl = lrbit - 1u;   // (lrbit 0: no start, lead1 false)
+        const int32_t at = ro + (int32_t)__builtin_popcount(EH & bl) + (int32_t)__builtin_popcount(EH2 & bl);
+        r.lds[(uint32_t)vw::mad24(lead1 ? 1 : 0, at, dmi)] = (uint8_t)b1v;
+    }
+    const uint32_t LEADr = LEAD & ~lrbit;
+    // predecessor classes, 2 bits per half (class mask byte by one v_perm)
+    auto spread = [](uint32_t x) {   // bit i -> bit 2 i (16 bits)
+        x = (x | (x << 8)) & 0x00FF00FFu;
+        x = (x | (x << 4)) & 0x0F0F0F0Fu;
+        x = (x | (x << 2)) & 0x33333333u;
+        return (x | (x << 1)) & 0x55555555u;
+    };
+    const uint32_t pcw = spread(q0 & 0xFFFFu) | (spread(q1 & 0xFFFFu) << 1);
     uint32_t tk = 0, ptk = 0;   // token index (in the lane) of half h; of the run start before it
 #pragma unroll
     for (int h = 0; h < 16; h++) {
         const int32_t hl = (int32_t)((LEAD >> h) & 1u), es = (int32_t)((XE >> h) & 1u);
+        const int32_t hr = (int32_t)((LEADr >> h) & 1u);
         const int32_t e1 = (int32_t)((EH >> h) & 1u), e2 = (int32_t)((EH2 >> h) & 1u);
-        const uint32_t pc = (((q1 >> h) & 1u) << 1) | ((q0 >> h) & 1u);    // predecessor class (plain when hl)
-        const uint32_t lb = (uint32_t)h == lr ? b1v : (cls_mask_f(pc) | (tk - ptk));
+        const uint32_t pc = (pcw >> (2 * h)) & 3u;    // predecessor class (plain when hr)
+        const uint32_t lb = vw::perm(0x80C0A000u, 0x80C0A000u, pc) | (tk - ptk);
         ptk = (RS >> h) & 1u ? tk : ptk;
         tk += (S >> h) & 1u;
         const uint32_t pay = d[h >> 1] >> (16 * (h & 1));
-        r.lds[(uint32_t)vw::mad24(hl, ro, dmi)] = (uint8_t)lb;
+        r.lds[(uint32_t)vw::mad24(hr, ro, dmi)] = (uint8_t)lb;
         ro += hl;
         r.lds[(uint32_t)vw::mad24(es, ro, dmi)] = (uint8_t)0xE1u;
         ro += es;
