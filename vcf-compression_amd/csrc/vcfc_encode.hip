@@ -1006,12 +1006,18 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
     const uint32_t vm = lastrel >= 15 ? 0xFFFFu : lastrel < 0 ? 0u : (2u << lastrel) - 1u;   // valid halves
     // TAB masks over halves 0..17: tb0 = first byte TAB (never valid), tb1 = second byte TAB (a token's end);
     // plain 3-byte candidates: bytes "a|b" from the half, a, b in {0,1}; a, b bits
-    uint32_t tb0 = 0, tb1 = 0;
+    // (SWAR over the halves' first bytes A and second bytes P, four halves a
+    // word: half 4k + i is byte i of A[k] / P[k])
+    uint32_t tb0, tb1;
+    {
+        const uint32_t z8 = zero_bytes4(d[8] ^ 0x09090909u);   // halves 16, 17
+        tb0 = even2(z8) << 16;
+        tb1 = odd2(z8) << 16;
+    }
 #pragma unroll
-    for (int j = 0; j < 9; j++) {
-        const uint32_t z = zero_bytes4(d[j] ^ 0x09090909u);
-        tb0 |= even2(z) << (2 * j);
-        tb1 |= odd2(z) << (2 * j);
+    for (int k = 0; k < 4; k++) {
+        tb0 |= zero_bytes4(vw::perm(d[2 * k + 1], d[2 * k], 0x06040200u) ^ 0x09090909u) << (4 * k);
+        tb1 |= zero_bytes4(vw::perm(d[2 * k + 1], d[2 * k], 0x07050301u) ^ 0x09090909u) << (4 * k);
     }
     if (lastrel >= 0 && lastrel <= 17) tb1 |= 1u << lastrel;   // the row's last half ends its token (line end)
     if (vw::ballot((tb0 & vm) != 0)) return false;           // an empty field, or a token of even length
@@ -1063,14 +1069,22 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
     // are left to k_encode_general
     if (vw::ballot((S & ~tb1 & ~(tb1 >> 1)) != 0)) return false;
     // plain 3-byte candidates: bytes "a|b" from the half, a, b in {0,1}; a, b bits
-    constexpr uint32_t Z3 = 0x00307C30u;   // "0|0"
+    // (SWAR, four halves a word: A = first bytes, P = second bytes, B = the
+    // byte after each half, i.e. the next half's first; bit 0 of the bytes
+    // of A / B gathered by one multiply)
     uint32_t p3 = 0, am = 0, bm = 0;
+    auto bits0 = [](uint32_t x) { return (((x & 0x01010101u) * 0x01020408u) >> 24) & 0xFu; };
+    uint32_t An = vw::perm(d[1], d[0], 0x06040200u);
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
-        const uint32_t e = d[j], o = vw::alignbyte(d[j + 1], d[j], 2);
-        p3 |= ((((e ^ Z3) & 0x00FEFFFEu) == 0 ? 1u : 0u) | (((o ^ Z3) & 0x00FEFFFEu) == 0 ? 2u : 0u)) << (2 * j);
-        am |= ((e & 1u) | ((o & 1u) << 1)) << (2 * j);
-        bm |= (((e >> 16) & 1u) | (((o >> 16) & 1u) << 1)) << (2 * j);
+    for (int k = 0; k < 4; k++) {
+        const uint32_t A = An;
+        An = k < 3 ? vw::perm(d[2 * k + 3], d[2 * k + 2], 0x06040200u) : d[8];   // (byte 0 of d[8]: half 16's first)
+        const uint32_t P = vw::perm(d[2 * k + 1], d[2 * k], 0x07050301u);
+        const uint32_t B = vw::alignbyte(An, A, 1);
+        const uint32_t y = (((A ^ 0x30303030u) | (B ^ 0x30303030u)) & 0xFEFEFEFEu) | (P ^ 0x7C7C7C7Cu);
+        p3 |= zero_bytes4(y) << (4 * k);
+        am |= bits0(A) << (4 * k);
+        bm |= bits0(B) << (4 * k);
     }
     const uint32_t PL = S & p3 & ~tb1 & (tb1 >> 1);           // plain: exactly 3 bytes "a|b"
     const uint32_t X0 = PL & bm, X1 = PL & am, XE = S & ~PL;  // class bits at the starts (bit 2: escape)
