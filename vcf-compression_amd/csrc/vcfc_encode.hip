@@ -1098,16 +1098,14 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
     const uint32_t lastc = (((XE >> hs) & 1u) << 2) | (((X1 >> hs) & 1u) << 1) | ((X0 >> hs) & 1u);
     const uint32_t pek = vw::shr1z(vw::scan_max(S ? ((l + 1u) << 3) | lastc : 0u));
     const uint32_t cin = pek ? (pek & 7u) : f.pcls;
-    // fill each start's class forward over its continuation halves
-    uint32_t c0 = X0, c1 = X1, ce = XE, has = S;
-#pragma unroll
-    for (int k = 1; k < 16; k <<= 1) {
-        c0 |= (c0 << k) & ~has;
-        c1 |= (c1 << k) & ~has;
-        ce |= (ce << k) & ~has;
-        has |= has << k;
-    }
-    const uint32_t pre = ~has & 0xFFFFu;   // halves before the lane's first start: the entering token's
+    // fill each start's class forward over its continuation halves: adding
+    // M << 1 to the non-start mask T carries through each run of T after a
+    // start in M and stops at the next start, so T & ((T + (M << 1)) ^ T)
+    // is those runs (starts of other masks split the carries)
+    const uint32_t T = ~S & 0xFFFFu;
+    auto fill = [T](uint32_t m) { return (m | (T & ((T + (m << 1)) ^ T))) & 0xFFFFu; };
+    uint32_t c0 = fill(X0), c1 = fill(X1), ce = fill(XE);
+    const uint32_t pre = S ? (S & (0u - S)) - 1u : 0xFFFFu;   // halves before the lane's first start: the entering token's
     c0 = (c0 | ((cin & 1u) ? pre : 0u)) & 0xFFFFu;
     c1 = (c1 | ((cin & 2u) ? pre : 0u)) & 0xFFFFu;
     ce = (ce | ((cin & 4u) ? pre : 0u)) & 0xFFFFu;
@@ -1614,15 +1612,19 @@ __device__ bool row_has_nl(const uint8_t *__restrict__ line, uint32_t len) {
     return false;
 }
 
-// Variable-token kernel: the rows the fast kernel flagged, GEN_ROWS per wave
+#ifndef VCFC_VAR_ROWS
+#define VCFC_VAR_ROWS 32
+#endif
+constexpr uint32_t VAR_ROWS = VCFC_VAR_ROWS;   // rows per wave of the variable-token kernel
+// Variable-token kernel: the rows the fast kernel flagged, VAR_ROWS per wave
 // (a flag load per 32 rows, so a batch without such rows costs next to
 // nothing); rows of another shape stay flagged for k_encode_general.
 __global__ __launch_bounds__(256) void k_encode_var(VcfcEncodeArgs a, uint64_t row_lo, uint64_t row_hi) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[K1_WAVES * RING_STRIDE];
     const uint32_t wave = vw::readfirst(threadIdx.x >> 6);
     const uint32_t l = vw::lane_id();
-    const uint64_t row0 = row_lo + ((uint64_t)blockIdx.x * K1_WAVES + wave) * GEN_ROWS;
-    const bool flagged = l < GEN_ROWS && row0 + l < row_hi && a.rec_size[row0 + l] == VCFCD_RETRY;
+    const uint64_t row0 = row_lo + ((uint64_t)blockIdx.x * K1_WAVES + wave) * VAR_ROWS;
+    const bool flagged = l < VAR_ROWS && row0 + l < row_hi && a.rec_size[row0 + l] == VCFCD_RETRY;
     uint64_t todo = vw::ballot(flagged);
     while (todo) {
         const uint64_t row = row0 + (uint64_t)__builtin_ctzll(todo);
@@ -1643,8 +1645,8 @@ __global__ __launch_bounds__(256) void k_encode_var(VcfcEncodeArgs a, uint64_t r
 }
 
 // blocks of k_encode_general to launch for m rows
-static uint64_t general_blocks(uint64_t m) {
-    const uint64_t per_block = (uint64_t)K1_WAVES * GEN_ROWS;   // GEN_ROWS rows per wave
+static uint64_t general_blocks(uint64_t m, uint32_t rows_per_wave = GEN_ROWS) {
+    const uint64_t per_block = (uint64_t)K1_WAVES * rows_per_wave;
     return (m + per_block - 1) / per_block;
 }
 
@@ -1986,7 +1988,7 @@ hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t s, hipEvent_t
     hipLaunchKernelGGL(k_encode_fast, dim3((unsigned)((a.n + K1_WAVES - 1) / K1_WAVES)), dim3(64 * K1_WAVES), 0, s, a,
                        (uint64_t)0, a.n);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_encode_var, dim3((unsigned)general_blocks(a.n)), dim3(64 * K1_WAVES), 0, s, a,
+    hipLaunchKernelGGL(k_encode_var, dim3((unsigned)general_blocks(a.n, VAR_ROWS)), dim3(64 * K1_WAVES), 0, s, a,
                        (uint64_t)0, a.n);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(k_encode_general, dim3((unsigned)general_blocks(a.n)), dim3(64 * K1_WAVES), 0, s, a,
