@@ -1612,10 +1612,9 @@ __device__ bool row_has_nl(const uint8_t *__restrict__ line, uint32_t len) {
     return false;
 }
 
-#ifndef VCFC_VAR_ROWS
-#define VCFC_VAR_ROWS 32
-#endif
-constexpr uint32_t VAR_ROWS = VCFC_VAR_ROWS;   // rows per wave of the variable-token kernel
+// rows per wave of the variable-token kernel (16: law 2 -1.8 %, headline
+// step +0.2 % in empty waves; 8: -1.7 % / +0.5 %; profiles/r03/ab/ab_var_rows.txt)
+constexpr uint32_t VAR_ROWS = 32;
 // Variable-token kernel: the rows the fast kernel flagged, VAR_ROWS per wave
 // (a flag load per 32 rows, so a batch without such rows costs next to
 // nothing); rows of another shape stay flagged for k_encode_general.
