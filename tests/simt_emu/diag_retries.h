@@ -1,5 +1,5 @@
 // TEST INFRASTRUCTURE ONLY: diagnostic hooks for the emulator build -- count
-// the rows the fast kernel hands to k_encode_general (emu_api.cpp reads it).
+// the rows that take the general path (emu_api.cpp reads it).
 #pragma once
 #define VCFC_DIAG_ROW_BEGIN()
 #define VCFC_DIAG_ROW_END(a, row)

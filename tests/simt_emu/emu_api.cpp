@@ -27,7 +27,7 @@ extern "C" int emu_encode_rows(const uint8_t *buf, const uint64_t *line_off, con
     emu::g.switches = 0;
     int st = (int)vcfc_encode_device(a, nullptr);
     *err_word = *a.err;
-    if (retries) *retries = *a.retry_count;   // rows the fast kernel handed to k_encode_general
+    if (retries) *retries = *a.retry_count;   // rows that took the general path
     if (switches) *switches = emu::g.switches;
     free(ws);
     return st;

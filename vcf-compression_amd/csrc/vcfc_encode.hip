@@ -7,7 +7,9 @@
 //   k_encode_fast     one wave64 per row: tokenise, RLE-encode, stage the
 //                     record in an LDS ring, stream it to the row's staging in
 //                     1 KiB bursts; rows of another shape are flagged
-//   k_encode_general  one wave per 32 rows, encodes the flagged ones (any shape)
+//   k_encode_var      one wave per 32 rows, encodes the flagged ones: odd-length
+//                     tokens on 2-byte half-slots, any other shape by the
+//                     general path (encode_general) in the same wave
 //   k_scan_lb<0>      rec_off[i] = sum_{k<i} rec_size_k, + each 4 KiB output
 //                     tile's first row                           (tiny)
 //   k_compact_out     output-ordered: 4 KiB output tiles, 16-byte stores
@@ -39,7 +41,7 @@
 #ifndef VCFC_DIAG_ROW_BEGIN
 #define VCFC_DIAG_ROW_BEGIN()            // k_encode_fast: a row starts
 #define VCFC_DIAG_ROW_END(a, row)        // k_encode_fast: the row's record is staged
-#define VCFC_DIAG_GENERAL_ROW(a)         // k_encode_general: a flagged row is taken
+#define VCFC_DIAG_GENERAL_ROW(a)         // a flagged row takes the general path
 #define VCFC_DIAG_WS_BYTES(n) 0ull       // extra workspace bytes (at VcfcWorkspaceLayout::dbg)
 #endif
 
@@ -936,7 +938,7 @@ __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring
 // so only a lane's last emitting half writes past its end (<= 3 bytes, into
 // the next lanes' first bytes); a final store rewrites every lane's first
 // min(count, 4) bytes.  Rows of other shapes stay flagged for
-// k_encode_general.
+// the general path.
 constexpr uint32_t HPC = 1024;   // half-slots per 2 KiB chunk
 
 struct VarState : FastState {
@@ -992,7 +994,7 @@ __device__ __forceinline__ void ring_flush_var(Ring &r) {
 }
 
 // One 2 KiB chunk C of a variable-token row.  false: not this shape (the
-// row goes to k_encode_general; nothing of it is kept).
+// row takes the general path; nothing of it is kept).
 __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState &f, Ring &r) {
     const uint32_t l = vw::lane_id();
     const uint32_t NH = f.T, phi = f.phi;
@@ -1066,7 +1068,7 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
         return true;
     }
     // tokens longer than 3 bytes beside 3-byte ones (or after a plain token)
-    // are left to k_encode_general
+    // are left to the general path
     if (vw::ballot((S & ~tb1 & ~(tb1 >> 1)) != 0)) return false;
     // plain 3-byte candidates: bytes "a|b" from the half, a, b in {0,1}; a, b bits
     // (SWAR, four halves a word: A = first bytes, P = second bytes, B = the
@@ -1535,7 +1537,7 @@ __device__ __forceinline__ bool row_setup(const VcfcEncodeArgs &a, uint64_t row,
 }
 
 // Fast kernel: one wave per row; rows without the GT-only shape are queued
-// for k_encode_general.
+// for the general path.
 // Pinned to 6 waves/SIMD (the SGPR count allows no more): without the pin the
 // branch-free escape emission takes 84 VGPRs and 5 waves, +5 % on the
 // headline rows (profiles/r02/ab/ab_esc8_emit.txt).
@@ -1555,37 +1557,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 6))) voi
         // it (a flag per row, no shared queue: 750k rows appending to one
         // counter serialise at the memory side, ~8 ms on the law-2 rows)
         a.rec_size[row] = ok ? bytes : VCFCD_RETRY;
-    }
-}
-
-// General kernel: each wave reads the flags of GEN_ROWS consecutive rows
-// with one load and encodes the ones the fast kernel flagged (VCFCD_RETRY),
-// one after the other.  A small grid (n / 128 blocks) costs the headline
-// rows, which flag none, next to nothing; 32 rows per wave keep the waves of
-// the law-2 rows (75 % flagged) balanced.
-// (8 rows per wave: law 2 -1.5 %, headline +0.4 % in empty waves,
-// ab_genrows_*.txt; a resident grid striding over rows: law 2 +13.6 %,
-// ab_gen_persist.txt)
-constexpr uint32_t GEN_ROWS = 32;   // rows per wave of the general kernel
-__global__ __launch_bounds__(256) void k_encode_general(VcfcEncodeArgs a, uint64_t row_lo, uint64_t row_hi) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[K1_WAVES * RING_STRIDE];
-    const uint32_t wave = vw::readfirst(threadIdx.x >> 6);
-    const uint32_t l = vw::lane_id();
-    const uint64_t row0 = row_lo + ((uint64_t)blockIdx.x * K1_WAVES + wave) * GEN_ROWS;
-    const bool flagged = l < GEN_ROWS && row0 + l < row_hi && a.rec_size[row0 + l] == VCFCD_RETRY;
-    uint64_t todo = vw::ballot(flagged);
-    while (todo) {
-        const uint64_t row = row0 + (uint64_t)__builtin_ctzll(todo);
-        todo &= todo - 1;
-        VCFC_DIAG_GENERAL_ROW(a);
-        Ring r;
-        if (!row_setup(a, row, lds + wave * RING_STRIDE, r)) continue;
-        uint32_t bytes = 0;
-        const uint32_t st = encode_general(a.buf + a.line_off[row], a.line_len[row], r, &bytes);
-        if (l == 0) {
-            a.rec_size[row] = st == VCFCD_OK ? bytes : 0u;
-            if (st != VCFCD_OK) atomicMin((unsigned long long *)a.err, (unsigned long long)((row << 8) | st));
-        }
     }
 }
 
@@ -1617,7 +1588,10 @@ __device__ bool row_has_nl(const uint8_t *__restrict__ line, uint32_t len) {
 constexpr uint32_t VAR_ROWS = 32;
 // Variable-token kernel: the rows the fast kernel flagged, VAR_ROWS per wave
 // (a flag load per 32 rows, so a batch without such rows costs next to
-// nothing); rows of another shape stay flagged for k_encode_general.
+// nothing); a row of another shape takes the general path in the same wave
+// (round 2 ran it as a kernel of its own, k_encode_general: one more launch,
+// ~4.5 us on the headline rows, which flag none).  A resident grid striding
+// over rows was 13.6 % slower on law 2 (profiles/r02/ab/ab_gen_persist.txt).
 __global__ __launch_bounds__(256) void k_encode_var(VcfcEncodeArgs a, uint64_t row_lo, uint64_t row_hi) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[K1_WAVES * RING_STRIDE];
     const uint32_t wave = vw::readfirst(threadIdx.x >> 6);
@@ -1638,13 +1612,23 @@ __global__ __launch_bounds__(256) void k_encode_var(VcfcEncodeArgs a, uint64_t r
             continue;
         }
         uint32_t bytes = 0;
-        const bool ok = encode_var(a.buf + a.line_off[row], a.line_len[row], r, &bytes);
-        if (l == 0 && ok) a.rec_size[row] = bytes;
+        if (encode_var(a.buf + a.line_off[row], a.line_len[row], r, &bytes)) {
+            if (l == 0) a.rec_size[row] = bytes;
+            continue;
+        }
+        // not the variable-token shape: the general path, in this wave
+        VCFC_DIAG_GENERAL_ROW(a);
+        row_setup(a, row, lds + wave * RING_STRIDE, r);   // (the ring again; the slot fits, checked above)
+        const uint32_t st = encode_general(a.buf + a.line_off[row], a.line_len[row], r, &bytes);
+        if (l == 0) {
+            a.rec_size[row] = st == VCFCD_OK ? bytes : 0u;
+            if (st != VCFCD_OK) atomicMin((unsigned long long *)a.err, (unsigned long long)((row << 8) | st));
+        }
     }
 }
 
-// blocks of k_encode_general to launch for m rows
-static uint64_t general_blocks(uint64_t m, uint32_t rows_per_wave = GEN_ROWS) {
+// blocks of k_encode_var to launch for m rows
+static uint64_t var_blocks(uint64_t m, uint32_t rows_per_wave = VAR_ROWS) {
     const uint64_t per_block = (uint64_t)K1_WAVES * rows_per_wave;
     return (m + per_block - 1) / per_block;
 }
@@ -1987,11 +1971,7 @@ hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t s, hipEvent_t
     hipLaunchKernelGGL(k_encode_fast, dim3((unsigned)((a.n + K1_WAVES - 1) / K1_WAVES)), dim3(64 * K1_WAVES), 0, s, a,
                        (uint64_t)0, a.n);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_encode_var, dim3((unsigned)general_blocks(a.n, VAR_ROWS)), dim3(64 * K1_WAVES), 0, s, a,
-                       (uint64_t)0, a.n);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_encode_general, dim3((unsigned)general_blocks(a.n)), dim3(64 * K1_WAVES), 0, s, a,
-                       (uint64_t)0, a.n);
+    hipLaunchKernelGGL(k_encode_var, dim3((unsigned)var_blocks(a.n)), dim3(64 * K1_WAVES), 0, s, a, (uint64_t)0, a.n);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[2], s);
     hipLaunchKernelGGL((k_scan_lb<0, true>), dim3((unsigned)nt), dim3(SCAN_THREADS), 0, s, a.rec_size, a.n,
