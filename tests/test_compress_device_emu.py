@@ -12,6 +12,7 @@ import pytest
 import emu_io as E
 import golden_io as G
 import test_ingest_emu as T
+from hop_cases import chr22_like, hop_trap_file
 
 OK, E_ARG = 0, 5
 
@@ -109,56 +110,6 @@ def test_short_lines_overflow_the_segment_slot():
         check(vcf, chunk, "short lines")
 
 
-PREFIX = b"1\t%d\trs\tA\tC\t50\tPASS\tAC=1\tGT\t"
-
-
-def hop_trap_file(kind, rnd, S_A=300, S_B=45):
-    """Lines on which the hop line index (vcfc_line_index with the header's
-    sample count S) guesses a data line's end wrongly: row A (longer than the
-    index's 1 KiB first window, which finds shorter lines exactly) has fewer
-    samples than the header, and the byte where A would end with S 3-byte
-    tokens is the '\\n' of a later line B with TABs at the 31 places 4, 8, ...
-    before it.  The hop index then counts A..B as one line; the encoder must
-    see the '\\n' inside it and the chunk is indexed again from every byte.
-      tab:    A ends in a full token: its '\\n' sits where a TAB would
-      escape: A ends in "0|" and B starts with TAB and 3-byte fields, so the
-              merged row is 3-byte tokens throughout, one of them "0|\\n"
-              (the fast kernel's escape path must refuse it)
-      var:    A mixes 1-byte tokens (the variable-token kernel's scan)
-      lines:  '#' and empty lines between A and B"""
-    toks = lambda k: [rnd.choice([b"0|0", b"0|1", b"1|1", b"0|2"]) for _ in range(k)]
-    pre = PREFIX % 7
-    if kind == "escape":
-        a = pre + b"\t".join(toks(S_A - 1) + [b"0|"])
-        b = b"\t" + b"\t".join([b"abc"] * 8) + b"\t" + b"\t".join(toks(S_B))
-        S = S_A + 8 + S_B                     # |B| = 4 (S - S_A)
-        mid = []
-    else:
-        if kind == "var":
-            at = toks(S_A)
-            for i in rnd.sample(range(S_A), 6):
-                at[i] = b"1"
-            at[0] = b"0"; at[1] = b"1|0"      # 6 x 1-byte: 12 bytes shorter
-        else:
-            at = toks(S_A)
-        a = pre + b"\t".join(at)
-        mid = [b"##between", b""] if kind == "lines" else []
-        # B ends where A's guess does: len(A) + 1 + sum(mid + 1) + len(B) = len(pre) + 4 S - 1
-        gap = sum(len(m) + 1 for m in mid)
-        S = S_A + 60
-        blen = len(pre) + 4 * S - 1 - len(a) - 1 - gap
-        pb = PREFIX % 8
-        nb = (blen - len(pb) + 1) // 4
-        pad = blen - (len(pb) + 4 * nb - 1)
-        pb = pb.replace(b"rs", b"rs" + b"x" * pad)
-        b = pb + b"\t".join(toks(nb))
-        assert len(b) == blen and nb >= 32
-    hdr = T.D.header(S)
-    rows = [PREFIX % (100 + i) + b"\t".join(toks(S)) for i in range(5)]
-    body = rows[:3] + [a] + mid + [b] + rows[3:]
-    return hdr + b"\n".join(body) + b"\n"
-
-
 @pytest.mark.parametrize("kind", ["tab", "escape", "var", "lines"])
 def test_hop_index_wrong_guess_is_caught(kind):
     rnd = random.Random(kind)
@@ -170,23 +121,6 @@ def test_hop_index_wrong_guess_is_caught(kind):
     st2, out2, _ = E.emu_compress_device(vcf, chunk=1 << 16, hop=False, redo=redo)
     assert st == st2 == OK and out == out2
     assert redo == [1, 0]   # the guess went wrong once, and was caught
-
-
-def chr22_like(rnd, n_rows, S, prefix_jitter=40):
-    """Rows of S 3-byte tokens behind prefixes whose lengths vary by up to
-    prefix_jitter bytes (the hop index guesses each end from the previous
-    row's prefix length), some '##' lines and an empty line among them."""
-    lines = T.D.header(S).rstrip(b"\n").split(b"\n")
-    for i in range(n_rows):
-        info = b"AC=%d;AF=0.%d;NS=%s" % (rnd.randrange(100), rnd.randrange(10 ** 6), b"9" * rnd.randrange(prefix_jitter))
-        toks = [rnd.choice([b"0|0", b"0|0", b"0|1", b"1|0", b"1|1", b"0|2"]) for _ in range(S)]
-        lines.append(b"\t".join([b"22", b"%d" % (16050000 + 37 * i), b"rs%d" % rnd.randrange(10 ** 8), b"A", b"G",
-                                 b"100", b"PASS", info, b"GT"] + toks))
-        if i % 17 == 5:
-            lines.append(b"##mid=%d" % i)
-        if i == 11:
-            lines.append(b"")
-    return b"\n".join(lines) + b"\n"
 
 
 @pytest.mark.parametrize("S,jitter", [(300, 40), (700, 300), (64, 5)])

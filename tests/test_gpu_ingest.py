@@ -177,3 +177,29 @@ def test_300mib_chr22_file_multi_chunk(torch, vcfc, ctx):
     pick = np.random.default_rng(1).integers(0, n, 40)
     for i, ln in zip(pick, rows.host_lines(pick)):
         assert recs[int(rec[i]):int(rec[i + 1])] == G.oracle_encode_line(ln)[1], i
+
+
+@pytest.mark.parametrize("kind", ["tab", "escape", "var", "lines"])
+def test_hop_index_wrong_guess_on_gpu(ctx, kind):
+    """The hop line index's traps (tests/hop_cases.py: a row shorter than the
+    header's sample count whose guessed end is a later row's '\\n') on the
+    GPU: the encoder's '\\n' check sends the chunk back to the full scan, and
+    the output is the oracle's -- whole file and 4 KiB chunks (every path of
+    both_paths)."""
+    from hop_cases import hop_trap_file
+    data = hop_trap_file(kind, random.Random(kind))
+    st_o, want, _ = G.oracle_compress(data)
+    assert st_o == 0
+    assert both_paths(ctx, data, 1 << 20) == (0, want, -1)
+    assert both_paths(ctx, data, 4096) == (0, want, -1)
+
+
+def test_hop_index_chr22_like_on_gpu(ctx):
+    """chr22-shaped rows whose prefix lengths jump by up to 300 bytes (guess
+    windows that miss and the VERIFY round), '##' and empty lines between
+    them: device path equals the oracle."""
+    from hop_cases import chr22_like
+    for S, jitter in ((300, 40), (700, 300), (64, 5)):
+        data = chr22_like(random.Random(S), 150, S, jitter)
+        st_o, want, _ = G.oracle_compress(data)
+        assert st_o == 0 and both_paths(ctx, data, 1 << 20) == (0, want, -1), S
