@@ -315,7 +315,7 @@ def test_variable_token_rows(seed):
     bytes) -- haploid beside diploid, '.', GT:DP:GQ, all-1-byte rows, long
     0|0 runs broken by 1-byte escapes -- byte-exact against the oracle at
     every alignment of the buffer; only rows mixing tokens longer than 3
-    bytes with 3-byte ones may be left to k_encode_general."""
+    bytes with 3-byte ones may be left to the general path."""
     rnd = random.Random(seed)
     lines = _var_rows(rnd, 72, ["hap", "dot", "long", "ones", "runs", "gdg"])
     want = [G.oracle_encode_line(x) for x in lines]
@@ -326,14 +326,14 @@ def test_variable_token_rows(seed):
         for i, (_, rec) in enumerate(want):
             assert out[int(ro[i]):int(ro[i + 1])] == rec, (seed, lead, i)
         # only rows with a token longer than 3 bytes may go on to
-        # k_encode_general (those mixing them with 3-byte tokens)
+        # the general path (those mixing them with 3-byte tokens)
         longer = sum(1 for x in lines if max(len(t) for t in x[len(PFX_V):].split(b"\t")) > 3)
         assert E.LAST_RETRIES[0] <= longer, (E.LAST_RETRIES[0], longer)
 
 
 def test_variable_token_rows_fall_back():
     """Rows the variable-token kernel must hand on (even-length tokens, empty
-    fields, a trailing TAB, CR) are encoded by k_encode_general, and the
+    fields, a trailing TAB, CR) are encoded by the general path, and the
     others of the batch stay exact."""
     rnd = random.Random(77)
     good = _var_rows(rnd, 8, ["hap", "long"])
@@ -352,7 +352,7 @@ def test_variable_token_rows_fall_back():
 def test_law2_synthetic_rows():
     """The synthetic law-2 rows (bench.py --law 2; kinds haploid, GT:DP:GQ,
     missing, unphased, '.'): byte-exact, and none of them reaches
-    k_encode_general (GT:DP:GQ rows take the variable-token kernel's escape
+    the general path (GT:DP:GQ rows take the variable-token kernel's escape
     chunks)."""
     rows = E.emu_synth_rows(40, 700, 2, seed=9)
     buf, lo, ll = rows

@@ -1,5 +1,5 @@
-"""Per-launch HBM bytes of the encoder (k_encode_fast + k_encode_var +
-k_encode_general) from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE;
+"""Per-launch HBM bytes of the encoder (k_encode_fast + k_encode_var; the
+round-2 k_encode_general counted where present) from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE;
 separate runs, MI355X_MICROARCH.md's recipe), written as the summary
 bench.py's roofline.traffic reads (profiles/pmc_k_encode*.json).  Usage:
   python tools/pmc_encode_json.py <fetch_dir> <write_dir> <workload key> <out.json> <source note>"""
@@ -28,7 +28,7 @@ def main():
         fb, wb = int(f.get(k, 0) * 1024 * 2), int(w.get(k, 0) * 1024)
         kern[k] = {"fetch_bytes": fb, "write_bytes": wb, "hbm_bytes": fb + wb}
     enc = [k for k in KERNELS if k != "k_compact_out"]
-    res = {"workload": key, "kernel": "k_encode (k_encode_fast + k_encode_var + k_encode_general)", "source": note,
+    res = {"workload": key, "kernel": "k_encode (k_encode_fast + k_encode_var)", "source": note,
            "fetch_bytes_per_launch": sum(kern[k]["fetch_bytes"] for k in enc),
            "write_bytes_per_launch": sum(kern[k]["write_bytes"] for k in enc),
            "hbm_bytes_per_launch": sum(kern[k]["hbm_bytes"] for k in enc),
