@@ -63,6 +63,7 @@ for s in $STEPS; do
          python3 tools/pmc_encode_json.py "$O/pmcenc_l2_FETCH_SIZE" "$O/pmcenc_l2_WRITE_SIZE" "general-shapes (chrX haploid/GT:DP:GQ/missing)/2504x1000000" "$O/pmc_k_encode_law2.json" "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes (tools/gpu_check.sh pmcenc, run $TAG)" > /dev/null || { echo "pmc json failed"; exit 1; } ;;
     benchdev) timeout -k 10 300 python bench.py --mode devfile > "$O/bench_devfile.json" 2> "$O/bench_devfile.err" || { echo "benchdev failed"; tail -30 "$O/bench_devfile.err"; exit 1; } ; cat "$O/bench_devfile.json" ;;
     profdev) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/profdev" -o run -- python3 "$R/bench.py" --mode devfile --steps 5 --warmup 1 > "$O/profdev.log" 2>&1) || { echo "profdev failed rc=$?"; tail -30 "$O/profdev.log"; exit 1; } ;;
+    rehearse2) VCFC_BENCH_REHEARSAL=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29623 bench.py --gpus 2 --steps 5 --warmup 1 --no-cpu-baseline > "$O/bench_n2_rehearsal.json" 2> "$O/bench_n2_rehearsal.err" || { echo "rehearse2 failed"; tail -30 "$O/bench_n2_rehearsal.err"; exit 1; } ; cat "$O/bench_n2_rehearsal.json" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
