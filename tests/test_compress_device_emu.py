@@ -144,3 +144,19 @@ def test_hop_index_trap_counts_fewer_lines(kind):
     hop, scan = E.emu_line_index(vcf, S), E.emu_line_index(vcf, 0)
     # A..B counted as one data line ('#' and empty lines between them swallowed)
     assert hop[0][0] < scan[0][0] and hop[0][1] == scan[0][1] - 1
+
+
+def test_hop_index_long_header():
+    """A header longer than the first 64 KiB read (the sample count comes
+    from a second, 1 MiB read) and one with an empty line before #CHROM: the
+    hop index is still used (the trap is hit and caught: one re-index)."""
+    rnd = random.Random(77)
+    trap = hop_trap_file("tab", rnd)
+    meta = b"".join(b"##contig=<ID=chr%d,length=%d>\n" % (i, 10 ** 8 + i) for i in range(3000))
+    assert len(meta) > 64 << 10
+    for vcf in (meta + trap, b"##fileformat=VCFv4.2\n\n" + trap.split(b"\n", 1)[1]):
+        redo = []
+        st, out, _ = E.emu_compress_device(vcf, chunk=1 << 20, redo=redo)
+        st_o, want, _ = G.oracle_compress(vcf)
+        assert st == st_o == OK and out == want
+        assert redo == [1]

@@ -166,20 +166,26 @@ inline bool header_ok(const uint8_t *p, uint64_t len) {
 
 // Samples of the "#CHROM" line held whole in p[0, len) (TABs - 8), 0 if none:
 // only a guess for the hop line index, never trusted for the output.
-inline uint32_t header_samples(const uint8_t *p, uint64_t len) {
+// *more: the window ended inside the header (a longer one may hold it).
+inline uint32_t header_samples(const uint8_t *p, uint64_t len, bool *more = nullptr) {
     static const char key[] = "#CHROM\t";
-    for (uint64_t q = 0; q + 7 <= len;) {
+    if (more) *more = false;
+    for (uint64_t q = 0; q < len;) {
         const uint8_t *e = static_cast<const uint8_t *>(memchr(p + q, '\n', len - q));
-        if (!e) return 0;
+        if (!e) {
+            if (more) *more = p[q] == '#';
+            return 0;
+        }
         const uint64_t end = (uint64_t)(e - p);
         if (end - q >= 7 && memcmp(p + q, key, 7) == 0) {
             uint64_t tabs = 0;
             for (uint64_t k = q; k < end; k++) tabs += p[k] == '\t';
             return tabs >= 9 && tabs - 8 < (1u << 24) ? (uint32_t)(tabs - 8) : 0u;
         }
-        if (p[q] != '#') return 0;   // the header ended
+        if (end > q && p[q] != '#') return 0;   // the header ended (empty lines are skipped)
         q = end + 1;
     }
+    if (more) *more = len > 0;   // the window ended at a line end inside the header
     return 0;
 }
 
@@ -624,9 +630,17 @@ inline int compress_device(const uint8_t *d_in, uint64_t N, uint8_t *d_out, uint
     {
         const char *hv = getenv("VCFC_HOP");
         if (cfg.hop_index && !(hv && hv[0] == '0')) {
-            std::vector<uint8_t> h(std::min<uint64_t>(N, 1u << 20));
-            if (!d2h(h.data(), d_in, h.size()) || !sync()) return ST_E_HIP;
-            S_hint = header_samples(h.data(), h.size());
+            // 64 KiB of the file into pinned memory, 1 MiB if the header is longer
+            for (uint64_t want = std::min<uint64_t>(N, 64u << 10);;) {
+                uint8_t *h = static_cast<uint8_t *>(M.host(Memory::H_IN0, want));
+                if (!h) return ST_E_HIP;
+                if (!d2h(h, d_in, want) || !sync()) return ST_E_HIP;
+                bool more = false;
+                S_hint = header_samples(h, want, &more);
+                const uint64_t cap = std::min<uint64_t>(N, 1u << 20);
+                if (!more || want >= cap) break;
+                want = cap;
+            }
             if (S_hint < 32) S_hint = 0;   // (the check reads 32 tokens)
         }
         if (trace) fprintf(stderr, "compress_device: S_hint=%u\n", S_hint);
