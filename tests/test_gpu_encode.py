@@ -229,3 +229,36 @@ def test_variable_token_rows(ctx, seed):
     st, want, _ = G.oracle_compress(data)
     assert st == 0
     assert ctx.compress_buffer(data) == want
+
+
+def test_encode_captured_in_hip_graph(torch, vcfc):
+    """vcfc_encode_rows_device enqueues its whole pipeline (memsets, the two
+    look-back scans, k_encode_fast, k_encode_var, k_compact_out) with no host
+    synchronisation, so it can be captured in a HIP graph: the replayed graph
+    writes the same records, offsets and status as an eager call, replay after
+    replay (the workspace state is re-zeroed by the captured memsets)."""
+    import workload
+    rows = workload.DeviceRows(torch, vcfc, 2000, 2504, 0, seed=41, device="cuda:0")
+    n = rows.n
+    want_out, want_rec, want_err = _device_encode(torch, vcfc, rows)
+    ws_bytes = vcfc.workspace_size(n, rows.line_bytes)
+    cap = vcfc.encode_bound(n, rows.line_bytes)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device="cuda:0")
+    out = torch.zeros(cap, dtype=torch.uint8, device="cuda:0")
+    rec = torch.zeros(n + 1, dtype=torch.int64, device="cuda:0")
+    err = torch.zeros(1, dtype=torch.int64, device="cuda:0")
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        vcfc.encode_rows_device(rows.buf.data_ptr(), rows.line_off.data_ptr(), rows.line_len.data_ptr(), n,
+                                rows.line_bytes, out.data_ptr(), cap, rec.data_ptr(), ws.data_ptr(), ws_bytes,
+                                err.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    for _ in range(3):
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert int(err.cpu().numpy().view(np.uint64)[0]) == want_err == vcfc.NO_ERROR
+        r = rec.cpu().numpy().astype(np.uint64)
+        assert np.array_equal(r, want_rec)
+        k = int(r[n])
+        assert torch.equal(out[:k], want_out[:k])
