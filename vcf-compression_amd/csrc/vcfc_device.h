@@ -16,7 +16,7 @@
 
 // error word: min over failing rows of (row << 8 | code); ~0 = no error
 #define VCFCD_NO_ERROR (~0ull)
-// rec_size value of a row the fast kernel leaves to the general kernel
+// rec_size value of a row the fast kernel leaves to k_encode_var
 #define VCFCD_RETRY 0xFFFFFFFFu
 
 // Alignment: buf, the lines in it and out may start at any byte.  The
@@ -44,7 +44,7 @@ struct VcfcEncodeArgs {
     uint32_t *rec_size;        // n
     uint64_t *partials;        // scan partials
     uint64_t *err;             // 1 word
-    uint32_t *retry_count;     // rows that took the general kernel (emulator builds only, diag hooks)
+    uint32_t *retry_count;     // rows that took the general path (emulator builds only, diag hooks)
     uint8_t *lb;               // look-back scan state (tickets, tile flags; zeroed per encode)
     uint32_t *tile_first;      // per 4 KiB output tile: the row holding its first byte (compaction)
     uint8_t *prim;             // per-row primary staging: record bytes [0, VCFC_PRIM) at prim + VCFC_PRIM * row

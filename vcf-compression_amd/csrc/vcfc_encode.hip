@@ -1553,8 +1553,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 6))) voi
     const bool ok = encode_fast(a.buf + a.line_off[row], a.line_len[row], r, &bytes);
     VCFC_DIAG_ROW_END(a, row);
     if (vw::lane_id() == 0) {
-        // not the fast shape: the general kernel's wave for this row takes
-        // it (a flag per row, no shared queue: 750k rows appending to one
+        // not the fast shape: k_encode_var's wave for this row takes it
+        // (a flag per row, no shared queue: 750k rows appending to one
         // counter serialise at the memory side, ~8 ms on the law-2 rows)
         a.rec_size[row] = ok ? bytes : VCFCD_RETRY;
     }

@@ -15,6 +15,8 @@
 //                 '\n' count, and the first NL_SLOT positions in order into
 //                 the segment's slot (per-lane masks, a wave prefix sum of
 //                 their popcounts)
+//   k_nl_hop      (instead, when the header gives the sample count: line ends
+//                 guessed and checked, ~0.5 KiB read per line; see below)
 //   scan          segment bases (the encoder's exclusive scan)
 //   k_nl_place    one lane per segment: its positions from the slot to their
 //                 place; a segment with more than NL_SLOT lines (average
