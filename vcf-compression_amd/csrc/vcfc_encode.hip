@@ -1927,6 +1927,17 @@ __global__ __launch_bounds__(256) void k_scan_lb(const uint32_t *__restrict__ in
     }
 }
 
+// Per-call state of one encode: the look-back tickets and tile flags zeroed,
+// the first-error word set to "none".  A kernel rather than two
+// hipMemsetAsync calls: replays of a HIP graph captured around
+// vcfc_encode_device did not re-run the captured memsets (the second replay
+// found the previous replay's tickets and its look-back spun; tools/dbg/
+// graph_probe.py), and a kernel node is replayed like every other launch.
+__global__ __launch_bounds__(256) void k_encode_reset(uint64_t *lb, uint64_t words, uint64_t *err) {
+    for (uint64_t i = threadIdx.x; i < words; i += 256) lb[i] = 0;
+    if (threadIdx.x == 0) *err = ~0ull;
+}
+
 }  // namespace
 
 VcfcWorkspaceLayout vcfc_encode_workspace_layout(uint64_t n, uint64_t total_line_bytes) {
@@ -1954,15 +1965,19 @@ VcfcWorkspaceLayout vcfc_encode_workspace_layout(uint64_t n, uint64_t total_line
 }
 
 hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t s, hipEvent_t *ev) {
-    hipError_t e = hipMemsetAsync(a.err, 0xFF, 8, s);
-    if (e != hipSuccess) return e;
-    if (a.n == 0) return hipMemsetAsync(a.rec_off, 0, 8, s);
+    hipError_t e;
+    if (a.n == 0) {
+        if ((e = hipMemsetAsync(a.err, 0xFF, 8, s)) != hipSuccess) return e;
+        return hipMemsetAsync(a.rec_off, 0, 8, s);
+    }
     const uint64_t nt = (a.n + SCAN_TILE - 1) / SCAN_TILE;   // scan tiles
     // lb: tickets (slot scan, size scan), retry counter, slot-scan flags
     // (nt + 1), size-scan flags (nt + 1)
     uint32_t *tickets = reinterpret_cast<uint32_t *>(a.lb);
     uint64_t *flags_a = reinterpret_cast<uint64_t *>(a.lb + 16), *flags_b = flags_a + nt + 1;
-    if ((e = hipMemsetAsync(a.lb, 0, 16 + 16 * (nt + 1), s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_encode_reset, dim3(1), dim3(256), 0, s, reinterpret_cast<uint64_t *>(a.lb),
+                       (uint64_t)(2 + 2 * (nt + 1)), a.err);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[0], s);
     hipLaunchKernelGGL((k_scan_lb<1, false>), dim3((unsigned)nt), dim3(SCAN_THREADS), 0, s, a.line_len, a.n, tickets,
                        flags_a, a.slot_off, nullptr, 0, nullptr);
