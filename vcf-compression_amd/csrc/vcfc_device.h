@@ -47,8 +47,9 @@ struct VcfcEncodeArgs {
     uint32_t *retry_count;     // rows that took the general path (emulator builds only, diag hooks)
     uint8_t *lb;               // look-back scan state (tickets, tile flags; zeroed per encode)
     uint32_t *tile_first;      // per 4 KiB output tile: the row holding its first byte (compaction)
-    uint8_t *prim;             // per-row primary staging: record bytes [0, VCFC_PRIM) at prim + VCFC_PRIM * row
-    uint8_t *slots;            // per-row overflow slots: record bytes [VCFC_PRIM, ...) at slots + slot_off[row]
+    uint8_t *prim;             // per-row primary staging: record bytes [0, prim_bytes) at prim + prim_bytes * row
+    uint8_t *slots;            // per-row overflow slots: record bytes [prim_bytes, ...) at slots + slot_off[row]
+    uint32_t prim_bytes;       // vcfc_prim_bytes of the workspace layout
     uint64_t slots_cap;
     uint64_t *dbg;             // diagnostic builds only (tools/diag hooks); else null
     // rows from the hop line index: a row holding a '\n' fails with
@@ -57,14 +58,22 @@ struct VcfcEncodeArgs {
     uint32_t nl_check = 0;
 };
 
-// Record staging: the first VCFC_PRIM bytes of every record go to a dense
+// Record staging: the first prim_bytes bytes of every record go to a dense
 // per-row array (the compaction then reads most records from consecutive
 // kilobytes), the rest (records of rare escape-heavy rows) to a per-row
-// overflow slot sized for the worst case.
-#define VCFC_PRIM 1024u
+// overflow slot sized for the worst case.  2 KiB for batches of long lines
+// (mean >= 4 KiB: records of 1-2 KiB, e.g. the random_vcf law's ~1.15 KB at
+// 2504 samples, stay in one region; k_compact -14 % on law 0 and -9 % on
+// law 1 in an A/B, 4 KiB slower again, profiles/r03/ab/ab_prim*.txt), else
+// 1 KiB (the region costs prim_bytes per row whatever the line length).
+// A multiple of the 1 KiB flush burst, so no burst straddles the regions.
+__host__ __device__ inline uint32_t vcfc_prim_bytes(uint64_t n, uint64_t total_line_bytes) {
+    return n && total_line_bytes / n >= 4096 ? 2048u : 1024u;
+}
 
 struct VcfcWorkspaceLayout {
     uint64_t slot_off, rec_size, partials, err, lb, lb_bytes, retry_count, tile_first, prim, slots, dbg, total;
+    uint32_t prim_bytes;
 };
 
 // Bytes of per-row staging for a line of `len` bytes: covers the worst-case
@@ -91,6 +100,7 @@ inline void vcfc_encode_args_workspace(VcfcEncodeArgs &a, uint8_t *ws, const Vcf
     a.lb = ws + L.lb;
     a.tile_first = reinterpret_cast<uint32_t *>(ws + L.tile_first);
     a.prim = ws + L.prim;
+    a.prim_bytes = L.prim_bytes;
     a.slots = ws + L.slots;
     a.slots_cap = L.dbg - L.slots;
     a.dbg = L.dbg < L.total ? reinterpret_cast<uint64_t *>(ws + L.dbg) : nullptr;

@@ -87,14 +87,15 @@ __device__ __forceinline__ uint32_t umin32(uint32_t a, uint32_t b) { return a < 
 
 // ---------------------------------------------------------------------------
 // LDS ring: record bytes [fpos, wpos) are pending.  Global staging: record
-// bytes [0, VCFC_PRIM) at prim, the rest at slot (see vcfc_device.h).
+// bytes [0, pb) at prim, the rest at slot (see vcfc_device.h; pb is a
+// multiple of BURST, so a burst lies wholly in one region).
 struct Ring {
     uint8_t *lds;
     uint8_t *prim;
     uint8_t *slot;
     uint32_t wpos, fpos;
+    uint32_t pb;   // prim_bytes
 };
-static_assert(VCFC_PRIM % 1024 == 0, "bursts must not straddle the staging regions");
 
 __device__ __forceinline__ void ring_put(Ring &r, uint32_t pos, uint32_t b) {
     r.lds[pos & RMASK] = (uint8_t)b;
@@ -113,8 +114,8 @@ __device__ __forceinline__ void ring_put(Ring &r, uint32_t pos, uint32_t b) {
 // 0.68 GB are written amid the 10 GB input stream, so it does not stay
 // resident -- profiles/r03/ab/ab_staging_cache_policy.txt)
 __device__ __forceinline__ void ring_stage(Ring &r, uint32_t f, uint4 v) {
-    if (r.fpos < VCFC_PRIM) vw::gstore16_nt(r.prim, f, v);
-    else vw::gstore16_nt(r.slot, f - VCFC_PRIM, v);
+    if (r.fpos < r.pb) vw::gstore16_nt(r.prim, f, v);
+    else vw::gstore16_nt(r.slot, f - r.pb, v);
 }
 __device__ __forceinline__ void ring_burst(Ring &r, uint32_t l) {
     const uint4 v = *reinterpret_cast<const uint4 *>(r.lds + ((r.fpos + 16u * l) & RMASK));
@@ -1522,7 +1523,8 @@ __device__ uint32_t encode_general(const uint8_t *__restrict__ line, uint32_t le
 // Row prologue shared by both encode kernels: slot bounds check + ring setup.
 __device__ __forceinline__ bool row_setup(const VcfcEncodeArgs &a, uint64_t row, uint8_t *lds, Ring &r) {
     r.lds = lds;
-    r.prim = a.prim + (uint64_t)VCFC_PRIM * row;
+    r.pb = a.prim_bytes;
+    r.prim = a.prim + (uint64_t)a.prim_bytes * row;
     r.slot = a.slots + a.slot_off[row];
     r.wpos = 8;
     r.fpos = 0;
@@ -1657,7 +1659,7 @@ __device__ __forceinline__ uint4 realign16(uint4 lo, uint4 hi, uint32_t sh) {
 // once, by one wave.  A block's bytes come from the record holding its first
 // byte (an unaligned 16-B load from that record's staging), merged with the
 // overflow slot's first bytes where the block crosses record byte
-// VCFC_PRIM, and with the next record's first bytes where it crosses a
+// prim_bytes, and with the next record's first bytes where it crosses a
 // record end (records hold >= 26 bytes, so a block meets at most two).
 // The size scan (k_scan_lb<0, true>) gives each tile the row holding its
 // first byte.  (4 KiB tiles: 2 KiB the same, 8 KiB +45 %, ab_compact_tile.txt;
@@ -1681,7 +1683,7 @@ __global__ __launch_bounds__(256) void k_compact_out(const uint8_t *__restrict__
                                                      const uint64_t *__restrict__ slot_off,
                                                      const uint64_t *__restrict__ rec_off, uint64_t n,
                                                      const uint32_t *__restrict__ tile_first,
-                                                     uint8_t *__restrict__ out, uint64_t out_cap) {
+                                                     uint8_t *__restrict__ out, uint64_t out_cap, uint32_t pb) {
     const uint32_t l = vw::lane_id();
     const uint64_t g = (uint64_t)blockIdx.x * 4 + vw::readfirst(threadIdx.x >> 6);
     const uint64_t G = (uint64_t)gridDim.x * 4;
@@ -1734,12 +1736,12 @@ __global__ __launch_bounds__(256) void k_compact_out(const uint8_t *__restrict__
             if (o >= lim) continue;
             const uint64_t r = r0 + idx[k];
             const uint64_t x = o - st[k];   // offset in the record
-            const uint8_t *prim = prims + (uint64_t)VCFC_PRIM * r;
+            const uint8_t *prim = prims + (uint64_t)pb * r;
             const uint8_t *slot = slots + sl[k];
-            uint4 v = x + 16 <= VCFC_PRIM ? vw::uload16(prim + x) : x >= VCFC_PRIM ? vw::uload16(slot + (x - VCFC_PRIM)) : vw::uload16(prim + x);
-            if (x < VCFC_PRIM && x + 16 > VCFC_PRIM) v = merge16(v, vw::uload16(slot), (uint32_t)(VCFC_PRIM - x));
+            uint4 v = x + 16 <= pb ? vw::uload16(prim + x) : x >= pb ? vw::uload16(slot + (x - pb)) : vw::uload16(prim + x);
+            if (x < pb && x + 16 > pb) v = merge16(v, vw::uload16(slot), (uint32_t)(pb - x));
             if (o + 16 > en[k] && en[k] < lim)   // the next non-empty record starts at en
-                v = merge16(v, vw::uload16(prims + (uint64_t)VCFC_PRIM * (r0 + idx2[k])), (uint32_t)(en[k] - o));
+                v = merge16(v, vw::uload16(prims + (uint64_t)pb * (r0 + idx2[k])), (uint32_t)(en[k] - o));
             if (o + 16 <= lim) {
                 // non-temporal: the records leave the chip (D2H, a file, the
                 // next stage), and the next batch's encode keeps L2 / MALL to
@@ -1956,7 +1958,8 @@ VcfcWorkspaceLayout vcfc_encode_workspace_layout(uint64_t n, uint64_t total_line
     L.lb_bytes = 16 + 16 * nt;
     o = al(o + L.lb_bytes);
     L.tile_first = o; o = al(o + 4 * (vcfc_record_bound(n, total_line_bytes) / CT + 2));
-    L.prim = o; o = al(o + (uint64_t)VCFC_PRIM * n);
+    L.prim_bytes = vcfc_prim_bytes(n, total_line_bytes);
+    L.prim = o; o = al(o + (uint64_t)L.prim_bytes * n);
     L.slots = o; o = al(o + total_line_bytes + total_line_bytes / 2 + 64 * (n + 1));
     L.dbg = o;
     o += VCFC_DIAG_WS_BYTES(n);
@@ -1997,7 +2000,7 @@ hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t s, hipEvent_t
     const uint64_t tiles = vcfc_record_bound(a.n, a.line_bytes_hint) / CT + 1;
     const uint64_t cblocks = tiles < 8192 ? (tiles + 3) / 4 : 2048;
     hipLaunchKernelGGL(k_compact_out, dim3((unsigned)cblocks), dim3(256), 0, s, a.prim, a.slots, a.slot_off,
-                       a.rec_off, a.n, a.tile_first, a.out, a.out_cap);
+                       a.rec_off, a.n, a.tile_first, a.out, a.out_cap, a.prim_bytes);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[4], s);
     return hipSuccess;
