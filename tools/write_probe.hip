@@ -11,6 +11,8 @@
 //   w5  as w4 with 4-B stores (a lane's four dwords one by one)
 //   w6  as w4 from a resident grid: wave g writes lines g, g + G, g + 2G, ...
 //       (G = 4 x blocks; blocks 1024 / 2048 / 4096 / 8192)
+//   w7  as w4 with a block per line: wave w of the block writes the line's
+//       1 KiB pieces w, w + 4, w + 8, ... (4x fewer lines written at once)
 // Build: hipcc --offload-arch=gfx950 -O3 -o build/write_probe tools/write_probe.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -71,16 +73,26 @@ __global__ __launch_bounds__(256) void w_line_persist(uint8_t *buf) {
     }
 }
 
+__global__ __launch_bounds__(256) void w_line_block(uint8_t *buf) {
+    const uint32_t l = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t row = blockIdx.x;
+    const uint64_t o0 = row * LINE + 37, e = o0 + LINE - 64;
+    for (uint64_t o = o0 + 1024 * w + 16 * l; o + 16 <= e; o += 4096) {
+        const v4u v = {0x09307C30u, 0x09307C30u, 0x09307C30u, 0x09307C30u};
+        __builtin_memcpy(buf + o, &v, 16);
+    }
+}
+
 int main() {
     uint8_t *buf;
     CK(hipMalloc(&buf, TOTAL + 64));
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    const char *names[10] = {"w0 grid plain", "w1 grid nt", "w2 line nt", "w3 line plain", "w4 line plain unaligned",
+    const char *names[11] = {"w0 grid plain", "w1 grid nt", "w2 line nt", "w3 line plain", "w4 line plain unaligned",
                              "w5 line plain unaligned dwords", "w6 resident 1024 blocks", "w6 resident 2048 blocks",
-                             "w6 resident 4096 blocks", "w6 resident 8192 blocks"};
-    for (int p = 0; p < 10; p++) {
+                             "w6 resident 4096 blocks", "w6 resident 8192 blocks", "w7 block per line"};
+    for (int p = 0; p < 11; p++) {
         float best = 1e9;
         for (int it = 0; it < 12; it++) {
             CK(hipEventRecord(e0));
@@ -90,7 +102,8 @@ int main() {
             if (p == 3) hipLaunchKernelGGL(w_line<false>, dim3(NLINE / 4), dim3(256), 0, 0, buf);
             if (p == 4) hipLaunchKernelGGL(w_line_u<false>, dim3(NLINE / 4), dim3(256), 0, 0, buf);
             if (p == 5) hipLaunchKernelGGL(w_line_u<true>, dim3(NLINE / 4), dim3(256), 0, 0, buf);
-            if (p >= 6) hipLaunchKernelGGL(w_line_persist, dim3(1024u << (p - 6)), dim3(256), 0, 0, buf);
+            if (p >= 6 && p < 10) hipLaunchKernelGGL(w_line_persist, dim3(1024u << (p - 6)), dim3(256), 0, 0, buf);
+            if (p == 10) hipLaunchKernelGGL(w_line_block, dim3(NLINE), dim3(256), 0, 0, buf);
             CK(hipEventRecord(e1));
             CK(hipEventSynchronize(e1));
             float ms;

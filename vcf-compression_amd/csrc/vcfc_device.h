@@ -62,7 +62,7 @@ struct VcfcEncodeArgs {
 // per-row array (the compaction then reads most records from consecutive
 // kilobytes), the rest (records of rare escape-heavy rows) to a per-row
 // overflow slot sized for the worst case.  2 KiB for batches of long lines
-// (mean >= 4 KiB: records of 1-2 KiB, e.g. the random_vcf law's ~1.15 KB at
+// (mean >= 4 KiB: records of 1-2 KiB, e.g. the random_vcf law's ~1.28 KB at
 // 2504 samples, stay in one region; k_compact -14 % on law 0 and -9 % on
 // law 1 in an A/B, 4 KiB slower again, profiles/r03/ab/ab_prim*.txt), else
 // 1 KiB (the region costs prim_bytes per row whatever the line length).
