@@ -12,6 +12,14 @@
 //   p4  one wave per row, 4 KiB chunks (four 16-B loads per lane, each 1 KiB
 //       contiguous), two in flight
 //   p5  p1 with the look-ahead load issued by lane 63 only
+//   p6  the encoder's dependency chain per row: line_off[row] (scalar load),
+//       then the line's first 1 KiB (prefix phase), a genotype start x9
+//       derived from those bytes, then p5's stream from x9 (three dependent
+//       latencies per row); V dependent VALU per 2 KiB chunk (0 / 96)
+//   p8  line_off[row], then p5's stream from the line start (two latencies:
+//       the prefix read as part of the first chunk); V as p6
+//   p6 V=192 / 288, and p6 at 6 waves per SIMD (26 KB of LDS per block, the
+//       encoder's occupancy) with V = 96 / 192 / 288
 // Build: hipcc --offload-arch=gfx950 -O3 -o build/stream_probe tools/stream_probe.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -110,18 +118,86 @@ __global__ __launch_bounds__(256) void p4(const uint8_t *buf, uint32_t *sink) {
     if (acc == 0x12345678u) sink[0] = acc;
 }
 
+// V dependent VALU on the chunk's words (models the encoder's per-chunk work)
+template <int V>
+__device__ __forceinline__ uint32_t work(uint32_t acc, v4u a, v4u b) {
+    uint32_t x = acc ^ fold(a) ^ fold(b);
+#pragma unroll
+    for (int i = 0; i < V / 2; i++) {
+        x = (x ^ (x << 7)) + (uint32_t)i;
+    }
+    return x;
+}
+
+template <bool PREFIX, int V, bool OCC6 = false>
+__global__ __launch_bounds__(256) void p6(const uint8_t *buf, const uint64_t *line_off, uint32_t *sink) {
+    const uint32_t l = threadIdx.x & 63;
+    if (OCC6) {   // 26 KB of LDS per block: 6 blocks = 6 waves per SIMD
+        __shared__ uint32_t occ[6656];
+        if (sink[1] == 0x12345678u) { occ[threadIdx.x] = l; sink[2] = occ[(threadIdx.x + 1) & 255]; }
+    }
+    const uint32_t yo = l == 63 ? 0u : 0x40000000u;
+    const uint64_t row = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= NROW) return;
+    // (uint32_t) casts: readfirstlane returns int, which would sign-extend
+    // offsets of 2 GiB and more into the upper word (a faulting address)
+    const uint64_t off = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)line_off[row]) |
+                         ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(line_off[row] >> 32)) << 32);
+    const uint8_t *line = buf + off;
+    uint32_t acc = 0, x9 = 0;
+    if (PREFIX) {
+        auto rp = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(line), (short)0, 1024, 0x00020000);
+        const v4u pv = ld16(rp, 16 * l);
+        acc = fold(pv);
+        x9 = ((uint32_t)__builtin_amdgcn_readfirstlane(acc) & 0x7Fu) + 64u;   // data-dependent genotype start
+    }
+    const uint8_t *g = line + x9;
+    const uint32_t glen = (uint32_t)ROW - x9;
+    auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(g), (short)0, (int)glen, 0x00020000);
+    const uint32_t nch = (glen + 2047) / 2048;
+    v4u a0 = ld16(rs, 32 * l), b0 = ld16(rs, 32 * l + 16);
+    uint32_t y0 = ld4(rs, 32 * l + 32 + yo);
+    v4u a1 = ld16(rs, 2048 + 32 * l), b1 = ld16(rs, 2048 + 32 * l + 16);
+    uint32_t y1 = ld4(rs, 2048 + 32 * l + 32 + yo);
+    v4u a2 = ld16(rs, 4096 + 32 * l), b2 = ld16(rs, 4096 + 32 * l + 16);
+    uint32_t y2 = ld4(rs, 4096 + 32 * l + 32 + yo);
+    for (uint32_t c = 0; c < nch; c += 3) {
+        acc = work<V>(acc ^ y0, a0, b0);
+        a0 = ld16(rs, (c + 3) * 2048 + 32 * l); b0 = ld16(rs, (c + 3) * 2048 + 32 * l + 16);
+        y0 = ld4(rs, (c + 3) * 2048 + 32 * l + 32 + yo);
+        acc = work<V>(acc ^ y1, a1, b1);
+        a1 = ld16(rs, (c + 4) * 2048 + 32 * l); b1 = ld16(rs, (c + 4) * 2048 + 32 * l + 16);
+        y1 = ld4(rs, (c + 4) * 2048 + 32 * l + 32 + yo);
+        acc = work<V>(acc ^ y2, a2, b2);
+        a2 = ld16(rs, (c + 5) * 2048 + 32 * l); b2 = ld16(rs, (c + 5) * 2048 + 32 * l + 16);
+        y2 = ld4(rs, (c + 5) * 2048 + 32 * l + 32 + yo);
+        asm volatile("" ::: "memory");
+    }
+    if (acc == 0x12345678u) sink[0] = acc;
+}
+
 int main() {
     const uint64_t bytes = ROW * NROW;
     uint8_t *buf;
     uint32_t *sink;
     CK(hipMalloc(&buf, bytes + 65536));
     CK(hipMalloc(&sink, 64));
+    CK(hipMemset(sink, 0, 64));
     CK(hipMemset(buf, 0x5A, bytes + 65536));
+    uint64_t *line_off;
+    {
+        std::vector<uint64_t> lo(NROW);
+        for (uint64_t i = 0; i < NROW; i++) lo[i] = i * ROW;
+        CK(hipMalloc(&line_off, 8 * NROW));
+        CK(hipMemcpy(line_off, lo.data(), 8 * NROW, hipMemcpyHostToDevice));
+    }
+    const char *pname[15] = {"p0", "p1", "p2", "p3", "p4", "p5", "p6 V=0", "p6 V=96", "p8 V=0", "p8 V=96",
+                             "p6 V=192", "p6 V=288", "p6 occ6 V=96", "p6 occ6 V=192", "p6 occ6 V=288"};
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     const unsigned rowsg = (unsigned)((NROW + 3) / 4);
-    for (int pat = 0; pat < 6; pat++) {
+    for (int pat = 0; pat < 15; pat++) {
         float best = 1e9f, tot = 0;
         for (int rep = 0; rep < 8; rep++) {
             CK(hipEventRecord(e0, 0));
@@ -131,6 +207,15 @@ int main() {
             if (pat == 3) hipLaunchKernelGGL(p3, dim3(rowsg), dim3(256), 0, 0, buf, sink);
             if (pat == 4) hipLaunchKernelGGL(p4, dim3(rowsg), dim3(256), 0, 0, buf, sink);
             if (pat == 5) hipLaunchKernelGGL(p1<2>, dim3(rowsg), dim3(256), 0, 0, buf, sink);
+            if (pat == 6) hipLaunchKernelGGL((p6<true, 0>), dim3(rowsg), dim3(256), 0, 0, buf, line_off, sink);
+            if (pat == 7) hipLaunchKernelGGL((p6<true, 96>), dim3(rowsg), dim3(256), 0, 0, buf, line_off, sink);
+            if (pat == 8) hipLaunchKernelGGL((p6<false, 0>), dim3(rowsg), dim3(256), 0, 0, buf, line_off, sink);
+            if (pat == 9) hipLaunchKernelGGL((p6<false, 96>), dim3(rowsg), dim3(256), 0, 0, buf, line_off, sink);
+            if (pat == 10) hipLaunchKernelGGL((p6<true, 192>), dim3(rowsg), dim3(256), 0, 0, buf, line_off, sink);
+            if (pat == 11) hipLaunchKernelGGL((p6<true, 288>), dim3(rowsg), dim3(256), 0, 0, buf, line_off, sink);
+            if (pat == 12) hipLaunchKernelGGL((p6<true, 96, true>), dim3(rowsg), dim3(256), 0, 0, buf, line_off, sink);
+            if (pat == 13) hipLaunchKernelGGL((p6<true, 192, true>), dim3(rowsg), dim3(256), 0, 0, buf, line_off, sink);
+            if (pat == 14) hipLaunchKernelGGL((p6<true, 288, true>), dim3(rowsg), dim3(256), 0, 0, buf, line_off, sink);
             CK(hipGetLastError());
             CK(hipEventRecord(e1, 0));
             CK(hipEventSynchronize(e1));
@@ -138,7 +223,7 @@ int main() {
             CK(hipEventElapsedTime(&ms, e0, e1));
             if (rep > 0) { best = ms < best ? ms : best; tot += ms; }
         }
-        printf("p%d best %.3f ms (%.0f GB/s), mean %.3f ms\n", pat, best, bytes / (best * 1e-3) / 1e9, tot / 7);
+        printf("%s best %.3f ms (%.0f GB/s), mean %.3f ms\n", pname[pat], best, bytes / (best * 1e-3) / 1e9, tot / 7);
     }
     return 0;
 }
