@@ -74,7 +74,6 @@ inline uint32_t alignbit(uint32_t hi, uint32_t lo, uint32_t s) {
 }
 inline int32_t sext24(int32_t v) { return (int32_t)((uint32_t)v << 8) >> 8; }
 inline int32_t mad24(int32_t a, int32_t b, int32_t x) { return (int32_t)((uint32_t)x + (uint32_t)(sext24(a) * sext24(b))); }
-inline uint32_t mul24(uint32_t a, uint32_t b) { return (uint32_t)((uint64_t)(a & 0xFFFFFFu) * (uint64_t)(b & 0xFFFFFFu)); }
 inline void wave_sync() { emu::collective(emu::OP_WAVESYNC, 0, 0, 0); }
 // lowest set bit index; value unspecified for 0 (v_ffbl_b32: callers must not use it)
 inline uint32_t ffbl(uint32_t x) { return (uint32_t)__builtin_ctz(x); }

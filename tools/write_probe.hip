@@ -13,6 +13,10 @@
 //       (G = 4 x blocks; blocks 1024 / 2048 / 4096 / 8192)
 //   w7  as w4 with a block per line: wave w of the block writes the line's
 //       1 KiB pieces w, w + 4, w + 8, ... (4x fewer lines written at once)
+//   w8  as w3 with every store instruction's 1 KiB aligned to 128 B (the
+//       line's bytes from its first 128-B boundary: no partial 128-B line
+//       inside a line, only at its two ends)
+//   w9  as w3 with 64-B aligned store windows
 // Build: hipcc --offload-arch=gfx950 -O3 -o build/write_probe tools/write_probe.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -83,16 +87,26 @@ __global__ __launch_bounds__(256) void w_line_block(uint8_t *buf) {
     }
 }
 
+template <uint32_t A>
+__global__ __launch_bounds__(256) void w_line_al(uint8_t *buf) {
+    const uint32_t l = threadIdx.x & 63;
+    const uint64_t row = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= NLINE) return;
+    const uint64_t o0 = row * LINE, a0 = (o0 + A - 1) & ~(uint64_t)(A - 1), e = o0 + LINE;
+    const v4u v = {0x09307C30u, 0x09307C30u, 0x09307C30u, 0x09307C30u};
+    for (uint64_t o = a0 + 16 * l; o + 16 <= e; o += 1024) *reinterpret_cast<v4u *>(buf + o) = v;
+}
+
 int main() {
     uint8_t *buf;
     CK(hipMalloc(&buf, TOTAL + 64));
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    const char *names[11] = {"w0 grid plain", "w1 grid nt", "w2 line nt", "w3 line plain", "w4 line plain unaligned",
+    const char *names[13] = {"w0 grid plain", "w1 grid nt", "w2 line nt", "w3 line plain", "w4 line plain unaligned",
                              "w5 line plain unaligned dwords", "w6 resident 1024 blocks", "w6 resident 2048 blocks",
-                             "w6 resident 4096 blocks", "w6 resident 8192 blocks", "w7 block per line"};
-    for (int p = 0; p < 11; p++) {
+                             "w6 resident 4096 blocks", "w6 resident 8192 blocks", "w7 block per line", "w8 line 128-B aligned", "w9 line 64-B aligned"};
+    for (int p = 0; p < 13; p++) {
         float best = 1e9;
         for (int it = 0; it < 12; it++) {
             CK(hipEventRecord(e0));
@@ -104,6 +118,8 @@ int main() {
             if (p == 5) hipLaunchKernelGGL(w_line_u<true>, dim3(NLINE / 4), dim3(256), 0, 0, buf);
             if (p >= 6 && p < 10) hipLaunchKernelGGL(w_line_persist, dim3(1024u << (p - 6)), dim3(256), 0, 0, buf);
             if (p == 10) hipLaunchKernelGGL(w_line_block, dim3(NLINE), dim3(256), 0, 0, buf);
+            if (p == 11) hipLaunchKernelGGL(w_line_al<128>, dim3(NLINE / 4), dim3(256), 0, 0, buf);
+            if (p == 12) hipLaunchKernelGGL(w_line_al<64>, dim3(NLINE / 4), dim3(256), 0, 0, buf);
             CK(hipEventRecord(e1));
             CK(hipEventSynchronize(e1));
             float ms;

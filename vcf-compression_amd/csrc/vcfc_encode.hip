@@ -69,17 +69,11 @@ __device__ __forceinline__ uint32_t cls_mask(uint32_t c) {
 __device__ __forceinline__ uint32_t cls_of(uint32_t k) {
     return k == 0x307C30u ? 0u : k == 0x317C30u ? 1u : k == 0x307C31u ? 2u : k == 0x317C31u ? 3u : CLS_ESC;
 }
-// bits 0, 8 and 16 of x -> bits 0, 1, 2: one 24-bit multiply (full rate;
-// a 32-bit v_mul_lo_u32 issues at quarter rate), products at distinct
-// positions 0/7/14, 8/15/22, 16/23/30, so no carries reach bits 14..16
-__device__ __forceinline__ uint32_t gather3(uint32_t x) {
-    return (vw::mul24(x & 0x00010101u, 0x4081u) >> 14) & 7u;
-}
 // bit i set <=> byte i of w is zero (exact, no false positives)
 __device__ __forceinline__ uint32_t zero_bytes4(uint32_t w) {
     uint32_t t = ((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w | 0x7F7F7F7Fu;
     t = ~t;  // 0x80 in every zero byte
-    return gather3(t >> 7) | (t >> 28);   // (t >> 28: bit 31 -> 8; bits 28-30 are clear)
+    return ((t >> 7) * 0x00204081u >> 21) & 0xFu;
 }
 __device__ __forceinline__ uint32_t tab_mask16(uint4 v) {
     return zero_bytes4(v.x ^ 0x09090909u) | (zero_bytes4(v.y ^ 0x09090909u) << 4) |
@@ -263,7 +257,7 @@ struct FastState {
 // tokens (f.T = its 2-byte half-slots instead of its tokens).
 template <bool VAR>
 __device__ __forceinline__ int fast_prefix_step(const Chunk &cur, uint32_t c, uint32_t lead, uint32_t len,
-                                                FastState &f, Ring &r, bool nlc = false) {
+                                                FastState &f, Ring &r) {
     const uint32_t l = vw::lane_id();
     const uint32_t bo = c * CHUNK + BPL * l;
     const int32_t x0 = (int32_t)bo - (int32_t)lead;   // line offset of the lane's byte 0
@@ -303,18 +297,11 @@ __device__ __forceinline__ int fast_prefix_step(const Chunk &cur, uint32_t c, ui
         const int32_t d = (int32_t)x9 - x0;
         below = d <= 0 ? 0u : d >= (int32_t)BPL ? ~0u : ((1u << d) - 1u);
     }
-    // a '\n' in the row's prefix bytes (the hop line index's guess went
-    // wrong, VcfcEncodeArgs::nl_check; nlc): not the fast shape.  Only
-    // there: a '\n' among the genotype bytes fails the chunk shapes, the
-    // variable-token kernel runs row_has_nl itself, and rows from any other
-    // line index are lines, whose '\n' bytes (if a caller passes one) are
-    // field bytes like any other, as in compress_data_line.  (Skipping the
-    // test on the other paths: ~30 VALU per row.)
+    // a '\n' in the row (the hop line index's guess went wrong, see
+    // VcfcEncodeArgs::nl_check): not the fast shape
     uint32_t lf = 0;
-    if (!VAR && nlc) {
 #pragma unroll
-        for (int k = 0; k < (int)TPL; k++) lf |= zero_bytes4(cur.w(k) ^ 0x0A0A0A0Au) << (4 * k);
-    }
+    for (int k = 0; k < (int)TPL; k++) lf |= zero_bytes4(cur.w(k) ^ 0x0A0A0A0Au) << (4 * k);
     // the fast shape: in this chunk's genotype bytes the TABs sit exactly at
     // x9 + 4k + 3 -- rows of other token lengths (haploid "0", GT:DP:GQ, '.')
     // leave here, before the genotype phase puts 6 KiB of loads in flight
@@ -838,7 +825,7 @@ __device__ __forceinline__ bool gt_step8(const Chunk8 &cur, uint32_t C, FastStat
     return false;   // tokens of another length or empty fields: the caller runs gt_general on this chunk
 }
 
-__device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring &r, uint32_t *rec_bytes, bool nlc) {
+__device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring &r, uint32_t *rec_bytes) {
     const uint32_t l = vw::lane_id();
     const uint32_t lead = (uint32_t)(reinterpret_cast<uintptr_t>(line) & 15);
     const uint8_t *A = line - lead;
@@ -858,7 +845,7 @@ __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring
     Chunk b = load_chunk(rsA, 0, lo16);
     int st;
     for (;;) {
-        st = (int)vw::readfirst((uint32_t)fast_prefix_step<false>(look_ahead(b), c, lead, len, f, r, nlc));
+        st = (int)vw::readfirst((uint32_t)fast_prefix_step<false>(look_ahead(b), c, lead, len, f, r));
         if (st != 0) break;
         c = vw::readfirst(c + 1);
         if (c >= nch) return false;   // < 10 fields
@@ -1089,7 +1076,7 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
     // byte after each half, i.e. the next half's first; bit 0 of the bytes
     // of A / B gathered by one multiply)
     uint32_t p3 = 0, am = 0, bm = 0;
-    auto bits0 = [](uint32_t x) { return gather3(x) | ((x >> 21) & 8u); };
+    auto bits0 = [](uint32_t x) { return (((x & 0x01010101u) * 0x01020408u) >> 24) & 0xFu; };
     uint32_t An = vw::perm(d[1], d[0], 0x06040200u);
 #pragma unroll
     for (int k = 0; k < 4; k++) {
@@ -1565,7 +1552,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 6))) voi
     Ring r;
     if (!row_setup(a, row, lds + wave * RING_STRIDE, r)) return;
     uint32_t bytes = 0;
-    const bool ok = encode_fast(a.buf + a.line_off[row], a.line_len[row], r, &bytes, a.nl_check != 0);
+    const bool ok = encode_fast(a.buf + a.line_off[row], a.line_len[row], r, &bytes);
     VCFC_DIAG_ROW_END(a, row);
     if (vw::lane_id() == 0) {
         // not the fast shape: k_encode_var's wave for this row takes it
@@ -1607,7 +1594,7 @@ constexpr uint32_t VAR_ROWS = 32;
 // (round 2 ran it as a kernel of its own, k_encode_general: one more launch,
 // ~4.5 us on the headline rows, which flag none).  A resident grid striding
 // over rows was 13.6 % slower on law 2 (profiles/r02/ab/ab_gen_persist.txt).
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) void k_encode_var(VcfcEncodeArgs a, uint64_t row_lo, uint64_t row_hi) {
+__global__ __launch_bounds__(256) void k_encode_var(VcfcEncodeArgs a, uint64_t row_lo, uint64_t row_hi) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[K1_WAVES * RING_STRIDE];
     const uint32_t wave = vw::readfirst(threadIdx.x >> 6);
     const uint32_t l = vw::lane_id();

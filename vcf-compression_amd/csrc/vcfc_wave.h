@@ -124,8 +124,6 @@ __device__ __forceinline__ uint32_t alignbit(uint32_t hi, uint32_t lo, uint32_t 
 }
 // x + a*b on the low 24 bits of a and b, signed (v_mad_i32_i24)
 __device__ __forceinline__ int32_t mad24(int32_t a, int32_t b, int32_t x) { return x + __mul24(a, b); }
-// low 32 bits of the product of the low 24 bits of a and b (v_mul_u32_u24, full rate)
-__device__ __forceinline__ uint32_t mul24(uint32_t a, uint32_t b) { return __umul24(a, b); }
 // ((hi:lo) >> 8*s)[31:0]
 __device__ __forceinline__ uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t s) {
     return __builtin_amdgcn_alignbyte(hi, lo, s);
