@@ -54,6 +54,25 @@ def test_strerror_and_bounds(lib):
     assert lib.vcfc_encode_bound(10, 1000) >= 1000 * 3 // 2
 
 
+def test_workspace_staging_primary_per_batch(lib):
+    """The encode workspace holds prim_bytes of staging per row: 2 KiB for
+    batches whose mean line is >= 4 KiB, else 1 KiB (vcfc_prim_bytes,
+    vcfc_device.h); the rest scales with the line bytes."""
+    lib.vcfc_encode_workspace_size.restype = ctypes.c_uint64
+    lib.vcfc_encode_workspace_size.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
+    ws = lib.vcfc_encode_workspace_size
+    n = 100_000
+    # one more byte of lines changes the line-dependent parts by a few bytes;
+    # crossing the 4 KiB mean adds the second KiB of staging per row
+    below, above = ws(n, n * 4096 - 1), ws(n, n * 4096)
+    assert above - below >= 1024 * n
+    assert above - below < 1024 * n + 4096
+    # short rows keep 1 KiB per row: the workspace of 100-sample rows
+    # (~420 B) stays within a few times their bytes
+    assert ws(n, n * 420) < 6 * n * 420
+    assert ws(0, 0) >= 0
+
+
 def test_no_gpu_fails_loudly(lib):
     import torch  # noqa: F401  (device count only; does not initialise HIP)
     if torch.cuda.device_count() > 0:
