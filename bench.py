@@ -61,6 +61,9 @@ def parse():
                          "file -> file compress (row e: every rank its byte range, outputs held and placed at "
                          "the all-gathered offsets), --ingest-rows rows per rank")
     ap.add_argument("--dist-dir", default="/tmp/vcfc_distfile", help="--mode distfile: where the files go")
+    ap.add_argument("--line-index", choices=["hop", "scan"], default="hop",
+                    help="--mode devfile: the line index (hop: line ends guessed from the header's sample count "
+                         "and checked; scan: every byte)")
     ap.add_argument("--dev-chunk", type=int, default=0,
                     help="--mode devfile: chunk bytes of the device-resident compress (0: the whole file)")
     ap.add_argument("--rows-total", type=int, default=None,
@@ -77,7 +80,7 @@ def parse():
     if a.rows is None:
         a.rows = 100_000 if big else 1_000_000
     if a.cpu_rows is None:
-        a.cpu_rows = max(1, int(1.2e9 // (4 * a.samples + 180)))   # ~120k rows at 2504 samples
+        a.cpu_rows = max(1, int(2.4e9 // (4 * a.samples + 180)))   # ~235k rows at 2504 samples (~15 s, 1 core)
     return a
 
 
@@ -489,6 +492,7 @@ def bench_devfile(args, torch, vcfc, workload):
     ctx = vcfc.Context(0)
     if args.dev_chunk:
         ctx.set_ingest_chunk(args.dev_chunk)
+    ctx.set_line_index(args.line_index)
     for _ in range(args.warmup):
         st, k, _ = ctx.compress_device(d_file.data_ptr(), N, d_out.data_ptr(), cap)
         assert st == 0 and k == want_len, (st, k, want_len)
@@ -499,7 +503,7 @@ def bench_devfile(args, torch, vcfc, workload):
     identical = bool(torch.equal(d_out[:H], d_file[:H])) and bool(torch.equal(d_out[H:want_len], recs[:rec_bytes]))
     ctx.close()
     ms = elapsed * 1e3 / args.steps
-    hop = os.environ.get("VCFC_HOP", "1") != "0"
+    hop = args.line_index == "hop"
     alg = N + want_len   # the file read once, the output written once
     res = {"metric": "input GT bytes/sec, device-resident VCF file bytes -> .vcfc bytes (line index + encode)",
            "value": round(rows.gt_bytes / (ms * 1e-3) / 1e9, 2), "unit": "GB/s", "n_gpus": 1,
@@ -512,7 +516,7 @@ def bench_devfile(args, torch, vcfc, workload):
                       "chunk": ("%d bytes of whole lines per line index + encode" % args.dev_chunk) if args.dev_chunk
                                else "the whole file (one line index, one encode)",
                       "line_index": ("hop (line ends guessed from the header's sample count, ~1.2 KiB read per "
-                                     "line, checked by the encoder)") if hop else "scan of every byte (VCFC_HOP=0)"},
+                                     "line, checked by the encoder)") if hop else "scan of every byte (--line-index scan)"},
            "roofline": {"kernel": "line index + encoder (whole step)", "bound": "hbm",
                         "achieved": round(alg / (ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
@@ -635,11 +639,13 @@ def bench_biobank_shard(args):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     rehearsal = os.environ.get("VCFC_BENCH_REHEARSAL") == "1"
+    check_world(args, torch, world, local, rehearsal)
     dev = torch.device("cuda:%d" % (0 if rehearsal else local))
     torch.cuda.set_device(dev)
     cdev = torch.device("cpu") if rehearsal else dev
     if world > 1:
         dist.init_process_group("gloo" if rehearsal else "nccl", **({} if rehearsal else {"device_id": dev}))
+    rccl = rccl_report(torch, dist, dev, cdev, world, rehearsal)
     R, B, S = args.rows_total, args.rows, args.samples
     lo, hi = R * rank // world, R * (rank + 1) // world
     nb = (hi - lo + B - 1) // B
@@ -752,7 +758,8 @@ def bench_biobank_shard(args):
                             "rows_verified_by_oracle_digest": full_rows[0],
                             "batches_verified_every_record": verified_batches,
                             "rows_reencoded_byte_for_byte": checked,
-                            "shard_checksum_rank0": "%016x:%016x (determinism across passes, not parity)" % ck}}
+                            "shard_checksum_rank0": "%016x:%016x (determinism across passes, not parity)" % ck},
+           "rccl_world": rccl}
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
@@ -782,11 +789,13 @@ def bench_distfile(args):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     rehearsal = os.environ.get("VCFC_BENCH_REHEARSAL") == "1"
+    check_world(args, torch, world, local, rehearsal)
     dev = torch.device("cuda:%d" % (0 if rehearsal else local))
     torch.cuda.set_device(dev)
     cdev = torch.device("cpu") if rehearsal else dev
     if world > 1:
         dist.init_process_group("gloo" if rehearsal else "nccl", **({} if rehearsal else {"device_id": dev}))
+    rccl = rccl_report(torch, dist, dev, cdev, world, rehearsal)
 
     def allgather(vals):
         if world == 1:
@@ -838,9 +847,10 @@ def bench_distfile(args):
     torch.cuda.empty_cache()
     barrier()
     ctx = vcfc.Context(0 if rehearsal else local)
+    hold = vcfc.hold_bytes()
 
-    def hold(path, off, length):
-        return ctx.compress_range_held(path, off, length, mem_bound=D.HOLD_BYTES, spill_dir=args.dist_dir)
+    def hold_out(path, off, length):
+        return ctx.compress_range_held(path, off, length, mem_bound=hold, spill_dir=args.dist_dir)
 
     def step():
         if rank == 0:
@@ -850,7 +860,7 @@ def bench_distfile(args):
         barrier()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
-        st, total, line = D.compress_shard(ip, op, rank, world, ctx.compress_range, hold, allgather)
+        st, total, line = D.compress_shard(ip, op, rank, world, ctx.compress_range, hold_out, allgather)
         torch.cuda.synchronize(dev)
         barrier()
         dt = time.perf_counter() - t0
@@ -886,12 +896,13 @@ def bench_distfile(args):
                                   % (law_name(args.law), S, n, n * world),
                       "input_bytes": len(header) + sum(x[0] for x in g),
                       "output_bytes": len(header) + sum(x[1] for x in g),
-                      "hold_bytes_per_rank_max": D.HOLD_BYTES,
+                      "hold_bytes_per_rank_max": hold,
                       "parallelism": "byte-range shards x%d, all-gather of shard sizes%s"
                                      % (world, " (rehearsal: gloo, one GPU)" if rehearsal else "")},
            "timing": "wall time between barriers per step: read + H2D + line index + encode + D2H + write "
                      "(rank 0 in place, other ranks held then placed at the all-gathered offset), max over ranks",
-           "output_identical_to_gpu_records": all(x[0] == 1 for x in okt)}
+           "output_identical_to_gpu_records": all(x[0] == 1 for x in okt),
+           "rccl_world": rccl}
     if rank == 0:
         print(json.dumps(res), flush=True)
         if not res["output_identical_to_gpu_records"]:
@@ -900,8 +911,79 @@ def bench_distfile(args):
         dist.destroy_process_group()
 
 
+SHARDED_MODES = ("encode", "biobank", "distfile")
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_argv(n, argv, port):
+    """The command that runs this bench as N ranks, one process per GPU:
+    torch.distributed.run on this node, rendezvous on 127.0.0.1.  `argv` is
+    bench.py's own argument list, passed through unchanged (each rank then
+    sees WORLD_SIZE == --gpus)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % n,
+            "--master-addr=127.0.0.1", "--master-port=%d" % port, os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(args, argv):
+    """`python bench.py --gpus N` with N > 1 and no WORLD_SIZE in the
+    environment: start the N ranks as a CHILD process (this parent has not
+    imported torch or touched the GPU, and never execs), wait for it and
+    return its exit code.  Rank 0's JSON line reaches our stdout directly."""
+    if args.mode not in SHARDED_MODES:
+        sys.stderr.write("bench.py: --mode %s runs on one GPU; --gpus %d applies to --mode %s\n"
+                         % (args.mode, args.gpus, "/".join(SHARDED_MODES)))
+        return 2
+    cmd = launcher_argv(args.gpus, argv, free_port())
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def check_world(args, torch, world, local, rehearsal):
+    """Inside a rank: the world is the --gpus the run asked for, and (outside
+    the one-GPU rehearsal) every rank owns a distinct device."""
+    if world != args.gpus:
+        raise RuntimeError("WORLD_SIZE=%d but --gpus %d" % (world, args.gpus))
+    if world > 1 and not rehearsal:
+        if torch.cuda.device_count() < world:
+            raise RuntimeError("%d ranks but only %d visible GPUs" % (world, torch.cuda.device_count()))
+        if not 0 <= local < torch.cuda.device_count():
+            raise RuntimeError("LOCAL_RANK %d out of range" % local)
+
+
+def world_devices(torch, dist, dev, cdev, world):
+    """PCI (domain, bus, device) of every rank's GPU, all-gathered: the run's
+    proof that its N ranks sit on N distinct devices."""
+    p = torch.cuda.get_device_properties(dev)
+    me = [int(p.pci_domain_id), int(p.pci_bus_id), int(p.pci_device_id)]
+    if world == 1:
+        return [me]
+    t = torch.tensor(me, dtype=torch.int64, device=cdev)
+    o = torch.empty(world * 3, dtype=torch.int64, device=cdev)
+    dist.all_gather_into_tensor(o, t)
+    return o.view(world, 3).cpu().tolist()
+
+
+def rccl_report(torch, dist, dev, cdev, world, rehearsal):
+    devs = world_devices(torch, dist, dev, cdev, world)
+    distinct = len({tuple(d) for d in devs}) == world
+    if world > 1 and not rehearsal and not distinct:
+        raise RuntimeError("ranks share a GPU: %s" % devs)
+    return {"world": world, "backend": ("gloo (one-GPU rehearsal)" if rehearsal else "nccl (RCCL)")
+            if world > 1 else None,
+            "devices_pci": ["%04x:%02x:%02x" % tuple(d) for d in devs], "distinct_devices": distinct}
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args, sys.argv[1:])
     if args.mode == "biobank" and args.rows_total:
         return bench_biobank_shard(args)
     if args.mode == "distfile":
@@ -926,6 +1008,7 @@ def main():
     # cuda:0, gloo with host tensors for the collectives (RCCL refuses two
     # ranks on one device).  Never used for a reported number.
     rehearsal = os.environ.get("VCFC_BENCH_REHEARSAL") == "1"
+    check_world(args, torch, world, local, rehearsal)
     dev = torch.device("cuda:%d" % (0 if rehearsal else local))
     torch.cuda.set_device(dev)
     cdev = torch.device("cpu") if rehearsal else dev   # collective tensors
@@ -934,6 +1017,7 @@ def main():
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=dev)
+    rccl = rccl_report(torch, dist, dev, cdev, world, rehearsal)
     S = args.samples
     if args.scaling == "strong":
         # the --rows rows split over the ranks (each rank generates its own
@@ -1021,6 +1105,7 @@ def main():
                       "line_bytes_per_gpu": rows.line_bytes, "record_bytes_per_gpu": out_bytes,
                       "compression_ratio": round(out_bytes / rows.line_bytes, 4),
                       "parallelism": "row shards x%d, RCCL all-gather of shard sizes" % world},
+           "rccl_world": rccl,
            "roofline": roof}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb, cpu_out, k = cpu_baseline(rows, torch, args)
@@ -1034,4 +1119,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -58,6 +58,20 @@ void vcfc_ctx_destroy(vcfc_ctx *ctx);
  * twice.  The reference reads line by line (getline, src/compress.cpp:218);
  * the output does not depend on the chunk size. */
 int vcfc_ctx_set_ingest_chunk(vcfc_ctx *ctx, uint64_t chunk_bytes);
+/* Line index of vcfc_compress_device: VCFC_LINE_INDEX_HOP (default) guesses
+ * each data line's end from the header's sample count and checks it (a wrong
+ * guess re-indexes the chunk from every byte, so the output never depends on
+ * it); VCFC_LINE_INDEX_SCAN reads every byte.  The reference finds lines with
+ * getline (src/compress.cpp:218). */
+#define VCFC_LINE_INDEX_HOP 0
+#define VCFC_LINE_INDEX_SCAN 1
+int vcfc_ctx_set_line_index(vcfc_ctx *ctx, int mode);
+/* Stage timings / decisions of the host drivers to stderr (diagnostics; off
+ * by default): OR of the flags below. */
+#define VCFC_TRACE_INGEST 1u        /* vcfc_compress_file/_buffer/_range: stage totals */
+#define VCFC_TRACE_DEVICE 2u        /* vcfc_compress_device: chunks, sample count, re-indexes */
+#define VCFC_TRACE_SPARSE_QUERY 4u  /* vcfc_sparse_query*: stage totals */
+int vcfc_ctx_set_trace(vcfc_ctx *ctx, unsigned flags);
 
 /* ---- one line: replaces compress_data_line (src/compress.hpp:20-23) --------
  * Appends the record for `line` (no trailing '\n'; `len` bytes) to `out`

@@ -55,6 +55,34 @@ def hop_trap_file(kind, rnd, S_A=300, S_B=45):
     return hdr + b"\n".join(body) + b"\n"
 
 
+def hop_trap_dense_segment(rnd, seg=16384, n_short=150):
+    """The 'tab' trap inside a 16 KiB index segment that holds more than
+    NL_SLOT (128) line ends, whose last line is a '#' line.  k_nl_place scans
+    such a segment again and keeps as many positions as the hop index counted
+    there -- one fewer than there are, since the hop missed row A's end -- so
+    without a check the '#' line would run on to the next segment's first
+    recorded end and be written verbatim, a data row inside it.
+    The hop index's count must be found wrong and the chunk indexed again."""
+    trap = hop_trap_file("tab", rnd)
+    hdr, body = trap.split(b"#CHROM", 1)
+    head = hdr + b"".join(b"##k%d\n" % i for i in range(n_short)) + b"#CHROM" + body.split(b"\n", 1)[0] + b"\n"
+    lines = body.split(b"\n", 1)[1].rstrip(b"\n").split(b"\n")
+    S = head.rstrip(b"\n").split(b"\n")[-1].count(b"\t") - 8
+    a_b, tail = lines[:5], lines[5:]          # rows[:3], A, B (the trap), then data rows
+    out = head + b"\n".join(a_b) + b"\n"
+    for r in tail[:-1]:                        # data rows while they fit before the segment end
+        if len(out) + len(r) + 1 + 64 > seg:
+            break
+        out += r + b"\n"
+    assert out.count(b"\n") > 128 + 2
+    k = seg - 2 - len(out)                     # '#' line ending at byte seg - 2: the segment's last end
+    assert k >= 8
+    out += b"##" + b"t" * (k - 2) + b"\n"
+    assert len(out) == seg - 1
+    out += PREFIX % 999 + b"\t".join([b"0|1"] * S) + b"\n"   # a data row across the segment end
+    return out + b"\n".join(tail[-1:]) + b"\n"
+
+
 def chr22_like(rnd, n_rows, S, prefix_jitter=40):
     """Rows of S 3-byte tokens behind prefixes whose lengths vary by up to
     prefix_jitter bytes (the hop index guesses each end from the previous

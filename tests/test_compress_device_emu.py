@@ -12,7 +12,7 @@ import pytest
 import emu_io as E
 import golden_io as G
 import test_ingest_emu as T
-from hop_cases import chr22_like, hop_trap_file
+from hop_cases import chr22_like, hop_trap_dense_segment, hop_trap_file
 
 OK, E_ARG = 0, 5
 
@@ -144,6 +144,22 @@ def test_hop_index_trap_counts_fewer_lines(kind):
     hop, scan = E.emu_line_index(vcf, S), E.emu_line_index(vcf, 0)
     # A..B counted as one data line ('#' and empty lines between them swallowed)
     assert hop[0][0] < scan[0][0] and hop[0][1] == scan[0][1] - 1
+
+
+def test_hop_index_wrong_guess_in_dense_segment():
+    """A wrong guess inside a segment of more than 128 line ends whose last
+    line is a '#' line (hop_trap_dense_segment): k_nl_place's rescan finds
+    more ends than the hop counted, flags the index, and the chunk is indexed
+    again from every byte -- the output is the reference's."""
+    vcf = hop_trap_dense_segment(random.Random(5))
+    S = vcf.split(b"#CHROM", 1)[1].split(b"\n", 1)[0].count(b"\t") - 8
+    hop, scan = E.emu_line_index(vcf, S), E.emu_line_index(vcf, 0)
+    assert hop[0][3] == 2 and scan[0][3] == 0          # counts[3]: the rescan found the hop's count wrong
+    redo = []
+    st, out, _ = E.emu_compress_device(vcf, chunk=1 << 16, redo=redo)
+    st_o, want, _ = G.oracle_compress(vcf)
+    assert st == st_o == OK and out == want
+    assert redo == [1]
 
 
 def test_hop_index_long_header():

@@ -203,3 +203,15 @@ def test_hop_index_chr22_like_on_gpu(ctx):
         data = chr22_like(random.Random(S), 150, S, jitter)
         st_o, want, _ = G.oracle_compress(data)
         assert st_o == 0 and both_paths(ctx, data, 1 << 20) == (0, want, -1), S
+
+
+def test_hop_index_wrong_guess_in_dense_segment_on_gpu(ctx):
+    """A wrong guess in a 16 KiB segment of more than 128 line ends whose last
+    line is a '#' line (hop_cases.hop_trap_dense_segment): k_nl_place's
+    rescan finds the hop's count short and the chunk is indexed again; the
+    '#' line is not written with a data row inside it."""
+    from hop_cases import hop_trap_dense_segment
+    data = hop_trap_dense_segment(random.Random(5))
+    st_o, want, _ = G.oracle_compress(data)
+    assert st_o == 0
+    assert both_paths(ctx, data, 1 << 20) == (0, want, -1)

@@ -157,3 +157,36 @@ def test_rank_failure_travels_through_the_allgather():
         assert r1[0] == D.E_IO and r1[2] == -1
         pts = D.split_points(len(data), 2, lambda o, n: data[o:o + n])
         assert open(op, "rb").read() == G.oracle_compress(data[:pts[1]])[1]
+
+
+def test_hold_bytes_is_a_share_of_the_host(monkeypatch):
+    """The held-output bound: 3/4 of MemAvailable over the node's
+    ranks less 1 GiB of pinned buffers each, capped by VCFC_HOLD_GB (32 GiB
+    default), never below one 64 MiB block."""
+    import vcfc
+    G = 1 << 30
+    monkeypatch.delenv("VCFC_HOLD_GB", raising=False)
+    assert vcfc.hold_bytes(8, avail=256 * G) == 23 * G            # 192 GiB / 8 - 1
+    assert vcfc.hold_bytes(1, avail=1024 * G) == 32 * G           # capped
+    assert vcfc.hold_bytes(8, avail=4 * G) == 64 << 20            # floor
+    monkeypatch.setenv("VCFC_HOLD_GB", "2")
+    assert vcfc.hold_bytes(8, avail=256 * G) == 2 * G
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "4")
+    monkeypatch.setenv("VCFC_HOLD_GB", "100")
+    assert vcfc.hold_bytes(avail=64 * G) == 11 * G               # 48 GiB / 4 - 1
+    assert vcfc.mem_available() is None or vcfc.mem_available() > 0
+
+
+def test_held_releases_on_exit_and_gc():
+    import vcfc
+    freed = []
+
+    class H(vcfc.Held):
+        def free(self):
+            freed.append(self._h)
+            self._h = None
+    with H(1234):
+        pass
+    h = H(99)
+    del h
+    assert freed == [1234, None, 99]

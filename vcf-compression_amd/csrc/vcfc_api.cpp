@@ -86,6 +86,8 @@ struct vcfc_ctx {
     HostBuf ing_host[vcfc_ing::Memory::N_HOST];
     HostBuf dec_host[vcfc_dec::Buffers::N_HOST];
     uint64_t ingest_chunk = 0;   // 0: default (128 MiB)
+    int line_index = VCFC_LINE_INDEX_HOP;
+    unsigned trace = 0;          // VCFC_TRACE_* flags
 };
 
 namespace {
@@ -216,6 +218,7 @@ vcfc_ing::Config ingest_config(const vcfc_ctx *c, uint64_t n) {
     vcfc_ing::Config cfg;
     const uint64_t want = c->ingest_chunk ? c->ingest_chunk : (128ull << 20);
     cfg.chunk = std::min<uint64_t>(want, std::max<uint64_t>((n + 4095) & ~4095ull, 4096));
+    cfg.trace = (c->trace & VCFC_TRACE_INGEST) != 0;
     return cfg;
 }
 
@@ -272,6 +275,18 @@ void vcfc_ctx_destroy(vcfc_ctx *c) {
 int vcfc_ctx_set_ingest_chunk(vcfc_ctx *c, uint64_t chunk_bytes) {
     if (!c || (chunk_bytes && (chunk_bytes < 4096 || chunk_bytes > (3ull << 30)))) return VCFC_E_ARG;
     c->ingest_chunk = chunk_bytes;
+    return VCFC_OK;
+}
+
+int vcfc_ctx_set_line_index(vcfc_ctx *c, int mode) {
+    if (!c || (mode != VCFC_LINE_INDEX_HOP && mode != VCFC_LINE_INDEX_SCAN)) return VCFC_E_ARG;
+    c->line_index = mode;
+    return VCFC_OK;
+}
+
+int vcfc_ctx_set_trace(vcfc_ctx *c, unsigned flags) {
+    if (!c || (flags & ~(VCFC_TRACE_INGEST | VCFC_TRACE_DEVICE | VCFC_TRACE_SPARSE_QUERY))) return VCFC_E_ARG;
+    c->trace = flags;
     return VCFC_OK;
 }
 
@@ -656,6 +671,8 @@ int vcfc_compress_device(vcfc_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *
     cfg.max_chunk = 1ull << 40;   // (line lengths are 32-bit; the index's positions 64-bit)
     const uint64_t want = c->ingest_chunk ? c->ingest_chunk : cfg.max_chunk;
     cfg.chunk = std::min<uint64_t>(want, std::max<uint64_t>((n + 4095) & ~4095ull, 4096));
+    cfg.hop_index = c->line_index == VCFC_LINE_INDEX_HOP;
+    cfg.trace = (c->trace & VCFC_TRACE_DEVICE) != 0;
     return vcfc_ing::compress_device(d_in, n, d_out, out_cap, out_len, M, c->stream, cfg, err_line);
 }
 
@@ -933,7 +950,7 @@ int vcfc_sparse_query_file(vcfc_ctx *c, const char *in_path, const char *ref, ui
     q.ref = reinterpret_cast<const uint8_t *>(ref); q.ref_len = ref_len; q.has_range = has_range;
     q.start = start; q.end = end;
     CtxDecodeBuffers B(c);
-    const int st = vcfc_dec::sparse_query(fd, q, B, c->stream, sink);
+    const int st = vcfc_dec::sparse_query(fd, q, B, c->stream, sink, (c->trace & VCFC_TRACE_SPARSE_QUERY) != 0);
     close(fd);
     return st;
 }

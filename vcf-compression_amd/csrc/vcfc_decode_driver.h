@@ -503,11 +503,11 @@ inline int sq_stage(int fd, SqBatch &b, Buffers &B) {
 // run up to two batches past the reference's last record; nothing it reads
 // there is used.
 inline int sq_traverse(int fd, uint64_t fsize, uint64_t ls, uint64_t S, const SparseQuery &q, Buffers &B,
-                       hipStream_t s, const Sink &sink) {
+                       hipStream_t s, const Sink &sink, bool trace) {
     const int64_t max_seek = sq_max_seek(fd);
     constexpr uint64_t SQ_BATCH = 4096;
-    struct Trace {   // stage times (VCFC_SQ_TRACE=1 prints them to stderr)
-        bool on = getenv("VCFC_SQ_TRACE") != nullptr;
+    struct Trace {   // stage times (VCFC_TRACE_SPARSE_QUERY prints them to stderr)
+        bool on = false;
         double walk = 0, dec = 0, eval = 0, wait_w = 0, wait_out = 0, total = 0;
         uint64_t recs = 0, batches = 0;
         static double now() {
@@ -521,6 +521,7 @@ inline int sq_traverse(int fd, uint64_t fsize, uint64_t ls, uint64_t S, const Sp
                         total * 1e3, walk * 1e3, dec * 1e3, eval * 1e3, wait_w * 1e3, wait_out * 1e3);
         }
     } tr;
+    tr.on = trace;
     const double t_begin = Trace::now();
     // ---- writer ------------------------------------------------------------
     struct WriteJob {
@@ -676,7 +677,8 @@ inline int sq_traverse(int fd, uint64_t fsize, uint64_t ls, uint64_t S, const Sp
     return status;
 }
 
-inline int sparse_query(int fd, const SparseQuery &q, Buffers &B, hipStream_t s, const Sink &sink) {
+inline int sparse_query(int fd, const SparseQuery &q, Buffers &B, hipStream_t s, const Sink &sink,
+                        bool trace = false) {
     struct stat sb;
     if (fstat(fd, &sb) != 0) return ST_E_IO;
     const uint64_t fsize = (uint64_t)sb.st_size;
@@ -733,7 +735,7 @@ inline int sparse_query(int fd, const SparseQuery &q, Buffers &B, hipStream_t s,
             break;
         }
     }
-    return sq_traverse(fd, fsize, (uint64_t)lseek(fd, 0, SEEK_CUR), S, q, B, s, sink);
+    return sq_traverse(fd, fsize, (uint64_t)lseek(fd, 0, SEEK_CUR), S, q, B, s, sink, trace);
 }
 
 }  // namespace vcfc_dec

@@ -287,7 +287,8 @@ __global__ __launch_bounds__(256) void k_nl_hop(const uint8_t *buf, uint64_t n, 
 // positions); a segment with more lines than its slot holds is scanned
 // again by the whole wave, one such segment after the other.
 __global__ __launch_bounds__(256) void k_nl_place(const uint8_t *buf, uint64_t n, uint64_t n_seg, const uint32_t *seg_cnt,
-                                                  const uint64_t *slot, const uint64_t *seg_base, uint64_t *nl) {
+                                                  const uint64_t *slot, const uint64_t *seg_base, uint64_t *nl,
+                                                  uint64_t *counts) {
     const uint32_t l = vw::lane_id();
     const uint64_t seg0 = ((uint64_t)blockIdx.x * IX_WAVES + vw::readfirst(threadIdx.x >> 6)) * 64;
     if (seg0 >= n_seg) return;
@@ -298,9 +299,14 @@ __global__ __launch_bounds__(256) void k_nl_place(const uint8_t *buf, uint64_t n
         uint64_t *dst = nl + (seg < n_seg ? seg_base[seg] : 0);
         for (uint32_t k = 0; k < c; k++) dst[k] = sl[k];
     }
-    // more lines than the slot holds: scan the segment again (at most c
-    // positions: the hop index may have counted fewer than there are, and
-    // the encoder then rejects the chunk's index)
+    // more lines than the slot holds: scan the segment again, keeping at
+    // most the c positions the count scan made room for.  The hop index may
+    // have counted fewer than there are (a guessed end across a line it did
+    // not see); the positions kept would then be the segment's first c, and
+    // the line after them would swallow a real '\n' -- a '#' line placed
+    // verbatim if it starts with '#', which the encoder never checks.  So a
+    // count that differs from the scan's marks the index as wrong
+    // (counts[3] = 2: the driver indexes the chunk again from every byte).
     for (uint64_t m = vw::ballot(c > NL_SLOT); m; m &= m - 1) {
         const uint32_t f = (uint32_t)__builtin_ctzll(m);
         const uint64_t sf = seg0 + f;
@@ -308,6 +314,7 @@ __global__ __launch_bounds__(256) void k_nl_place(const uint8_t *buf, uint64_t n
         uint64_t *dst = nl + seg_base[sf];
         uint32_t o = 0;
         for (uint32_t w = 0; w < SEG; w += WIN) o += nl_window(buf, n, sf * SEG + w + 16 * l, dst, o, cf);
+        if (o != cf && l == 0) atomicMax((unsigned long long *)(counts + 3), 2ull);
     }
 }
 
@@ -419,7 +426,7 @@ hipError_t vcfc_line_index_place(const uint8_t *buf, uint64_t n, uint64_t n_line
     if ((e = hipMemsetAsync(x.counts + 3, 0, 8, s)) != hipSuccess) return e;
     const uint64_t n_seg = (n + SEG - 1) / SEG;
     hipLaunchKernelGGL(k_nl_place, dim3((unsigned)((n_seg + 64 * IX_WAVES - 1) / (64 * IX_WAVES))), dim3(64 * IX_WAVES), 0,
-                       s, buf, n, n_seg, seg_cnt, slot, seg_base, nl);
+                       s, buf, n, n_seg, seg_cnt, slot, seg_base, nl, x.counts);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const dim3 g((unsigned)((n_lines + 255) / 256)), blk(256);
     hipLaunchKernelGGL(k_line_kind, g, blk, 0, s, buf, nl, n_lines, is_data, is_pass);

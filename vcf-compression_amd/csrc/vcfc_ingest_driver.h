@@ -148,6 +148,7 @@ struct Config {
                                      // LEN header holds < 2^30 anyway, reference src/utils.hpp:160)
     int read_threads = 8;
     bool hop_index = true;           // compress_device: the hop line index (S from "#CHROM")
+    bool trace = false;              // stage totals / decisions to stderr (vcfc_ctx_set_trace)
     uint64_t *hop_redo = nullptr;    // compress_device: chunks indexed again after a wrong hop guess
 };
 
@@ -270,7 +271,7 @@ inline int compress_stream(Source &src, const Sink &sink, Memory &M, hipStream_t
     Queue<int> free_in;
     for (int k = 0; k < 3; k++) free_in.put(k);
     std::vector<uint8_t> carry;
-    const bool trace = getenv("VCFC_INGEST_TRACE") != nullptr;
+    const bool trace = cfg.trace;
     double t_read = 0, t_gpu = 0, t_write = 0, t_wait_in = 0, t_wait_out = 0;
     const double t_begin = now_s();
     std::thread reader([&] {
@@ -603,7 +604,7 @@ inline int compress_device(const uint8_t *d_in, uint64_t N, uint8_t *d_out, uint
     if (err_line) *err_line = -1;
     *out_len = 0;
     if (N == 0) return ST_OK;
-    const bool trace = getenv("VCFC_DEV_TRACE") != nullptr;
+    const bool trace = cfg.trace;
     if (trace) fprintf(stderr, "compress_device: N=%llu chunk=%llu max=%llu\n", (unsigned long long)N,
                        (unsigned long long)cfg.chunk, (unsigned long long)cfg.max_chunk);
     if (cfg.chunk < 16 || cfg.chunk > cfg.max_chunk) return ST_E_ARG;
@@ -625,11 +626,11 @@ inline int compress_device(const uint8_t *d_in, uint64_t N, uint8_t *d_out, uint
     // The sample count S from the "#CHROM" line (in the first MiB) lets the
     // line index hop over a data line's genotypes (vcfc_line_index S_hint);
     // a chunk whose hop index the encoder finds wrong (VCFCD_E_NEWLINE) is
-    // indexed again from every byte.  VCFC_HOP=0: always every byte.
+    // indexed again from every byte.  cfg.hop_index false
+    // (VCFC_LINE_INDEX_SCAN): always every byte.
     uint32_t S_hint = 0;
     {
-        const char *hv = getenv("VCFC_HOP");
-        if (cfg.hop_index && !(hv && hv[0] == '0')) {
+        if (cfg.hop_index) {
             // 64 KiB of the file into pinned memory, 1 MiB if the header is longer
             for (uint64_t want = std::min<uint64_t>(N, 64u << 10);;) {
                 uint8_t *h = static_cast<uint8_t *>(M.host(Memory::H_IN0, want));
@@ -703,7 +704,12 @@ inline int compress_device(const uint8_t *d_in, uint64_t N, uint8_t *d_out, uint
         if (vcfc_line_index_place(d_c, n, n_lines, d_ix1, d_ix2, L, x, s) != hipSuccess || !d2h(hsmall, d_small, 32) ||
             !sync())
             return ST_E_HIP;
-        if (hsmall[3]) {   // a line of 4 GiB or more (or a hop across lines)
+        // counts[3]: 1 = a line of 4 GiB or more (k_line_place), 2 = a hop
+        // index that missed a line end in a segment of more than NL_SLOT
+        // lines (k_nl_place's rescan; the other missed ends reach the encoder
+        // inside a data row, VCFCD_E_NEWLINE below).  Either way the scan
+        // index decides: it never sets 2, and refuses 1.
+        if (hsmall[3]) {
             if (hop) {
                 if (cfg.hop_redo) ++*cfg.hop_redo;
                 hop = 0;

@@ -23,9 +23,9 @@ import os
 import sys
 
 E_IO = 7   # include/vcfc.h VCFC_E_IO
-# output a rank holds in host memory until its offset is known (the rest
-# spills to a temporary file beside the output): VCFC_HOLD_GB, default 32
-HOLD_BYTES = int(float(os.environ.get("VCFC_HOLD_GB", "32")) * (1 << 30))
+# Output a rank holds in host memory until its offset is known (the rest
+# spills to a temporary file beside the output): vcfc.hold_bytes(), this
+# rank's share of the host's MemAvailable, capped by VCFC_HOLD_GB (32 GiB).
 
 
 def split_points(data_len, world, read_at):
@@ -188,7 +188,7 @@ def main():
     def hold(path, off, length):
         if ctx is None:
             return vcfc.E_HIP, 0, -1, 0, None
-        return ctx.compress_range_held(path, off, length, mem_bound=HOLD_BYTES,
+        return ctx.compress_range_held(path, off, length, mem_bound=vcfc.hold_bytes(),
                                        spill_dir=os.path.dirname(os.path.abspath(out_path)))
 
     def allgather(vals):

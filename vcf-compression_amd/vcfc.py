@@ -37,8 +37,10 @@ EXPORTS = [
     "vcfc_query_match_device", "vcfc_decode_selected_device", "vcfc_sparse_query_file",
     "vcfc_sparsify_shard", "vcfc_ctx_set_ingest_chunk", "vcfc_record_hash_device",
     "vcfc_compress_range", "vcfc_compress_device", "vcfc_compress_range_held", "vcfc_held_place",
-    "vcfc_held_sizes", "vcfc_held_free",
+    "vcfc_held_sizes", "vcfc_held_free", "vcfc_ctx_set_line_index", "vcfc_ctx_set_trace",
 ]
+LINE_INDEX_HOP, LINE_INDEX_SCAN = 0, 1                       # include/vcfc.h VCFC_LINE_INDEX_*
+TRACE_INGEST, TRACE_DEVICE, TRACE_SPARSE_QUERY = 1, 2, 4     # include/vcfc.h VCFC_TRACE_*
 
 
 class VcfValidationError(RuntimeError):
@@ -67,6 +69,8 @@ def lib():
     L.vcfc_ctx_destroy.argtypes = [vp]
     L.vcfc_ctx_destroy.restype = None
     L.vcfc_ctx_set_ingest_chunk.argtypes = [vp, u64]
+    L.vcfc_ctx_set_line_index.argtypes = [vp, ctypes.c_int]
+    L.vcfc_ctx_set_trace.argtypes = [vp, ctypes.c_uint]
     L.vcfc_record_hash_device.argtypes = [vp, vp, u64, vp, vp]
     L.vcfc_compress_range.argtypes = [vp, ctypes.c_char_p, u64, u64, ctypes.c_int, u64, ctypes.POINTER(u64),
                                       ctypes.POINTER(i64), ctypes.POINTER(u64)]
@@ -156,11 +160,60 @@ def parse_coordinate_string(q):
     return VcfCoordinateQuery(qb[:ref_len.value], bool(has_range.value), start.value, end.value)
 
 
+HOLD_CAP_DEFAULT = 32 << 30     # VCFC_HOLD_GB unset: at most 32 GiB held per rank
+INGEST_PINNED_BYTES = 1 << 30   # a rank's own pinned ingest slots and staging (3 x 128 MiB + margin)
+
+
+def mem_available(meminfo="/proc/meminfo"):
+    """MemAvailable of this host in bytes (None when it cannot be read)."""
+    try:
+        with open(meminfo) as f:
+            for line in f:
+                if line.startswith("MemAvailable:"):
+                    return int(line.split()[1]) * 1024
+    except OSError:
+        pass
+    return None
+
+
+def hold_bytes(local_world=None, avail=None):
+    """How much output one rank may hold in host memory before it spills
+    (Context.compress_range_held's mem_bound): a share of the host's available
+    memory -- 3/4 of MemAvailable split over the node's ranks, less each rank's
+    pinned ingest buffers -- capped by VCFC_HOLD_GB (default 32 GiB), and at
+    least 64 MiB (one hold block).  Bounding by the host, not a constant,
+    keeps 8 ranks from overcommitting a node into the OOM killer while their
+    peers wait in the all-gather."""
+    import os
+    if local_world is None:
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")) or 1)
+    env = os.environ.get("VCFC_HOLD_GB")
+    cap = int(float(env) * (1 << 30)) if env else HOLD_CAP_DEFAULT
+    avail = mem_available() if avail is None else avail
+    if avail is not None:
+        cap = min(cap, (avail * 3 // 4) // max(1, local_world) - INGEST_PINNED_BYTES)
+    return max(64 << 20, cap)
+
+
 class Held:
-    """Output of Context.compress_range_held, placed once its offset is known."""
+    """Output of Context.compress_range_held, placed once its offset is known.
+    Owns host memory (up to its bound) and a spill file: free() releases them,
+    as do `with` and garbage collection."""
 
     def __init__(self, h):
         self._h = h
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.free()
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
 
     def place(self, fd, off):
         """Write every held byte at file offset `off` of fd; returns the status."""
@@ -201,6 +254,15 @@ class Context:
         """Input chunk of compress_file / compress_buffer (0 = default 128 MiB);
         the output does not depend on it."""
         raise_for(lib().vcfc_ctx_set_ingest_chunk(self._h, int(chunk_bytes)))
+
+    def set_line_index(self, mode):
+        """compress_device's line index: "hop" (default; guessed line ends,
+        checked) or "scan" (every byte).  The output does not depend on it."""
+        raise_for(lib().vcfc_ctx_set_line_index(self._h, {"hop": LINE_INDEX_HOP, "scan": LINE_INDEX_SCAN}[mode]))
+
+    def set_trace(self, flags):
+        """Stage timings of the host drivers to stderr (TRACE_* flags)."""
+        raise_for(lib().vcfc_ctx_set_trace(self._h, int(flags)))
 
     def __enter__(self):
         return self
@@ -266,11 +328,14 @@ class Context:
                                        ctypes.byref(line), ctypes.byref(lines))
         return st, nb.value, line.value, lines.value
 
-    def compress_range_held(self, in_path, off, length, mem_bound=16 << 30, spill_dir=None):
+    def compress_range_held(self, in_path, off, length, mem_bound=None, spill_dir=None):
         """compress_range with the output held (host memory up to mem_bound
-        bytes, the rest in a spill file) until its file offset is known.
+        bytes -- default hold_bytes(), this rank's share of the host -- the
+        rest in a spill file) until its file offset is known.
         Returns (status, bytes, failing line in the range or -1, lines in the
         range, Held); does not raise."""
+        if mem_bound is None:
+            mem_bound = hold_bytes()
         nb, line, lines, h = ctypes.c_uint64(0), ctypes.c_int64(-1), ctypes.c_uint64(0), ctypes.c_void_p()
         st = lib().vcfc_compress_range_held(self._h, in_path.encode(), off, length, mem_bound,
                                             spill_dir.encode() if spill_dir else None, ctypes.byref(h),
