@@ -70,6 +70,9 @@ def parse():
                     help="--mode biobank: encode the rank's whole share of this many rows (5M = configs[3]) "
                          "as back-to-back --rows batches, every record digested and sampled rows re-encoded "
                          "by the CPU checker; a step is the whole shard")
+    ap.add_argument("--sample-rows", type=int, default=1000,
+                    help="--mode biobank --rows-total: random rows of every other batch digest-checked against "
+                         "the oracle per pass (besides one whole batch per pass)")
     ap.add_argument("--sparse-rows", type=int, default=200_000, help="rows of the --mode sparse file")
     ap.add_argument("--ingest-rows", type=int, default=200_000, help="rows of the --mode ingest file")
     ap.add_argument("--query-frac", type=float, default=0.125, help="rows selected by the --mode query range")
@@ -625,8 +628,9 @@ def bench_biobank_shard(args):
     folded into a shard checksum; two rows per batch are re-encoded by the
     CPU checker (oracle) and compared byte for byte, and each pass checks
     EVERY record of one whole batch (a different batch per pass: pass p
-    takes batch 7p mod nb) against the checker's threaded digests and sizes
-    (SURVEY §7 hard part 7).
+    takes batch 7p mod nb) and --sample-rows random rows of every other
+    batch against the checker's threaded digests and sizes (SURVEY §7 hard
+    part 7: per-row hashes plus a sampled CPU re-encode across the shard).
     One step = the whole shard; `ms_per_step` and `value` use the summed
     encode time of its batches (HIP events on the encode stream), max over
     ranks; the wall time including generation and checks is reported too."""
@@ -667,6 +671,7 @@ def bench_biobank_shard(args):
     line_off_host = rows.line_off.cpu().numpy()
     cpu_threads = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
     verified_batches = []
+    sampled_batches = set()
 
     def verify_batch(b, n, d):
         """every record of batch b: the oracle's size and digest (threaded)"""
@@ -679,6 +684,23 @@ def bench_biobank_shard(args):
             raise RuntimeError("batch %d: rows %s differ from the CPU checker" % (b, bad[:8].tolist()))
         verified_batches.append(b)
         return n
+
+    def verify_sample(b, n, d, k):
+        """k random rows of batch b (gathered on the GPU, ~k x 400 KB to the
+        host): the oracle's sizes and digests of its own encode against the
+        GPU's in-place digests d."""
+        idx = np.sort(rng.choice(n, size=min(k, n), replace=False))
+        offs = line_off_host[idx].astype(np.int64)
+        lens = rows.line_len_host[idx].astype(np.int64)
+        blob = torch.cat([rows.buf[int(o):int(o) + int(ln)] for o, ln in zip(offs, lens)]).cpu().numpy()
+        loc = np.concatenate([[0], np.cumsum(lens)[:-1]])
+        st, size, want = G.oracle_encode_rows_hash(blob, loc, lens, threads=cpu_threads)
+        r = rec[:n + 1].cpu().numpy().astype(np.uint64)
+        bad = np.nonzero((st != 0) | (size.astype(np.uint64) != (r[idx + 1] - r[idx])) | (want != d[idx]))[0]
+        if bad.size:
+            raise RuntimeError("batch %d: rows %s differ from the CPU checker" % (b, idx[bad[:8]].tolist()))
+        sampled_batches.add(b)
+        return len(idx)
 
     def shard_pass(check, p=0):
         enc_ms, gt, recb, checked = 0.0, 0, 0, 0
@@ -708,6 +730,8 @@ def bench_biobank_shard(args):
             cxor ^= int(np.bitwise_xor.reduce(d))
             if b == (7 * p) % nb:
                 full_rows[0] += verify_batch(b, n, d)
+            elif args.sample_rows:
+                full_rows[0] += verify_sample(b, n, d, args.sample_rows)
             for i in rng.integers(0, n, 2):
                 line = rows.host_lines([int(i)])[0]
                 got = out[int(rec[i].item()):int(rec[i + 1].item())].cpu().numpy().tobytes()
@@ -757,6 +781,8 @@ def bench_biobank_shard(args):
                             "rows_verified": full_rows[0] + checked,
                             "rows_verified_by_oracle_digest": full_rows[0],
                             "batches_verified_every_record": verified_batches,
+                            "batches_verified_by_sample": len(sampled_batches),
+                            "sample_rows_per_batch": args.sample_rows,
                             "rows_reencoded_byte_for_byte": checked,
                             "shard_checksum_rank0": "%016x:%016x (determinism across passes, not parity)" % ck},
            "rccl_world": rccl}

@@ -215,3 +215,52 @@ def test_range_query_full_batch(torch, vcfc):
         assert ost == 0, name
         host = rows.host_lines([i for i in pick if ra is not None and ra <= i <= rb])
         assert olines == b"".join(x + b"\n" for x in host), name
+
+
+@pytest.mark.parametrize("law,line_index", [(1, "hop"), (1, "scan"), (2, "hop")])
+def test_full_file_compress_device(torch, vcfc, law, line_index):
+    """BASELINE configs[2] at config size: the whole-file compress()
+    (reference src/compress.cpp:205-257) of a 2504 x 1M VCF file (header +
+    1M data lines, ~10.2 GB for the chr22 law) whose bytes are in HBM
+    (vcfc_compress_device: GPU line index + encoder over the whole file).
+    The output must be the header followed by the device encoder's records of
+    the same rows, byte for byte on the GPU (torch.equal), and every record's
+    digest must equal the oracle's threaded digest of its own encode.  Law 1
+    with the hop line index and with the full scan; law 2 (haploid,
+    GT:DP:GQ, missing: lines the hop cannot predict, found 1 KiB per round)."""
+    import workload
+    from test_gpu_encode import _device_encode
+    n, S = 1_000_000, 2504
+    dev = torch.device("cuda:0")
+    rows = workload.DeviceRows(torch, vcfc, n, S, law, seed=51 + law, device="cuda:0")
+    out, rec, err = _device_encode(torch, vcfc, rows)
+    assert err == vcfc.NO_ERROR
+    rec_bytes = int(rec[n])
+    hdr = _header(S)
+    H = len(hdr)
+    N = H + rows.total_bytes
+    d_file = torch.empty(N, dtype=torch.uint8, device=dev)
+    d_file[:H] = torch.frombuffer(bytearray(hdr), dtype=torch.uint8).to(dev)
+    d_file[H:] = rows.buf[:rows.total_bytes]
+    cap = int(vcfc.lib().vcfc_compress_bound(N))
+    d_out = torch.empty(cap, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize(dev)
+    with vcfc.Context(0) as ctx:
+        ctx.set_line_index(line_index)
+        st, k, el = ctx.compress_device(d_file.data_ptr(), N, d_out.data_ptr(), cap)
+    assert (st, el) == (0, -1) and k == H + rec_bytes
+    assert bool(torch.equal(d_out[:H], d_file[:H]))
+    assert bool(torch.equal(d_out[H:k], out[:rec_bytes]))
+    del d_file, out
+    # every record of the file's output against the oracle's digest
+    rec_t = torch.from_numpy(rec.astype(np.int64) + H).to(dev)
+    h = torch.empty(n, dtype=torch.int64, device=dev)
+    vcfc.record_hash_device(d_out.data_ptr(), rec_t.data_ptr(), n, h.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize(dev)
+    got_h = h.cpu().numpy().view(np.uint64)
+    buf = rows.buf[:rows.total_bytes].cpu().numpy()
+    st, size, want_h = G.oracle_encode_rows_hash(buf, rows.line_off.cpu().numpy(), rows.line_len.cpu().numpy(),
+                                                 threads=threads())
+    assert (st == 0).all()
+    bad = np.nonzero((size.astype(np.uint64) != np.diff(rec)) | (want_h != got_h))[0]
+    assert bad.size == 0, "rows differ from the oracle: %s" % bad[:10].tolist()
