@@ -364,3 +364,51 @@ def test_law2_synthetic_rows():
         gdg += b"GT:DP:GQ" in line
         assert out[int(ro[i]):int(ro[i + 1])] == G.oracle_encode_line(line)[1], i
     assert gdg > 0 and E.LAST_RETRIES[0] == 0
+
+
+@pytest.mark.parametrize("seed", [51, 52, 53, 54])
+def test_sparse_clean_ranges(seed):
+    """The sparse clean path (k_encode_fast ev_append / ev_flush): 512-token
+    chunks holding 0, 1, a few, 62, 63, 64 or 65 non-0|0 tokens (the EV_MAX
+    boundary: a range closes early, or the chunk goes to clean8), runs of one
+    class crossing chunk ends inside a pending range, 0|0 gaps spanning whole
+    chunks and 127-multiples, ranges cut by dense, escape and last chunks,
+    and an event at token 0 (the first chunk's virtual run)."""
+    rnd = random.Random(seed)
+    classes = [b"0|1", b"1|0", b"1|1"]
+    lines = []
+    for i in range(16):
+        nch = rnd.choice([3, 5, 6, 9, 13])
+        toks = []
+        for c in range(nch):
+            kind = rnd.choice(["zero", "few", "edge", "edge", "dense", "esc", "run"])
+            chunk = [b"0|0"] * 512
+            if kind == "few":
+                for p in rnd.sample(range(512), rnd.choice([1, 2, 5, 20])):
+                    chunk[p] = rnd.choice(classes)
+            elif kind == "edge":
+                for p in rnd.sample(range(512), rnd.choice([61, 62, 63, 64, 65])):
+                    chunk[p] = rnd.choice(classes)
+            elif kind == "dense":
+                chunk = [rnd.choice(classes + [b"0|0"]) for _ in range(512)]
+            elif kind == "esc":
+                chunk[rnd.randrange(512)] = b"0|2"
+            elif kind == "run":   # one class from near the chunk end into the next chunk
+                cl = rnd.choice(classes)
+                for p in range(512 - rnd.randint(1, 40), 512):
+                    chunk[p] = cl
+                toks += chunk
+                chunk = [cl] * rnd.randint(1, 40) + [b"0|0"] * 600
+                chunk = chunk[:512]
+            toks += chunk
+        if rnd.random() < 0.5:
+            toks[0] = rnd.choice(classes)
+        toks = toks[:len(toks) - rnd.randrange(300)]
+        pfx = b"22\t%d\trs%d\tA\tG\t100\tPASS\t%s\tGT\t" % (100 + i, i, b"Z" * rnd.randint(1, 50))
+        lines.append(pfx + b"\t".join(toks))
+    for lead in (0, 6):
+        st, out, ro, err = run(lines, lead=lead)
+        assert err == (1 << 64) - 1
+        assert E.LAST_RETRIES[0] == 0
+        for i, ln in enumerate(lines):
+            assert out[int(ro[i]):int(ro[i + 1])] == G.oracle_encode_line(ln)[1], (lead, i)
