@@ -99,7 +99,14 @@ uint64_t vcfc_encode_workspace_size(uint64_t n_rows, uint64_t total_line_bytes);
  *                    where total >= sum of d_line_len
  *   d_err            one uint64: ~0 = success, else (row << 8 | status) of the
  *                    first failing row (rows before it are valid output)
- * Returns VCFC_OK if the work was enqueued. Capturable in a hipGraph. */
+ * Returns VCFC_OK if the work was enqueued.  Capturable in a hipGraph: the
+ * per-call state is reset by a kernel, not by hipMemsetAsync -- on this ROCm
+ * a captured 24-byte memset node writes garbage into its first 16 bytes from
+ * the second replay on (4- and 8-byte nodes replay correctly;
+ * tools/dbg/memset_graph_probe.py, profiles/r04/memset_graph_probe.txt).
+ * The n == 0 call enqueues two 8-byte memsets (safe).  The host-driven entry
+ * points below (vcfc_compress_*, the decoders) synchronise and are not meant
+ * for capture. */
 int vcfc_encode_rows_device(const uint8_t *d_buf, const uint64_t *d_line_off,
                             const uint32_t *d_line_len, uint64_t n, uint64_t total_line_bytes,
                             uint8_t *d_out, uint64_t out_cap, uint64_t *d_rec_off,

@@ -81,11 +81,6 @@ inline int popc64(uint64_t m) { return __builtin_popcountll(m); }
 inline int hibit64(uint64_t m) { return 63 - __builtin_clzll(m); }
 inline uint32_t mulhi(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }
 inline uint4 gload16(const void *base, uint32_t idx) { return ((const uint4 *)base)[idx]; }
-typedef uint8_t lds_u8;   // (the product header's address-space-3 pointers)
-typedef uint32_t lds_u32;
-inline lds_u8 *lds(void *p) { return (lds_u8 *)p; }
-inline uint4 lds_load16(const lds_u8 *p) { uint4 v; memcpy(&v, p, 16); return v; }
-inline void lds_store4u(lds_u8 *p, uint32_t v) { memcpy(p, &v, 4); }
 inline uint4 uload16(const void *p) { uint4 v; memcpy(&v, p, 16); return v; }
 inline uint32_t gload4(const void *base, uint32_t idx) { return ((const uint32_t *)base)[idx]; }
 inline void gstore16(void *base, uint64_t byte_off, uint4 v) { *(uint4 *)((uint8_t *)base + byte_off) = v; }

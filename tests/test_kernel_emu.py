@@ -368,7 +368,8 @@ def test_law2_synthetic_rows():
 
 @pytest.mark.parametrize("seed", [51, 52, 53, 54])
 def test_sparse_clean_ranges(seed):
-    """The sparse clean path (k_encode_fast ev_append / ev_flush): 512-token
+    """Sparse clean chunks (the shape a sparse event path would take, round 4;
+    measured slower and not kept -- DESIGN.md §4 round 4): 512-token
     chunks holding 0, 1, a few, 62, 63, 64 or 65 non-0|0 tokens (the EV_MAX
     boundary: a range closes early, or the chunk goes to clean8), runs of one
     class crossing chunk ends inside a pending range, 0|0 gaps spanning whole

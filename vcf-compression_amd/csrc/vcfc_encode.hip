@@ -56,10 +56,7 @@ constexpr uint32_t RMASK = RING - 1;
 // see esc8), padded to keep the next wave's ring 16-B aligned
 constexpr uint32_t RING_TAIL = 64;
 constexpr uint32_t RING_DUMMY = RING + RING_TAIL;
-// + the event list of the sparse clean path (k_encode_fast, see ev_flush)
-constexpr uint32_t RING_EV = RING_DUMMY + 16;
-constexpr uint32_t EV_MAX = 63;        // events per step (lane EV_MAX closes the range)
-constexpr uint32_t RING_STRIDE = RING_EV + 4 * (EV_MAX + 1);
+constexpr uint32_t RING_STRIDE = RING_DUMMY + 16;
 constexpr uint32_t BURST = 1024;       // flush granule (64 lanes x 16 B)
 constexpr uint32_t CLS_ESC = 4, CLS_NONE = 5;
 
@@ -93,7 +90,7 @@ __device__ __forceinline__ uint32_t umin32(uint32_t a, uint32_t b) { return a < 
 // bytes [0, pb) at prim, the rest at slot (see vcfc_device.h; pb is a
 // multiple of BURST, so a burst lies wholly in one region).
 struct Ring {
-    vw::lds_u8 *lds;
+    uint8_t *lds;
     uint8_t *prim;
     uint8_t *slot;
     uint32_t wpos, fpos;
@@ -117,11 +114,15 @@ __device__ __forceinline__ void ring_put(Ring &r, uint32_t pos, uint32_t b) {
 // 0.68 GB are written amid the 10 GB input stream, so it does not stay
 // resident -- profiles/r03/ab/ab_staging_cache_policy.txt)
 __device__ __forceinline__ void ring_stage(Ring &r, uint32_t f, uint4 v) {
+#ifdef VCFC_DIAG_NOSTORE   // (diagnostic, wrong output: no staging stores)
+    if (f == 0x7FFFFFFFu) vw::gstore16_nt(r.prim, 0, v);
+    return;
+#endif
     if (r.fpos < r.pb) vw::gstore16_nt(r.prim, f, v);
     else vw::gstore16_nt(r.slot, f - r.pb, v);
 }
 __device__ __forceinline__ void ring_burst(Ring &r, uint32_t l) {
-    const uint4 v = vw::lds_load16(r.lds + ((r.fpos + 16u * l) & RMASK));
+    const uint4 v = *reinterpret_cast<const uint4 *>(r.lds + ((r.fpos + 16u * l) & RMASK));
     ring_stage(r, r.fpos + 16u * l, v);
     r.fpos += BURST;
 }
@@ -140,7 +141,7 @@ __device__ __forceinline__ void ring_flush(Ring &r, bool final) {
     if (final && r.wpos > r.fpos) {
         const uint32_t rem = r.wpos - r.fpos;  // < BURST
         if (16u * l < rem) {
-            const uint4 v = vw::lds_load16(r.lds + ((r.fpos + 16u * l) & RMASK));
+            const uint4 v = *reinterpret_cast<const uint4 *>(r.lds + ((r.fpos + 16u * l) & RMASK));
             ring_stage(r, r.fpos + 16u * l, v);
         }
         r.fpos = r.wpos;
@@ -252,11 +253,6 @@ struct FastState {
     uint32_t T, phi;    // token count, gt0's byte phase mod 4
     uint32_t pcls, prs; // class / run start(+1) of the previous token
     uint32_t esc;       // the last genotype chunk held an escape: test the escape shape first
-    // sparse clean path: a range of chunks [ev_tlo, ev_tlo + 512 ev_span)
-    // whose non-0|0 tokens (ev_m of them) wait in the LDS event list; pcls /
-    // prs then describe the token before ev_tlo
-    uint32_t ev_m, ev_span;
-    int32_t ev_tlo;
 };
 
 // Prefix phase for chunk c: 0 = no sample yet, 1 = first sample starts in
@@ -330,7 +326,7 @@ __device__ __forceinline__ int fast_prefix_step(const Chunk &cur, uint32_t c, ui
         const int32_t dq = (int32_t)(8u - lead) - (int32_t)e;
         const uint32_t pw = vw::shr1(cur.w(TPL - 1), 0u);
         const uint32_t sh = (4u - e) & 3u;
-        vw::lds_u32 *rd = (vw::lds_u32 *)r.lds;
+        uint32_t *rd = reinterpret_cast<uint32_t *>(r.lds);
         const uint32_t base = (uint32_t)((int32_t)bo + dq);
         // dword k holds ring bytes [base + 4k, +4) = lane bytes [4k - e, 4k - e + 4)
 #pragma unroll
@@ -369,7 +365,7 @@ __device__ __forceinline__ int fast_prefix_step(const Chunk &cur, uint32_t c, ui
 // General genotype step over one 1 KiB half-chunk (4 slots per lane):
 // escapes, the row's last token, anything the clean 2 KiB path rejects.
 // tf = token index of the half's first slot.  false = not the fast shape.
-__device__ __forceinline__ bool gt_general(const Chunk &cur, int32_t tf, FastState &f, Ring &r) {
+__device__ bool gt_general(const Chunk &cur, int32_t tf, FastState &f, Ring &r) {
     const uint32_t l = vw::lane_id();
     const uint32_t T = f.T, phi = f.phi;
     constexpr uint32_t Z = 0x09307C30u;   // "0|0\t"
@@ -599,119 +595,6 @@ __device__ __forceinline__ void clean8(const uint32_t (&d)[TPL8], int32_t t0, in
     ring_flush(r, false);
 }
 
-// ---------------------------------------------------------------------------
-// Sparse clean path.  At chr22 allele frequencies a clean 2 KiB chunk holds a
-// few dozen non-0|0 tokens among its 512, and clean8's run machinery costs the
-// same for every chunk.  Instead, a chunk with at most EV_MAX such tokens only
-// appends them ("events": token index << 2 | class) to a per-wave LDS list,
-// and ev_flush encodes a whole range of up to EV_SPAN chunks at once, one
-// event per lane: the tokens between events are 0|0 runs, so a lane's bytes
-// follow from its event, the previous one (DPP) and the run start (max-scan)
-// alone.  All-0|0 chunks inside a range add nothing.  Same emission rule as
-// clean8: [close of the previous run][full 0|0 bytes of the gap][close of the
-// gap's 0|0 run][this token's full byte].
-#ifndef VCFC_SPARSE
-#define VCFC_SPARSE 0   // (A/B pending: build_ab/sparse sets 1)
-#endif
-constexpr uint32_t EV_SPAN = 4;   // chunks per range: <= 2048 tokens, so <= 17 full 0|0 bytes per lane
-
-// floor(x / cap) for x < 2^23 (as mod_cap)
-__device__ __forceinline__ uint32_t div_cap(uint32_t x, bool is00) {
-    x &= 0x7FFFFFu;
-    const uint64_t p = (uint64_t)x * (is00 ? 8454661u : 8659209u);
-    return vw::alignbit((uint32_t)(p >> 32), (uint32_t)p, is00 ? 30u : 28u);
-}
-
-// Encode the pending range [ev_tlo, thi) (wave-uniform call, ev_span > 0).
-// Lane i < m holds event i (token t, class c in 1..3); lane m stands for the
-// range end (t = thi: no token of its own) and closes the range.
-__device__ __forceinline__ void ev_flush(FastState &f, Ring &r, int32_t thi) {
-    const uint32_t l = vw::lane_id();
-    const uint32_t m = f.ev_m;
-    vw::wave_sync();   // (the list was written by other lanes)
-    const uint32_t e = l < m ? ((const vw::lds_u32 *)(r.lds + RING_EV))[l] : 0u;
-    const bool own = l < m;
-    const int32_t t = own ? (int32_t)(e >> 2) : thi;
-    const uint32_t c = e & 3u;
-    uint32_t pc0 = f.pcls, prs = f.prs;
-    if (pc0 == CLS_NONE) {
-        // the row's first chunk: token 0 continues a virtual run of its own
-        // class begun at token 0 (as clean8)
-        const uint32_t e0 = vw::readlane(e, 0);
-        pc0 = (m > 0 && (e0 >> 2) == 0) ? (e0 & 3u) : 0u;
-        prs = 1;
-    }
-    // the token before this one: the previous event or, past a gap, a 0|0
-    const int32_t tp = (int32_t)vw::shr1((uint32_t)t, (uint32_t)(f.ev_tlo - 1));
-    const uint32_t cp = vw::shr1(c, pc0);   // class of the previous event (lane 0: of token ev_tlo - 1)
-    const int32_t g = t - tp - 1;           // 0|0 tokens between them
-    const bool start = own && (g > 0 ? 0u : cp) != c;
-    const uint32_t incl = vw::scan_max(start ? (uint32_t)t + 1u : 0u);
-    const uint32_t rs1 = vw::umax(incl, prs);              // start + 1 of this event's run
-    const uint32_t rsp = vw::umax(vw::shr1z(incl), prs);   // ... of the previous event's run (lane 0: entering)
-    // (a) the previous run [rsp - 1, tp] closes when a gap or a start follows it
-    const bool is00p = cp == 0;
-    const uint32_t pendA = mod_cap((uint32_t)(tp + 2 - (int32_t)rsp), is00p);
-    const bool leadA = (g > 0 ? !is00p : (g == 0 && start)) && pendA != 0;
-    // (b) the gap's 0|0 run [s0, t - 1] (s0: the entering 0|0 run's start if it continues it)
-    const int32_t s0 = is00p ? (int32_t)prs - 1 : tp + 1;
-    const uint32_t nf = g > 0 ? div_cap((uint32_t)(t - s0), true) - div_cap((uint32_t)(tp + 1 - s0), true) : 0u;
-    const uint32_t pendB = mod_cap((uint32_t)(t - s0), true);
-    const bool leadB = own && g > 0 && pendB != 0;
-    // (c) this token completes a chunk of 31 of its run
-    const bool fullC = own && mod_cap((uint32_t)(t + 1 - (int32_t)rs1), false) == 30u;
-    const uint32_t cnt = (leadA ? 1u : 0u) + nf + (leadB ? 1u : 0u) + (fullC ? 1u : 0u);
-    const uint32_t incl2 = vw::scan_add(cnt);
-    const uint32_t base = (r.wpos + incl2 - cnt) & RMASK;
-    vw::lds_u8 *const lb = r.lds + base;
-    vw::lds_u8 *const dm = r.lds + RING_DUMMY;
-    *(leadA ? lb : dm) = (uint8_t)(cls_mask_f(cp) | pendA);
-    uint32_t o = leadA ? 1u : 0u;
-    for (uint32_t k = 0; vw::ballot(k < nf); k++)
-        if (k < nf) lb[o + k] = 0x7Fu;
-    o += nf;
-    *(leadB ? lb + o : dm) = (uint8_t)pendB;
-    o += leadB ? 1u : 0u;
-    *(fullC ? lb + o : dm) = (uint8_t)(cls_mask_f(c) | 31u);
-    ring_unwrap(r, base + cnt);
-    r.wpos += vw::readlane(incl2, 63);
-    // the token before thi: lane m's view
-    f.pcls = vw::readlane(g > 0 ? 0u : cp, m);
-    f.prs = vw::readlane(g > 0 ? (uint32_t)(s0 + 1) : rsp, m);
-    f.ev_m = 0;
-    f.ev_span = 0;
-    ring_flush(r, false);
-}
-
-// A clean interior chunk: append its non-0|0 tokens to the event list.
-// EV_NO_ROOM: the pending range is full (EV_SPAN chunks, or too many events
-// for one more chunk) -- the caller closes it and appends again; EV_DENSE:
-// more than EV_MAX such tokens (clean8 takes the chunk).
-constexpr uint32_t EV_APPENDED = 0, EV_NO_ROOM = 1, EV_DENSE = 2;
-__device__ __forceinline__ uint32_t ev_append(const uint32_t (&d)[TPL8], int32_t t0, int32_t tf, FastState &f, Ring &r) {
-    const uint32_t cbL = class_bytes(d[0], d[1], d[2], d[3]), cbH = class_bytes(d[4], d[5], d[6], d[7]);
-    uint32_t nz = ~(zero_bytes4(cbL ^ 0x90909090u) | (zero_bytes4(cbH ^ 0x90909090u) << 4)) & 0xFFu;
-    const uint32_t cnt = (uint32_t)__builtin_popcount(nz);
-    const uint32_t inc = vw::scan_add(cnt);
-    const uint32_t tot = vw::readlane(inc, 63);
-    if (tot > EV_MAX) return EV_DENSE;
-    if (f.ev_span == EV_SPAN || f.ev_m + tot > EV_MAX) return EV_NO_ROOM;
-    if (f.ev_span == 0) f.ev_tlo = tf;
-    vw::lds_u32 *ev = (vw::lds_u32 *)(r.lds + RING_EV);
-    uint32_t o = f.ev_m + inc - cnt;
-    while (vw::ballot(nz != 0)) {
-        if (nz) {
-            const uint32_t j = vw::ffbl(nz);
-            const uint32_t cls = ((j < 4 ? cbL : cbH) >> (8u * (j & 3u))) & 3u;
-            ev[o++] = ((uint32_t)(t0 + (int32_t)j) << 2) | cls;
-            nz &= nz - 1u;
-        }
-    }
-    f.ev_m += tot;
-    f.ev_span++;
-    return EV_APPENDED;
-}
-
 // classes of four 3-byte tokens (byte j = 0x90 + 2a + b, or 0x94 for an
 // escape) and their escape mask (byte j = 0xFF for an escape)
 __device__ __forceinline__ void esc_classes(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3, uint32_t &cb,
@@ -801,12 +684,12 @@ __device__ __forceinline__ void esc8(const uint32_t (&d)[TPL8], int32_t t0, int3
     // dummy word, so the slots need no branches; an escape's four bytes
     // (0xE1 and its token) leave as one unaligned ds_write_b32.
     const uint32_t base = (r.wpos + incl2 - cnt) & RMASK;
-    vw::lds_u8 *const lb = r.lds + base;
+    uint8_t *const lb = r.lds + base;
     // Stores that emit nothing go to one dummy word shared by the wave:
     // same-address stores add no bank conflict, where a dummy word per lane
     // collides with the real stores of other lanes on the same banks (law 0:
     // 3.09 -> 2.64 ms k_encode in an A/B, profiles/r02/ab/ab_dummy_law0.txt).
-    vw::lds_u8 *const dm = r.lds + RING_DUMMY;
+    uint8_t *const dm = r.lds + RING_DUMMY;
     *(full ? lb : dm) = (uint8_t)(m0 | cap);
     uint32_t o = full ? 1u : 0u;
     // The first start's lead byte follows the full byte (nothing else comes
@@ -832,7 +715,7 @@ __device__ __forceinline__ void esc8(const uint32_t (&d)[TPL8], int32_t t0, int3
         r.lds[(uint32_t)vw::mad24(s, ldm + (int32_t)o, (int32_t)dmi)] = (uint8_t)b;
         o += (uint32_t)s;
         const uint32_t pay = (d[j] << 8) | 0xE1u;   // 0xE1, then the token's three bytes
-        vw::lds_store4u(r.lds + (uint32_t)vw::mad24(e, ldm + (int32_t)o, (int32_t)dmi), pay);
+        __builtin_memcpy(r.lds + (uint32_t)vw::mad24(e, ldm + (int32_t)o, (int32_t)dmi), &pay, 4);
         o += 4u * (uint32_t)e;
         njp = s ? -j : njp;
     }
@@ -879,10 +762,8 @@ __device__ __forceinline__ bool shape3(const uint32_t (&d)[TPL8], int32_t t0, ui
     return bad;
 }
 
-// Genotype chunk C (2 KiB) on the skip / sparse / clean / escape paths.
-// false = not handled (nothing written): the chunk needs the general step.
-// A pending sparse range is closed at one place (ev_flush is inlined once
-// for the whole step) before any path that needs the run state.
+// Genotype chunk C (2 KiB) on the skip / clean / escape paths.  false = not
+// handled (nothing written): the chunk needs the general step.
 __device__ __forceinline__ bool gt_step8(const Chunk8 &cur, uint32_t C, FastState &f, Ring &r) {
     const uint32_t l = vw::lane_id();
     const uint32_t T = f.T, phi = f.phi;
@@ -894,24 +775,30 @@ __device__ __forceinline__ bool gt_step8(const Chunk8 &cur, uint32_t C, FastStat
 #pragma unroll
     for (int j = 0; j < (int)TPL8; j++) d[j] = vw::alignbyte(j + 1 == (int)TPL8 ? ya : cur.w(j + 1), cur.w(j), phi);
     const int32_t t0 = tf + (int32_t)(TPL8 * l);
-    const bool pclean = f.pcls < CLS_ESC || f.pcls == CLS_NONE;   // (a pending range ends on a clean class)
-    // interior chunk: every slot a token, none of them the last.  After a
-    // chunk with escapes the next one most likely has some too (the
-    // random_vcf law: ~20 per chunk): test the escape shape alone.
-    const bool interior = tf + (int32_t)SLOTS8 < (int32_t)T;
-    bool clean = false;
-    [[maybe_unused]] uint32_t sp = EV_DENSE;
-    if (interior && !f.esc) {
+    const bool pclean = f.pcls < CLS_ESC || f.pcls == CLS_NONE;
+#ifdef VCFC_DIAG_NOSTEP   // (diagnostic, wrong output: the genotype stream without its step)
+    {
+        uint32_t x = 0;
+#pragma unroll
+        for (int j = 0; j < (int)TPL8; j++) x ^= d[j];
+        if (x == 0x12345678u) r.lds[RING_DUMMY] = (uint8_t)t0;
+        return true;
+    }
+#endif
+    if (tf + (int32_t)SLOTS8 < (int32_t)T) {
+        // interior chunk: every slot a token, none of them the last.  After
+        // a chunk with escapes the next one most likely has some too (the
+        // random_vcf law: ~20 per chunk): test the escape shape alone.
+        if (f.esc) {
+            if (vw::ballot(shape3<false>(d, t0, T)) == 0) {
+                esc8<false>(d, t0, tf, f, r);
+                return true;
+            }
+            return false;
+        }
         const uint32_t o = ((d[0] ^ Z) | (d[1] ^ Z)) | ((d[2] ^ Z) | (d[3] ^ Z)) |
                            ((d[4] ^ Z) | (d[5] ^ Z)) | ((d[6] ^ Z) | (d[7] ^ Z));
-        const bool zero = vw::ballot(o != 0) == 0;
-#if VCFC_SPARSE
-        if (zero && f.ev_span && f.ev_span < EV_SPAN) {   // all 0|0 inside a pending range: no events
-            f.ev_span++;
-            return true;
-        }
-#endif
-        if (zero && f.pcls == 0 && !f.ev_span) {
+        if (f.pcls == 0 && vw::ballot(o != 0) == 0) {
             // one 0|0 run through the whole chunk: only full 127-chunks
             // complete.  Token t has run offset t + 1 - prs; count the
             // multiples of 127 in [a0 + 1, a0 + 512].
@@ -922,30 +809,10 @@ __device__ __forceinline__ bool gt_step8(const Chunk8 &cur, uint32_t C, FastStat
             ring_flush(r, false);
             return true;
         }
-        clean = pclean && vw::ballot((o & 0xFFFEFFFEu) != 0) == 0;
-#if VCFC_SPARSE
-        if (clean) {
-            sp = ev_append(d, t0, tf, f, r);
-            if (sp == EV_APPENDED) return true;
-        }
+        if (pclean && vw::ballot((o & 0xFFFEFFFEu) != 0) == 0) {
+#ifdef VCFC_DIAG_CLEAN_SKIP   // (diagnostic, wrong output: the clean step costs nothing)
+            return true;
 #endif
-    }
-#if VCFC_SPARSE
-    if (f.ev_span) ev_flush(f, r, tf);   // the pending range ends where this chunk starts
-    if (sp == EV_NO_ROOM) {              // (now there is)
-        ev_append(d, t0, tf, f, r);
-        return true;
-    }
-#endif
-    if (interior) {
-        if (f.esc) {
-            if (vw::ballot(shape3<false>(d, t0, T)) == 0) {
-                esc8<false>(d, t0, tf, f, r);
-                return true;
-            }
-            return false;
-        }
-        if (clean) {
             clean8<false>(d, t0, tf, f, r);
             return true;
         }
@@ -984,7 +851,6 @@ __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring
     const uint32_t lo16 = BPL * l;
     FastState f;
     f.nf = 0; f.carryT = 1; f.gt0 = -1; f.T = 0; f.phi = 0; f.pcls = CLS_NONE; f.prs = 0; f.esc = 0;
-    f.ev_m = 0; f.ev_span = 0; f.ev_tlo = 0;
     r.wpos = 8;
     r.fpos = 0;
 
@@ -1045,7 +911,6 @@ __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring
         C0 = vw::readfirst(gen + 1);
         if (C0 >= ncG) break;
     }
-    // (no sparse range is pending here: the last chunk closes it)
     const uint32_t pcls = f.pcls, prs = f.prs;
     const int32_t gt0 = f.gt0;
     // row end: pending chunk of the last run, then '\n'
@@ -1123,7 +988,7 @@ __device__ __forceinline__ uint32_t odd2(uint32_t z) { return ((z >> 1) & 1u) | 
 // full burst starts on a 1 KiB boundary).
 __device__ __forceinline__ void ring_half_burst(Ring &r, uint32_t l) {
     if (l < 32) {
-        const uint4 v = vw::lds_load16(r.lds + ((r.fpos + 16u * l) & RMASK));
+        const uint4 v = *reinterpret_cast<const uint4 *>(r.lds + ((r.fpos + 16u * l) & RMASK));
         ring_stage(r, r.fpos + 16u * l, v);
     }
     r.fpos += BURST / 2;
@@ -1369,7 +1234,6 @@ __device__ bool encode_var(const uint8_t *__restrict__ line, uint32_t len, Ring 
     const uint32_t lo16 = BPL * l;
     VarState f;
     f.nf = 0; f.carryT = 1; f.gt0 = -1; f.T = 0; f.phi = 0; f.pcls = CLS_NONE; f.prs = 0; f.esc = 0; f.ntok = 0;
-    f.ev_m = 0; f.ev_span = 0; f.ev_tlo = 0;
     r.wpos = 8;
     r.fpos = 0;
     // prefix phase: as encode_fast
@@ -1501,8 +1365,8 @@ __device__ uint32_t encode_general(const uint8_t *__restrict__ line, uint32_t le
                 const uint32_t cnt = (uint32_t)__builtin_popcount(in16) + 2u * nfs;
                 const uint32_t inc2 = vw::scan_add(cnt);
                 const uint32_t base = (r.wpos + inc2 - cnt) & RMASK;
-                vw::lds_u8 *const lb = r.lds + base;
-                vw::lds_u8 *const dm = r.lds + RING_DUMMY;   // shared dummy word (see esc8)
+                uint8_t *const lb = r.lds + base;
+                uint8_t *const dm = r.lds + RING_DUMMY;   // shared dummy word (see esc8)
                 uint32_t o = 0;
 #pragma unroll
                 for (int i = 0; i < 16; i++) {
@@ -1611,8 +1475,8 @@ __device__ uint32_t encode_general(const uint8_t *__restrict__ line, uint32_t le
                              (uint32_t)__builtin_popcount(MID);
         const uint32_t inc2 = vw::scan_add(cnt);
         const uint32_t base = (r.wpos + inc2 - cnt) & RMASK;
-        vw::lds_u8 *const lb = r.lds + base;
-        vw::lds_u8 *const dm = r.lds + RING_DUMMY;   // shared dummy word (see esc8)
+        uint8_t *const lb = r.lds + base;
+        uint8_t *const dm = r.lds + RING_DUMMY;   // shared dummy word (see esc8)
         // pass 1: the raw bytes, each at its place after the bytes inserted before it
         uint32_t o = 0;
 #pragma unroll
@@ -1678,7 +1542,7 @@ __device__ uint32_t encode_general(const uint8_t *__restrict__ line, uint32_t le
 
 // Row prologue shared by both encode kernels: slot bounds check + ring setup.
 __device__ __forceinline__ bool row_setup(const VcfcEncodeArgs &a, uint64_t row, uint8_t *lds, Ring &r) {
-    r.lds = vw::lds(lds);
+    r.lds = lds;
     r.pb = a.prim_bytes;
     r.prim = a.prim + (uint64_t)a.prim_bytes * row;
     r.slot = a.slots + a.slot_off[row];
@@ -2088,9 +1952,13 @@ __global__ __launch_bounds__(256) void k_scan_lb(const uint32_t *__restrict__ in
 // Per-call state of one encode: the look-back tickets and tile flags zeroed,
 // the first-error word set to "none".  A kernel rather than two
 // hipMemsetAsync calls: replays of a HIP graph captured around
-// vcfc_encode_device did not re-run the captured memsets (the second replay
-// found the previous replay's tickets and its look-back spun; tools/dbg/
-// graph_probe.py), and a kernel node is replayed like every other launch.
+// vcfc_encode_device spun in the look-back on the second replay
+// (tools/dbg/graph_probe.py).  Round 4 pinned the cause
+// (tools/dbg/memset_graph_probe.py, profiles/r04/memset_graph_probe.txt):
+// memset nodes of 4 and 8 bytes replay correctly, but a 24-byte node writes
+// garbage into its first 16 bytes from the second replay on, consistent
+// with the hang (the ticket array's memset, far more than 8 bytes, did not
+// leave zeros).  A kernel node is replayed like every other launch.
 __global__ __launch_bounds__(256) void k_encode_reset(uint64_t *lb, uint64_t words, uint64_t *err) {
     for (uint64_t i = threadIdx.x; i < words; i += 256) lb[i] = 0;
     if (threadIdx.x == 0) *err = ~0ull;

@@ -190,22 +190,6 @@ __device__ __forceinline__ uint32_t bload4(brsrc r, uint32_t off, const int aux 
     return aux == 2 ? __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 2)
                     : __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
 }
-// LDS through address-space-3 pointers: byte addresses stay 32-bit, so a
-// store address computed as base + a * b is one v_mad_u32_u24.  Through a
-// generic pointer hipcc folds the multiply into a 64-bit address
-// (v_mad_u64_u32, a quarter-rate instruction) before it narrows the address
-// for the ds_write.
-typedef __attribute__((address_space(3))) uint8_t lds_u8;
-typedef __attribute__((address_space(3))) uint32_t lds_u32;
-typedef __attribute__((address_space(3), aligned(1))) uint32_t lds_u32u;   // any byte address
-typedef __attribute__((address_space(3))) v4u lds_v4u;
-__device__ __forceinline__ lds_u8 *lds(void *p) { return (lds_u8 *)p; }
-__device__ __forceinline__ uint4 lds_load16(const lds_u8 *p) {
-    const v4u v = *(const lds_v4u *)p;
-    return make_uint4(v.x, v.y, v.z, v.w);
-}
-__device__ __forceinline__ void lds_store4u(lds_u8 *p, uint32_t v) { *(lds_u32u *)p = v; }
-
 // Keep just-issued prefetch loads where they are: the memory clobber stops
 // LLVM from sinking them towards their (next-iteration) use, which would
 // shrink the prefetch distance to zero.  Emits no instruction.
