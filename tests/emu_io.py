@@ -167,6 +167,15 @@ def emu_compress_device(vcf, chunk=4096, cap=None, max_chunk=0, hop=True, redo=N
     return st, out[:n.value].tobytes(), el.value
 
 
+def emu_hop_read(reset=True):
+    """Bytes the hop line index's walkers loaded since the last reset (the
+    emulator's VCFC_DIAG_HOP_READ counter)."""
+    L = lib()
+    L.emu_hop_read.restype = ctypes.c_ulonglong
+    L.emu_hop_read.argtypes = [ctypes.c_int]
+    return int(L.emu_hop_read(1 if reset else 0))
+
+
 def emu_line_index(vcf, S_hint=0):
     """The GPU line index of vcf (ending in '\n') on the emulator: (counts
     [lines, data lines, pass lines, long], data line offsets, lengths)."""

@@ -98,3 +98,40 @@ def chr22_like(rnd, n_rows, S, prefix_jitter=40):
         if i == 11:
             lines.append(b"")
     return b"\n".join(lines) + b"\n"
+
+
+def law2_like(rnd, n_rows, S, kinds=(0, 1, 2, 3, 4), dp_width=2):
+    """Rows shaped like bench.py --law 2: per row one kind --
+    0 haploid "0"/"1" for a fixed half of the samples beside "a|b", 1
+    "a|b:DP:GQ" (DP and GQ of dp_width digits; 0 = widths vary per token), 2 / 3
+    3-byte tokens ("./." or unphased), 4 "." for a fixed fifth of the
+    samples -- with '##' lines among them.  Kinds 0, 1 (fixed width) and 4 repeat
+    one genotype-region length per kind: the hop index's TRY candidates."""
+    male = [rnd.random() < 0.5 for _ in range(S)]
+    miss = [rnd.random() < 0.2 for _ in range(S)]
+    lines = D.header(S).rstrip(b"\n").split(b"\n")
+    for i in range(n_rows):
+        kind = rnd.choice(kinds)
+        toks = []
+        for j in range(S):
+            a, b = rnd.randrange(2), rnd.randrange(2)
+            if kind == 0 and male[j]:
+                toks.append(b"%d" % a)
+            elif kind == 4 and miss[j]:
+                toks.append(b".")
+            elif kind == 1:
+                w = dp_width or rnd.choice([1, 2, 3])
+                lo, hi = 10 ** (w - 1), 10 ** w - 1
+                toks.append(b"%d|%d:%d:%d" % (a, b, rnd.randint(lo, hi), rnd.randint(lo, hi)))
+            elif kind == 2:
+                toks.append(b"./." if rnd.random() < 0.3 else b"%d|%d" % (a, b))
+            elif kind == 3:
+                toks.append(b"%d/%d" % (a, b))
+            else:
+                toks.append(b"%d|%d" % (a, b))
+        fmt = b"GT:DP:GQ" if kind == 1 else b"GT"
+        lines.append(b"\t".join([b"X", b"%d" % (2781479 + 37 * i), b".", b"A", b"G", b"50", b"PASS",
+                                 b"AC=%d;KIND=%d" % (rnd.randrange(1000), kind), fmt] + toks))
+        if i % 23 == 7:
+            lines.append(b"##mid=%d" % i)
+    return b"\n".join(lines) + b"\n"

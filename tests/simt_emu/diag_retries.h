@@ -6,3 +6,6 @@
 #define VCFC_DIAG_GENERAL_ROW(a) \
     if (vw::lane_id() == 0) atomicAdd((a).retry_count, 1u)
 #define VCFC_DIAG_WS_BYTES(n) 0ull
+// bytes the hop line index's walkers load (k_nl_hop), summed per process
+void emu_diag_hop_read(unsigned long long bytes);
+#define VCFC_DIAG_HOP_READ(bytes) emu_diag_hop_read((unsigned long long)(bytes))

@@ -9,6 +9,16 @@
 #include "vcfc_device.h"
 #include "vcfc_decode_driver.h"
 #include "emu.h"
+#include <atomic>
+
+// bytes the hop line index's walkers loaded (VCFC_DIAG_HOP_READ, diag_retries.h)
+static std::atomic<unsigned long long> g_hop_read{0};
+void emu_diag_hop_read(unsigned long long bytes) { g_hop_read += bytes; }
+extern "C" unsigned long long emu_hop_read(int reset) {
+    const unsigned long long v = g_hop_read.load();
+    if (reset) g_hop_read = 0;
+    return v;
+}
 
 extern "C" int emu_encode_rows(const uint8_t *buf, const uint64_t *line_off, const uint32_t *line_len,
                                uint64_t n, uint8_t *out, uint64_t out_cap, uint64_t *rec_off,

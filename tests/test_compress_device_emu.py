@@ -12,7 +12,7 @@ import pytest
 import emu_io as E
 import golden_io as G
 import test_ingest_emu as T
-from hop_cases import chr22_like, hop_trap_dense_segment, hop_trap_file
+from hop_cases import chr22_like, hop_trap_dense_segment, hop_trap_file, law2_like
 
 OK, E_ARG = 0, 5
 
@@ -176,3 +176,26 @@ def test_hop_index_long_header():
         st_o, want, _ = G.oracle_compress(vcf)
         assert st == st_o == OK and out == want
         assert redo == [1]
+
+
+@pytest.mark.parametrize("S,dp_width", [(300, 2), (700, 2), (300, 0)])
+def test_hop_index_law2_rows(S, dp_width):
+    """Law-2-shaped files (hop_cases.law2_like: haploid, GT:DP:GQ, '.', '#'
+    lines): the hop index's learned candidates (TRY / LEARN) give exactly the
+    scan index's tables, and the walkers read far less than the file when the
+    genotype-region lengths repeat per row kind (dp_width 2); with DP/GQ of
+    random widths (dp_width 0) the GT:DP:GQ rows are found by FIND and
+    nothing breaks."""
+    rnd = random.Random(S + dp_width)
+    vcf = law2_like(rnd, 240, S, dp_width=dp_width)
+    E.emu_hop_read()
+    hop = E.emu_line_index(vcf, S)
+    read = E.emu_hop_read()
+    assert hop == E.emu_line_index(vcf, 0)
+    if dp_width:
+        # (240 rows over ~12 walkers of 2 segments each: learning the three
+        # row kinds is a large share here; the 13 GB GPU file spreads it over
+        # ~120 rows per wave)
+        assert read < 0.8 * len(vcf), (read, len(vcf))
+    for chunk in (1 << 16, 1 << 22):
+        check(vcf, chunk, "law2-like S=%d" % S)

@@ -1064,6 +1064,33 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
         int32_t ro = (int32_t)base - dmi;
         const uint32_t vm2 = vm & ~(lastin ? (1u << lastrel) : 0u);
 #ifndef VCFC_VAR_SIZE_ONLY   // (diagnostic: the cost of a size-only pass, wrong output)
+        if (vw::ballot(vm != 0xFFFFu) == 0) {
+            // Interior chunk (every half valid, none the row's last): half h's
+            // two bytes sit at lane offset 2h + c_h, c_h = starts in halves
+            // 0..h, and its 0xE1 (a start) just before them.  Half h's 0xE1
+            // store is issued before half h-1's second byte: when h starts
+            // nothing that is exactly where it lands, so the byte store after
+            // it rewrites it (same lane, later instruction) -- no per-store
+            // dummy select; half 0's goes to the dummy word unless it is a
+            // start (its slot would be the previous lane's last byte).  The
+            // bytes come straight from the dwords (ds_write_b8 / _d16_hi):
+            // ~3 VALU per half instead of ~10.
+            uint32_t a = base;   // base + c_{h-1}
+            r.lds[(S & 1u) ? base : RING_DUMMY] = (uint8_t)0xE1u;
+            a += S & 1u;
+            r.lds[a] = (uint8_t)d[0];
+            uint32_t hi8 = d[0] >> 8;
+#pragma unroll
+            for (int h = 1; h < 16; h++) {
+                const uint32_t an = a + ((S >> h) & 1u);
+                r.lds[an + 2u * h - 1u] = (uint8_t)0xE1u;
+                r.lds[a + 2u * h - 1u] = (uint8_t)((h & 1) ? hi8 : (hi8 >> 16));   // half h-1's second byte
+                r.lds[an + 2u * h] = (uint8_t)((h & 1) ? (d[h >> 1] >> 16) : d[h >> 1]);
+                if (!(h & 1)) hi8 = d[h >> 1] >> 8;
+                a = an;
+            }
+            r.lds[a + 31u] = (uint8_t)(hi8 >> 16);   // half 15's second byte
+        } else {
 #pragma unroll
         for (int h = 0; h < 16; h++) {
             const int32_t es = (int32_t)((S >> h) & 1u);
@@ -1074,6 +1101,7 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
             r.lds[(uint32_t)vw::mad24(e1, ro, dmi)] = (uint8_t)pay;
             r.lds[(uint32_t)vw::mad24(e2, ro + 1, dmi)] = (uint8_t)(pay >> 8);
             ro += e1 + e2;
+        }
         }
 #endif
         ring_unwrap(r, base + cnt);
@@ -1614,7 +1642,7 @@ constexpr uint32_t VAR_ROWS = 32;
 // (round 2 ran it as a kernel of its own, k_encode_general: one more launch,
 // ~4.5 us on the headline rows, which flag none).  A resident grid striding
 // over rows was 13.6 % slower on law 2 (profiles/r02/ab/ab_gen_persist.txt).
-__global__ __launch_bounds__(256) void k_encode_var(VcfcEncodeArgs a, uint64_t row_lo, uint64_t row_hi) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) void k_encode_var(VcfcEncodeArgs a, uint64_t row_lo, uint64_t row_hi) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[K1_WAVES * RING_STRIDE];
     const uint32_t wave = vw::readfirst(threadIdx.x >> 6);
     const uint32_t l = vw::lane_id();

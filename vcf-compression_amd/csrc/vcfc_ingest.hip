@@ -29,6 +29,15 @@
 #include <vcfc_wave.h>   // angle brackets: tests/simt_emu shadows it
 #include "vcfc_device.h"
 
+// Diagnostic builds (tests/simt_emu) pass -DVCFC_DIAG='"hooks.h"'; the
+// product build defines the hook empty.
+#ifdef VCFC_DIAG
+#include VCFC_DIAG
+#endif
+#ifndef VCFC_DIAG_HOP_READ
+#define VCFC_DIAG_HOP_READ(bytes)   // bytes a walker loads in one round (emulator diagnostics)
+#endif
+
 namespace {
 
 constexpr uint32_t SEG = 16384;          // bytes per wave
@@ -124,19 +133,34 @@ __global__ __launch_bounds__(256) void k_nl_scan(const uint8_t *buf, uint64_t n,
 //           is '\n' and the 31 bytes 4, 8, ..., 124 before it are TABs; if
 //           the guess window missed e, VERIFY loads the 256 bytes ending at e
 //           next round.  No 9th TAB in MW < 1024 bytes: the line again with
-//           1 KiB.  '#' lines, prefixes over 1 KiB, a failed check: FIND.
+//           1 KiB.  '#' lines, prefixes over 1 KiB, a failed check: TRY, or
+//           FIND when there is nothing to try.
+//   TRY     (round 4) genotype regions of other lengths: the walker keeps
+//           HOP_K learned candidates -- a region length G and the TAB mask of
+//           the 256 bytes ending at that line's '\n' -- and tries them in
+//           turn: taken when the window ending at gt0 + G holds exactly that
+//           TAB mask and its only '\n' is the last byte.  Rows whose token
+//           lengths are a per-column trait (haploid males, '.' for the same
+//           samples) or fixed-width (GT:DP:GQ with two-digit DP/GQ) repeat
+//           one G per row kind, so a law-2 file is hopped too.
 //   FIND    the next 1 KiB scanned for its first '\n' (also the walker's
 //           start: the first '\n' at or after its span's first byte - 1).
+//   LEARN   after FIND ended a data line whose region is >= 256 bytes: the
+//           256 bytes ending at its '\n' become a candidate (round robin).
+// A walker whose TRYs keep failing (HOP_TRUST misses more than hits) stops
+// trying and learning: lines of random lengths cost what they did before.
 // Loads are 16 B per lane over contiguous 256-byte rows (coalesced).  A
 // chr22-shaped file is read for ~0.5 KiB per line instead of every byte.
 // A line predicted across a '\n' it did not see (a shorter line whose guessed
-// end lands on a later line's '\n' with TABs at the 31 checked places) is
+// end lands on a later line's '\n' with TABs at the checked places) is
 // caught by the encoder (VcfcEncodeArgs::nl_check), and the chunk is indexed
 // again by k_nl_scan.
 constexpr uint32_t HOPW = 4;                   // walkers per wave
 constexpr uint64_t HOP_WALKERS = 32768;   // (devfile step: 16384 +1.2 %, 8192 +4.6 %)
 constexpr uint32_t GW = 256;                   // guess window (16 B per lane)
-constexpr uint32_t HOP_LINE = 0, HOP_VERIFY = 1, HOP_FIND = 2, HOP_DONE = 3;
+constexpr uint32_t HOP_LINE = 0, HOP_VERIFY = 1, HOP_FIND = 2, HOP_DONE = 3, HOP_TRY = 4, HOP_LEARN = 5;
+constexpr uint32_t HOP_K = 3;                  // learned candidates per walker
+constexpr uint32_t HOP_TRUST = 8;              // TRY credit: +1 per hit (capped), -1 per all-miss
 
 // 16 bytes at p (bytes at or past n read as 0)
 __device__ __forceinline__ uint4 load16(const uint8_t *buf, uint64_t n, uint64_t p) {
@@ -172,6 +196,11 @@ __global__ __launch_bounds__(256) void k_nl_hop(const uint8_t *buf, uint64_t n, 
     uint64_t p = 0, q = lo == 0 ? 0 : lo - 1, e = 0;
     uint32_t pl = 0, rows = 4;          // previous prefix length; 256-byte rows of the next LINE window
     uint32_t cur = 0, cc = 0;           // current segment (in the span) and its count
+    // learned candidates (walker-uniform lengths; this lane's 16-bit TAB mask of each)
+    uint32_t cg[HOP_K] = {0, 0, 0}, csig[HOP_K] = {0, 0, 0};
+    uint32_t tk = 0, ins = 0, trust = HOP_TRUST;
+    uint64_t gt = 0;                    // the current data line's gt0 (lrn: it may be learned)
+    bool lrn = false;
     auto record = [&](uint64_t x) {     // (the walker's lanes; lo <= x < hi, in order)
         const uint32_t k = (uint32_t)((x - lo) / SEG);
         for (; cur < k; cur++, cc = 0)
@@ -180,22 +209,38 @@ __global__ __launch_bounds__(256) void k_nl_hop(const uint8_t *buf, uint64_t n, 
         cc++;
     };
     auto wbits = [&](bool pr) { return (uint32_t)(vw::ballot(pr) >> sh) & 0xFFFFu; };
+    // the first candidate at or after k (HOP_K: none), trusted walkers only
+    auto next_cand = [&](uint32_t k) {
+        for (; k < HOP_K; k++)
+            if (cg[k] && trust) break;
+        return k;
+    };
+    // a failed prediction: the candidates, else FIND from fq
+    auto to_try = [&](uint64_t fq) {
+        q = fq;
+        tk = lrn ? next_cand(0) : HOP_K;
+        mode = tk < HOP_K ? HOP_TRY : HOP_FIND;
+    };
     while (vw::ballot(mode != HOP_DONE)) {
+        const uint32_t mode0 = mode;   // (the round's mode: the steps below may switch it for the next round)
         // ---- loads: the main window (LINE: `rows` rows, FIND: 4), the guess window ----
         const uint64_t base = mode == HOP_FIND ? q : p;
         const uint32_t nr = mode == HOP_FIND ? 4u : mode == HOP_LINE ? rows : 0u;
         uint4 v[4];
 #pragma unroll
         for (uint32_t k = 0; k < 4; k++) v[k] = k < nr ? load16(buf, n, base + 256u * k + 16u * wl) : make_uint4(0, 0, 0, 0);
-        uint64_t g0 = 0;
+        uint64_t g0 = 0, ek = 0;
         if (mode == HOP_LINE) {
             const uint64_t x = p + pl + 4ull * S - 1;   // the end if the prefix is as long as the last one
             g0 = x >= GW / 2 + 62 ? x - (GW / 2 + 62) : 0;
-        } else if (mode == HOP_VERIFY) {
-            g0 = e + 1 >= GW ? e + 1 - GW : 0;
+        } else if (mode == HOP_VERIFY || mode == HOP_LEARN || mode == HOP_TRY) {
+            // (TRY: the candidate's end; VERIFY / LEARN: e)
+            ek = mode == HOP_TRY ? gt + (tk == 0 ? cg[0] : tk == 1 ? cg[1] : cg[2]) : e;
+            g0 = ek + 1 >= GW ? ek + 1 - GW : 0;
         }
-        const bool gv = (mode == HOP_LINE || mode == HOP_VERIFY) && g0 + GW <= n;
+        const bool gv = mode != HOP_FIND && mode != HOP_DONE && g0 + GW <= n && (mode == HOP_LINE || ek + 1 >= GW);
         const uint4 ga = gv ? *reinterpret_cast<const uint4 *>(buf + g0 + 16u * wl) : make_uint4(0, 0, 0, 0);
+        if (l == w0 && mode != HOP_DONE) VCFC_DIAG_HOP_READ(256u * nr + (gv ? GW : 0u));
         // ---- the first '\n' of the main window (row-major: row k, then lane) ----
         uint64_t first = ~0ull;
 #pragma unroll
@@ -211,7 +256,45 @@ __global__ __launch_bounds__(256) void k_nl_hop(const uint8_t *buf, uint64_t n, 
             if (first != ~0ull) { e = first; found = true; }
             else if (q + 1024 >= n) { e = n - 1; found = true; }   // (buf[n - 1] is '\n')
             else q += 1024;
+            // a data line the candidates did not know: learn its region
+            if (found && lrn && trust && e >= gt + GW - 1) { found = false; mode = HOP_LEARN; }
         }
+        // ---- TRY / LEARN: the window ending at ek ----
+        const uint32_t gtm = tab_mask_v(ga), gnl = nl_mask_v(ga);
+        const uint32_t sig = tk == 0 ? csig[0] : tk == 1 ? csig[1] : csig[2];
+        const bool tok = gv && ek < n && gtm == sig && gnl == (wl == 15 ? 0x8000u : 0u);
+        const bool thit = wbits(!tok) == 0;   // (collectives stay wave-uniform)
+        if (mode == HOP_TRY) {
+            if (thit) {
+                e = ek; found = true;
+                trust = trust < HOP_TRUST ? trust + 1 : trust;
+            } else {
+                tk = next_cand(tk + 1);
+                if (tk >= HOP_K) {
+                    mode = HOP_FIND;   // (q: where the prediction left it)
+                    trust = trust ? trust - 1 : 0;
+                }
+            }
+        }
+        // LEARN: every walker of the wave takes the lowest learner's candidate
+        // (a law-2 row kind is learned once per wave, not once per walker),
+        // a learner also its own; a length already held is not taken again
+        auto insert = [&](uint32_t G, uint32_t sg) {
+            if (G == cg[0] || G == cg[1] || G == cg[2]) return;
+            if (ins == 0) { cg[0] = G; csig[0] = sg; }
+            else if (ins == 1) { cg[1] = G; csig[1] = sg; }
+            else { cg[2] = G; csig[2] = sg; }
+            ins = ins + 1 == HOP_K ? 0u : ins + 1;
+        };
+        const uint64_t lm = vw::ballot(mode0 == HOP_LEARN && gv);
+        if (lm) {
+            const uint32_t sw0 = (uint32_t)__builtin_ctzll(lm) & ~15u;
+            const uint32_t Gown = (uint32_t)(e - gt);
+            const uint32_t Gs = vw::shfl(Gown, sw0), ss = vw::shfl(gtm, sw0 + wl);
+            insert(Gs, ss);
+            if (mode0 == HOP_LEARN && gv) insert(Gown, gtm);
+        }
+        if (mode0 == HOP_LEARN) found = true;
         // ---- LINE: the 9th TAB, the predicted end ----
         uint32_t t9 = ~0u, acc = 0;
 #pragma unroll
@@ -233,6 +316,7 @@ __global__ __launch_bounds__(256) void k_nl_hop(const uint8_t *buf, uint64_t n, 
         }
         const uint32_t b0 = vw::shfl(v[0].x & 0xFFu, w0);
         if (mode == HOP_LINE) {
+            lrn = false;
             if (first != ~0ull) { e = first; found = true; }
             else if (S == 0 || b0 == '#') { mode = HOP_FIND; q = p + 256u * rows; }
             else if (t9 == ~0u) {
@@ -242,14 +326,16 @@ __global__ __launch_bounds__(256) void k_nl_hop(const uint8_t *buf, uint64_t n, 
                 pl = t9 + 1;
                 const uint32_t want = pl + 96;
                 rows = want <= 256 ? 1u : want <= 512 ? 2u : 4u;
+                gt = p + t9 + 1;
+                lrn = true;
                 e = p + t9 + 4ull * S;   // gt0 + 4 S - 1
-                if (e >= n) { mode = HOP_FIND; q = p + 256u * nr; }
+                if (e >= n) to_try(p + 256u * nr);
                 else if (gv && e >= g0 + 124 && e < g0 + GW) check = true;
                 else mode = HOP_VERIFY;
             }
         } else if (mode == HOP_VERIFY) {
             if (gv && e >= g0 + 124) check = true;
-            else { mode = HOP_FIND; q = p; }
+            else to_try(p);
         }
         // ---- the check: byte e is '\n', bytes e - 4 i (i = 1..31) TABs ----
         bool bad = false;
@@ -266,7 +352,7 @@ __global__ __launch_bounds__(256) void k_nl_hop(const uint8_t *buf, uint64_t n, 
         const bool bw = wbits(bad) != 0;
         if (check) {
             if (!bw) found = true;
-            else { mode = HOP_FIND; q = p + 256u * nr; }   // (past the first window: no '\n' there)
+            else to_try(p + 256u * nr);   // (past the first window: no '\n' there)
         }
         // ---- the line end: record, next line ----
         if (found) {
