@@ -37,7 +37,7 @@ def lib():
         L.emu_compress_device.argtypes = [ctypes.c_char_p, u64, vp, u64, ctypes.POINTER(u64),
                                           ctypes.POINTER(ctypes.c_int64), u64, u64, ctypes.c_int,
                                           ctypes.POINTER(u64)]
-        L.emu_line_index.argtypes = [ctypes.c_char_p, u64, ctypes.c_uint32, vp, vp, u64, vp]
+        L.emu_line_index.argtypes = [ctypes.c_char_p, u64, ctypes.c_uint32, vp, vp, u64, vp, u64]
         L.emu_synth.argtypes = [vp, vp, u64, vp, vp, vp, ctypes.c_uint32, ctypes.c_int, u64]
         _lib = L
     return _lib
@@ -154,14 +154,15 @@ def emu_compress(vcf, chunk=4096, read_threads=2, cap=None, max_chunk=0):
 def emu_compress_device(vcf, chunk=4096, cap=None, max_chunk=0, hop=True, redo=None):
     """compress() of device-resident bytes (vcfc_ing::compress_device) on the
     emulator: (status, bytes, err_line).  hop: the hop line index when the
-    header gives S; redo (a list): gets the count of chunks indexed again."""
+    header gives S (True; "learn" / "nolearn" force its learned candidates on
+    or off); redo (a list): gets the count of chunks indexed again."""
     cap = cap or 2 * len(vcf) + 4096
     out = np.zeros(cap, dtype=np.uint8)
     n = ctypes.c_uint64(0)
     el = ctypes.c_int64(-1)
     r = ctypes.c_uint64(0)
     st = lib().emu_compress_device(vcf, len(vcf), out.ctypes.data, cap, ctypes.byref(n), ctypes.byref(el), chunk,
-                                   max_chunk, 1 if hop else 0, ctypes.byref(r))
+                                   max_chunk, {"learn": 2, "nolearn": 3}.get(hop, 1 if hop else 0), ctypes.byref(r))
     if redo is not None:
         redo.append(r.value)
     return st, out[:n.value].tobytes(), el.value
@@ -176,14 +177,18 @@ def emu_hop_read(reset=True):
     return int(L.emu_hop_read(1 if reset else 0))
 
 
-def emu_line_index(vcf, S_hint=0):
+def emu_line_index(vcf, S_hint=0, hop_walkers=0):
     """The GPU line index of vcf (ending in '\n') on the emulator: (counts
-    [lines, data lines, pass lines, long], data line offsets, lengths)."""
+    [lines, data lines, pass lines, long], data line offsets, lengths).
+    hop_walkers: walkers of the hop index (0: the product's count)."""
     cap = vcf.count(b"\n") + 1
     off = np.zeros(cap, dtype=np.uint64)
     ln = np.zeros(cap, dtype=np.uint32)
     cnt = np.zeros(4, dtype=np.uint64)
-    st = lib().emu_line_index(vcf, len(vcf), S_hint, off.ctypes.data, ln.ctypes.data, cap, cnt.ctypes.data)
+    L = lib()
+    L.emu_line_index.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                 ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64]
+    st = L.emu_line_index(vcf, len(vcf), S_hint, off.ctypes.data, ln.ctypes.data, cap, cnt.ctypes.data, hop_walkers)
     assert st == 0
     k = int(cnt[1])
     return [int(c) for c in cnt], off[:k].tolist(), ln[:k].tolist()

@@ -180,7 +180,8 @@ extern "C" int emu_compress_device(const uint8_t *in, uint64_t n, uint8_t *out, 
     vcfc_ing::Config cfg;
     cfg.chunk = chunk;
     if (max_chunk) cfg.max_chunk = max_chunk;
-    cfg.hop_index = hop != 0;
+    cfg.hop_index = hop != 0;            // hop: 0 scan, 1 hop (learning when the first lines need it),
+    cfg.hop_learn = hop == 2 ? 1 : hop == 3 ? 0 : -1;   // 2 hop learning, 3 hop without learning
     cfg.hop_redo = hop_redo;
     return vcfc_ing::compress_device(in, n, out, cap, out_len, M, nullptr, cfg, err_line);
 }
@@ -217,14 +218,14 @@ extern "C" int emu_held(const uint8_t *data, uint64_t n, uint64_t piece, uint64_
 // The line index (csrc/vcfc_ingest.hip) of in[0, n) (last byte '\n'): the
 // data lines' offsets and lengths and the counts; S_hint != 0: the hop index.
 extern "C" int emu_line_index(const uint8_t *in, uint64_t n, uint32_t S_hint, uint64_t *off, uint32_t *len,
-                              uint64_t cap, uint64_t *counts) {
+                              uint64_t cap, uint64_t *counts, uint64_t hop_walkers) {
     const VcfcLineIndexLayout L1 = vcfc_line_index_layout(n, 0);
     std::vector<uint8_t> ws1(L1.total1 + 64);
     std::vector<uint64_t> cnt(4, 0);
     VcfcLineIndex x;
     memset(&x, 0, sizeof x);
     x.counts = cnt.data();
-    if (vcfc_line_index(in, n, ws1.data(), L1, x, nullptr, S_hint) != hipSuccess) return 1;
+    if (vcfc_line_index(in, n, ws1.data(), L1, x, nullptr, S_hint, hop_walkers) != hipSuccess) return 1;
     const uint64_t lines = cnt[0];
     const VcfcLineIndexLayout L = vcfc_line_index_layout(n, lines);
     std::vector<uint8_t> ws2(L.total2 + 64);
@@ -238,4 +239,9 @@ extern "C" int emu_line_index(const uint8_t *in, uint64_t n, uint32_t S_hint, ui
     memcpy(off, lo.data(), 8 * k);
     memcpy(len, ll.data(), 4 * k);
     return 0;
+}
+
+// compress_device's choice of the hop index's learning (host code)
+extern "C" int emu_data_lines_irregular(const uint8_t *p, uint64_t len, uint32_t S) {
+    return vcfc_ing::data_lines_irregular(p, len, S) ? 1 : 0;
 }

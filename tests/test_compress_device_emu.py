@@ -178,7 +178,7 @@ def test_hop_index_long_header():
         assert redo == [1]
 
 
-@pytest.mark.parametrize("S,dp_width", [(300, 2), (700, 2), (300, 0)])
+@pytest.mark.parametrize("S,dp_width", [(2504, 2), (700, 2), (300, 0)])
 def test_hop_index_law2_rows(S, dp_width):
     """Law-2-shaped files (hop_cases.law2_like: haploid, GT:DP:GQ, '.', '#'
     lines): the hop index's learned candidates (TRY / LEARN) give exactly the
@@ -187,15 +187,35 @@ def test_hop_index_law2_rows(S, dp_width):
     random widths (dp_width 0) the GT:DP:GQ rows are found by FIND and
     nothing breaks."""
     rnd = random.Random(S + dp_width)
-    vcf = law2_like(rnd, 240, S, dp_width=dp_width)
+    vcf = law2_like(rnd, 120 if S > 1000 else 240, S, dp_width=dp_width)
+    scan = E.emu_line_index(vcf, 0)
+    assert E.emu_line_index(vcf, S) == scan              # the product's walker count (~20 lines each)
     E.emu_hop_read()
-    hop = E.emu_line_index(vcf, S)
+    assert E.emu_line_index(vcf, S, hop_walkers=4) == scan   # one wave, ~60 lines per walker
     read = E.emu_hop_read()
-    assert hop == E.emu_line_index(vcf, 0)
-    if dp_width:
-        # (240 rows over ~12 walkers of 2 segments each: learning the three
-        # row kinds is a large share here; the 13 GB GPU file spreads it over
-        # ~120 rows per wave)
-        assert read < 0.8 * len(vcf), (read, len(vcf))
+    if S > 1000 and dp_width:
+        # 2504 samples (~13 KB lines), ~30 lines per walker, 120 per wave --
+        # as the 13 GB config-size file: the three learned kinds are read
+        # once per wave, every other line for ~1.3 KB of windows
+        assert read < 0.3 * len(vcf), (read, len(vcf))
     for chunk in (1 << 16, 1 << 22):
         check(vcf, chunk, "law2-like S=%d" % S)
+    st_o, want, _ = G.oracle_compress(vcf)
+    for hop in ("learn", "nolearn"):   # (compress_device chooses by the first data lines; both are exact)
+        st, got, _ = E.emu_compress_device(vcf, chunk=1 << 22, hop=hop)
+        assert st == st_o == OK and got == want, hop
+
+
+def test_hop_learn_choice():
+    """compress_device turns the learned candidates on when the first data
+    lines are not all S 3-byte tokens (vcfc_ingest_driver.h
+    data_lines_irregular), off for chr22-shaped files."""
+    import ctypes
+    lib = E.lib()
+    S = 300
+    chr22 = chr22_like(random.Random(1), 20, S)
+    law2 = law2_like(random.Random(2), 20, S, kinds=(0, 1))
+    # (the helper itself, through the emulator build's host code)
+    lib.emu_data_lines_irregular.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint32]
+    assert lib.emu_data_lines_irregular(chr22, len(chr22), S) == 0
+    assert lib.emu_data_lines_irregular(law2, len(law2), S) == 1

@@ -198,8 +198,13 @@ VcfcLineIndexLayout vcfc_line_index_layout(uint64_t chunk_bytes, uint64_t n_line
 // S_hint (the header's sample count, 0: none) selects the hop index
 // (k_nl_hop: data line ends predicted from S and checked) over the full
 // '\n' scan; its result must be confirmed by the encoder (VcfcEncodeArgs::nl_check).
+// hop_walkers: walkers of the hop index (0: HOP_WALKERS; the tests use a few,
+// so each walks as many lines as at config size).  hop_learn: the walkers
+// learn the genotype-region lengths of lines that are not 3-byte tokens
+// (TRY / LEARN, k_nl_hop<true>).
 hipError_t vcfc_line_index(const uint8_t *buf, uint64_t n, uint8_t *ws, const VcfcLineIndexLayout &L,
-                           const VcfcLineIndex &x, hipStream_t s, uint32_t S_hint = 0);
+                           const VcfcLineIndex &x, hipStream_t s, uint32_t S_hint = 0, uint64_t hop_walkers = 0,
+                           bool hop_learn = true);
 // phase 2 (n_lines = counts[0]): '\n' positions, data / pass line arrays; counts[1], counts[2]
 hipError_t vcfc_line_index_place(const uint8_t *buf, uint64_t n, uint64_t n_lines, const uint8_t *ws1, uint8_t *ws2,
                                  const VcfcLineIndexLayout &L, const VcfcLineIndex &x, hipStream_t s);

@@ -960,6 +960,8 @@ constexpr uint32_t HPC = 1024;   // half-slots per 2 KiB chunk
 
 struct VarState : FastState {
     uint32_t ntok;   // tokens started so far
+    uint32_t nlc;    // refuse a row holding a '\n' (VcfcEncodeArgs::nl_check: the hop line index guessed its end)
+    uint32_t nlhit;  // ... and this one does
 };
 
 struct Chunk8v {
@@ -1023,6 +1025,33 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
     for (int j = 0; j < 9; j++) d[j] = vw::alignbyte(w[j + 1], w[j], phi);
     const int32_t lastrel = (int32_t)NH - 1 - (int32_t)(C * HPC + 16u * l);   // the row's last half, lane-relative
     const uint32_t vm = lastrel >= 15 ? 0xFFFFu : lastrel < 0 ? 0u : (2u << lastrel) - 1u;   // valid halves
+    if (f.nlc) {
+        // a '\n' among the row's genotype bytes (token-relative offsets below
+        // 2 NH - 1; past them lie the line's own '\n' and the next line): the
+        // hop line index merged two lines.  haszero per dword is exact here:
+        // a borrow only runs upwards, from a '\n' inside the row.
+        const int32_t rel0 = (int32_t)(2u * NH - 1u) - (int32_t)(C * CHUNK8 + 32u * l);
+        uint32_t z = 0;
+        if ((C + 1u) * CHUNK8 <= 2u * NH - 1u) {
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const uint32_t x = d[j] ^ 0x0A0A0A0Au;
+                z |= (x - 0x01010101u) & ~x;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const uint32_t x = d[j] ^ 0x0A0A0A0Au;
+                const int32_t k = rel0 - 4 * j;
+                const uint32_t vb = k >= 4 ? 0x80808080u : k <= 0 ? 0u : (0x80808080u & ((1u << (8 * k)) - 1u));
+                z |= (x - 0x01010101u) & ~x & vb;
+            }
+        }
+        if (vw::ballot((z & 0x80808080u) != 0)) {
+            f.nlhit = 1;
+            return false;
+        }
+    }
     // TAB masks over halves 0..17: tb0 = first byte TAB (never valid), tb1 = second byte TAB (a token's end);
     // plain 3-byte candidates: bytes "a|b" from the half, a, b in {0,1}; a, b bits
     // (SWAR over the halves' first bytes A and second bytes P, four halves a
@@ -1252,7 +1281,8 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
     return true;
 }
 
-__device__ bool encode_var(const uint8_t *__restrict__ line, uint32_t len, Ring &r, uint32_t *rec_bytes) {
+__device__ bool encode_var(const uint8_t *__restrict__ line, uint32_t len, Ring &r, uint32_t *rec_bytes, bool nlc,
+                           bool *nlhit) {
     const uint32_t l = vw::lane_id();
     const uint32_t lead = (uint32_t)(reinterpret_cast<uintptr_t>(line) & 15);
     const uint8_t *A = line - lead;
@@ -1262,6 +1292,8 @@ __device__ bool encode_var(const uint8_t *__restrict__ line, uint32_t len, Ring 
     const uint32_t lo16 = BPL * l;
     VarState f;
     f.nf = 0; f.carryT = 1; f.gt0 = -1; f.T = 0; f.phi = 0; f.pcls = CLS_NONE; f.prs = 0; f.esc = 0; f.ntok = 0;
+    f.nlc = nlc ? 1u : 0u; f.nlhit = 0;
+    *nlhit = false;
     r.wpos = 8;
     r.fpos = 0;
     // prefix phase: as encode_fast
@@ -1303,7 +1335,10 @@ __device__ bool encode_var(const uint8_t *__restrict__ line, uint32_t len, Ring 
         C = vw::readfirst(C + 3);
         if (!ok || C >= ncG) break;
     }
-    if (!ok) return false;
+    if (!ok) {
+        *nlhit = f.nlhit != 0;
+        return false;
+    }
     // row end: pending chunk of the last run, then '\n'
     const uint32_t T = f.ntok, pcls = f.pcls, prs = f.prs;
     uint32_t extra = 0, pb = 0;
@@ -1654,15 +1689,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
         todo &= todo - 1;
         Ring r;
         if (!row_setup(a, row, lds + wave * RING_STRIDE, r)) continue;
-        if (a.nl_check && row_has_nl(a.buf + a.line_off[row], a.line_len[row])) {
-            if (l == 0) {   // not encoded: the caller indexes the lines again
+        // a.nl_check (the hop line index guessed line ends): a row holding a
+        // '\n' is not encoded and the caller indexes the lines again.  The
+        // variable-token path checks its genotype chunks as it reads them
+        // (round 4; a separate scan of every flagged row cost law 2 ~1 ms on
+        // the device file), the general path scans the row first.
+        uint32_t bytes = 0;
+        bool nlhit = false;
+        const bool var_ok = encode_var(a.buf + a.line_off[row], a.line_len[row], r, &bytes, a.nl_check, &nlhit);
+        if (!var_ok && !nlhit && a.nl_check) nlhit = row_has_nl(a.buf + a.line_off[row], a.line_len[row]);
+        if (nlhit) {
+            if (l == 0) {
                 a.rec_size[row] = 0;
                 atomicMin((unsigned long long *)a.err, (unsigned long long)((row << 8) | VCFCD_E_NEWLINE));
             }
             continue;
         }
-        uint32_t bytes = 0;
-        if (encode_var(a.buf + a.line_off[row], a.line_len[row], r, &bytes)) {
+        if (var_ok) {
             if (l == 0) a.rec_size[row] = bytes;
             continue;
         }

@@ -185,6 +185,13 @@ __device__ __forceinline__ uint32_t walker_scan(uint32_t v) {
     return v;
 }
 
+// LEARN (TRY / LEARN compiled in) is chosen by the host when the first data
+// lines of the file are not all 3-byte-token lines: the candidate state puts
+// the walker at 116 VGPRs (4 waves per SIMD; pinned to 5 it spills 16
+// dwords) and costs the configs[1] device file +3.7 %, while law-2 files go
+// 16.5 -> 13.7 ms (profiles/r04/ab/ab_tall_law*.txt); without it the walker
+// is round 3's (86 VGPRs, 5 waves).
+template <bool LEARN>
 __global__ __launch_bounds__(256) void k_nl_hop(const uint8_t *buf, uint64_t n, uint64_t n_seg, uint32_t S,
                                                 uint32_t wseg, uint32_t *seg_cnt, uint64_t *slot) {
     const uint32_t l = vw::lane_id(), wl = l & 15u, w0 = l & ~15u, sh = l & 48u;   // w0: the walker's first lane
@@ -198,9 +205,9 @@ __global__ __launch_bounds__(256) void k_nl_hop(const uint8_t *buf, uint64_t n, 
     uint32_t cur = 0, cc = 0;           // current segment (in the span) and its count
     // learned candidates (walker-uniform lengths; this lane's 16-bit TAB mask of each)
     uint32_t cg[HOP_K] = {0, 0, 0}, csig[HOP_K] = {0, 0, 0};
-    uint32_t tk = 0, ins = 0, trust = HOP_TRUST;
+    uint32_t ins = 0, trust = HOP_TRUST;
     uint64_t gt = 0;                    // the current data line's gt0 (lrn: it may be learned)
-    bool lrn = false;
+    bool lrn = false, tdef = false;     // tdef: the TRY round also checks the 3-byte end e (VERIFY's job)
     auto record = [&](uint64_t x) {     // (the walker's lanes; lo <= x < hi, in order)
         const uint32_t k = (uint32_t)((x - lo) / SEG);
         for (; cur < k; cur++, cc = 0)
@@ -209,38 +216,46 @@ __global__ __launch_bounds__(256) void k_nl_hop(const uint8_t *buf, uint64_t n, 
         cc++;
     };
     auto wbits = [&](bool pr) { return (uint32_t)(vw::ballot(pr) >> sh) & 0xFFFFu; };
-    // the first candidate at or after k (HOP_K: none), trusted walkers only
-    auto next_cand = [&](uint32_t k) {
-        for (; k < HOP_K; k++)
-            if (cg[k] && trust) break;
-        return k;
-    };
+    // learned candidates to try (trusted walkers, data lines only)
+    auto have_cand = [&]() { return LEARN && lrn && trust != 0 && (cg[0] | cg[1] | cg[2]) != 0; };
     // a failed prediction: the candidates, else FIND from fq
     auto to_try = [&](uint64_t fq) {
         q = fq;
-        tk = lrn ? next_cand(0) : HOP_K;
-        mode = tk < HOP_K ? HOP_TRY : HOP_FIND;
+        tdef = false;
+        mode = have_cand() ? HOP_TRY : HOP_FIND;
     };
     while (vw::ballot(mode != HOP_DONE)) {
         const uint32_t mode0 = mode;   // (the round's mode: the steps below may switch it for the next round)
         // ---- loads: the main window (LINE: `rows` rows, FIND: 4), the guess window ----
         const uint64_t base = mode == HOP_FIND ? q : p;
         const uint32_t nr = mode == HOP_FIND ? 4u : mode == HOP_LINE ? rows : 0u;
+        // (TRY: rows 0..2 hold the 256 bytes ending at each learned
+        // candidate's end gt0 + G_k, all tried in one round)
         uint4 v[4];
+        uint32_t cvalid = 0;
 #pragma unroll
-        for (uint32_t k = 0; k < 4; k++) v[k] = k < nr ? load16(buf, n, base + 256u * k + 16u * wl) : make_uint4(0, 0, 0, 0);
-        uint64_t g0 = 0, ek = 0;
+        for (uint32_t k = 0; k < 4; k++) {
+            const uint32_t G = k == 0 ? cg[0] : k == 1 ? cg[1] : cg[2];
+            const bool cv = LEARN && k < 3 && mode == HOP_TRY && G != 0 && gt + G + 1 >= GW && gt + G < n;
+            cvalid |= cv ? 1u << k : 0u;
+            v[k] = k < nr ? load16(buf, n, base + 256u * k + 16u * wl)
+                          : cv ? *reinterpret_cast<const uint4 *>(buf + gt + G + 1 - GW + 16u * wl) : make_uint4(0, 0, 0, 0);
+        }
+        uint64_t g0 = 0;
+        bool gok = true;   // (VERIFY / TRY / LEARN: the window ends at e = g0 + GW - 1)
         if (mode == HOP_LINE) {
             const uint64_t x = p + pl + 4ull * S - 1;   // the end if the prefix is as long as the last one
             g0 = x >= GW / 2 + 62 ? x - (GW / 2 + 62) : 0;
-        } else if (mode == HOP_VERIFY || mode == HOP_LEARN || mode == HOP_TRY) {
-            // (TRY: the candidate's end; VERIFY / LEARN: e)
-            ek = mode == HOP_TRY ? gt + (tk == 0 ? cg[0] : tk == 1 ? cg[1] : cg[2]) : e;
-            g0 = ek + 1 >= GW ? ek + 1 - GW : 0;
+        } else if (mode == HOP_VERIFY || mode == HOP_LEARN || (mode == HOP_TRY && tdef)) {
+            gok = e + 1 >= GW;
+            g0 = gok ? e + 1 - GW : 0;
+        } else {
+            gok = false;
         }
-        const bool gv = mode != HOP_FIND && mode != HOP_DONE && g0 + GW <= n && (mode == HOP_LINE || ek + 1 >= GW);
+        const bool gv = mode != HOP_FIND && mode != HOP_DONE && g0 + GW <= n && gok;
         const uint4 ga = gv ? *reinterpret_cast<const uint4 *>(buf + g0 + 16u * wl) : make_uint4(0, 0, 0, 0);
-        if (l == w0 && mode != HOP_DONE) VCFC_DIAG_HOP_READ(256u * nr + (gv ? GW : 0u));
+        if (l == w0 && mode != HOP_DONE)
+            VCFC_DIAG_HOP_READ(256u * nr + (gv ? GW : 0u) + GW * (uint32_t)__builtin_popcount(cvalid));
         // ---- the first '\n' of the main window (row-major: row k, then lane) ----
         uint64_t first = ~0ull;
 #pragma unroll
@@ -257,42 +272,44 @@ __global__ __launch_bounds__(256) void k_nl_hop(const uint8_t *buf, uint64_t n, 
             else if (q + 1024 >= n) { e = n - 1; found = true; }   // (buf[n - 1] is '\n')
             else q += 1024;
             // a data line the candidates did not know: learn its region
-            if (found && lrn && trust && e >= gt + GW - 1) { found = false; mode = HOP_LEARN; }
+            if (LEARN && found && lrn && trust && e >= gt + GW - 1) { found = false; mode = HOP_LEARN; }
         }
-        // ---- TRY / LEARN: the window ending at ek ----
-        const uint32_t gtm = tab_mask_v(ga), gnl = nl_mask_v(ga);
-        const uint32_t sig = tk == 0 ? csig[0] : tk == 1 ? csig[1] : csig[2];
-        const bool tok = gv && ek < n && gtm == sig && gnl == (wl == 15 ? 0x8000u : 0u);
-        const bool thit = wbits(!tok) == 0;   // (collectives stay wave-uniform)
-        if (mode == HOP_TRY) {
-            if (thit) {
-                e = ek; found = true;
-                trust = trust < HOP_TRUST ? trust + 1 : trust;
-            } else {
-                tk = next_cand(tk + 1);
-                if (tk >= HOP_K) {
-                    mode = HOP_FIND;   // (q: where the prediction left it)
-                    trust = trust ? trust - 1 : 0;
-                }
+        // ---- TRY / LEARN (wave-uniform branches: a wave of 3-byte-token
+        // lines pays nothing for them).  TRY: candidate k holds when the
+        // window ending at gt0 + G_k has exactly its TAB mask and its only
+        // '\n' is the last byte ----
+        uint32_t chit = 0;   // the region length of the first candidate that holds (0: none)
+        if (LEARN && vw::ballot(mode0 == HOP_TRY || mode0 == HOP_LEARN)) {
+            const uint32_t gtm = tab_mask_v(ga);
+#pragma unroll
+            for (uint32_t k = 0; k < 3; k++) {
+                const uint32_t sg = k == 0 ? csig[0] : k == 1 ? csig[1] : csig[2];
+                const bool tok = ((cvalid >> k) & 1u) && tab_mask_v(v[k]) == sg &&
+                                 nl_mask_v(v[k]) == (wl == 15 ? 0x8000u : 0u);
+                const bool hk = wbits(!tok) == 0;   // (collectives stay wave-uniform)
+                // (the length itself: a LEARN below may replace the slot this round)
+                const uint32_t G = k == 0 ? cg[0] : k == 1 ? cg[1] : cg[2];
+                if (hk && chit == 0 && mode0 == HOP_TRY) chit = G;
             }
-        }
-        // LEARN: every walker of the wave takes the lowest learner's candidate
-        // (a law-2 row kind is learned once per wave, not once per walker),
-        // a learner also its own; a length already held is not taken again
-        auto insert = [&](uint32_t G, uint32_t sg) {
-            if (G == cg[0] || G == cg[1] || G == cg[2]) return;
-            if (ins == 0) { cg[0] = G; csig[0] = sg; }
-            else if (ins == 1) { cg[1] = G; csig[1] = sg; }
-            else { cg[2] = G; csig[2] = sg; }
-            ins = ins + 1 == HOP_K ? 0u : ins + 1;
-        };
-        const uint64_t lm = vw::ballot(mode0 == HOP_LEARN && gv);
-        if (lm) {
-            const uint32_t sw0 = (uint32_t)__builtin_ctzll(lm) & ~15u;
-            const uint32_t Gown = (uint32_t)(e - gt);
-            const uint32_t Gs = vw::shfl(Gown, sw0), ss = vw::shfl(gtm, sw0 + wl);
-            insert(Gs, ss);
-            if (mode0 == HOP_LEARN && gv) insert(Gown, gtm);
+            // LEARN: every walker of the wave takes the lowest learner's
+            // candidate (a law-2 row kind is learned once per wave, not once
+            // per walker), a learner also its own; a length already held is
+            // not taken again
+            auto insert = [&](uint32_t G, uint32_t sg) {
+                if (G == cg[0] || G == cg[1] || G == cg[2]) return;
+                if (ins == 0) { cg[0] = G; csig[0] = sg; }
+                else if (ins == 1) { cg[1] = G; csig[1] = sg; }
+                else { cg[2] = G; csig[2] = sg; }
+                ins = ins + 1 == HOP_K ? 0u : ins + 1;
+            };
+            const uint64_t lm = vw::ballot(mode0 == HOP_LEARN && gv);
+            if (lm) {
+                const uint32_t sw0 = (uint32_t)__builtin_ctzll(lm) & ~15u;
+                const uint32_t Gown = (uint32_t)(e - gt);
+                const uint32_t Gs = vw::shfl(Gown, sw0), ss = vw::shfl(gtm, sw0 + wl);
+                insert(Gs, ss);
+                if (mode0 == HOP_LEARN && gv) insert(Gown, gtm);
+            }
         }
         if (mode0 == HOP_LEARN) found = true;
         // ---- LINE: the 9th TAB, the predicted end ----
@@ -331,11 +348,17 @@ __global__ __launch_bounds__(256) void k_nl_hop(const uint8_t *buf, uint64_t n, 
                 e = p + t9 + 4ull * S;   // gt0 + 4 S - 1
                 if (e >= n) to_try(p + 256u * nr);
                 else if (gv && e >= g0 + 124 && e < g0 + GW) check = true;
-                else mode = HOP_VERIFY;
+                else if (have_cand()) {   // (the TRY round checks e too: VERIFY's window)
+                    mode = HOP_TRY;
+                    tdef = true;
+                    q = p + 256u * nr;
+                } else mode = HOP_VERIFY;
             }
         } else if (mode == HOP_VERIFY) {
             if (gv && e >= g0 + 124) check = true;
             else to_try(p);
+        } else if (mode == HOP_TRY && tdef && gv) {
+            check = true;
         }
         // ---- the check: byte e is '\n', bytes e - 4 i (i = 1..31) TABs ----
         bool bad = false;
@@ -352,7 +375,17 @@ __global__ __launch_bounds__(256) void k_nl_hop(const uint8_t *buf, uint64_t n, 
         const bool bw = wbits(bad) != 0;
         if (check) {
             if (!bw) found = true;
-            else to_try(p + 256u * nr);   // (past the first window: no '\n' there)
+            else if (mode0 != HOP_TRY) to_try(p + 256u * nr);   // (past the first window: no '\n' there)
+        }
+        if (mode0 == HOP_TRY && !found) {   // the 3-byte end failed: the first candidate that holds
+            if (chit) {
+                e = gt + chit;
+                found = true;
+                trust = trust < HOP_TRUST ? trust + 1 : trust;
+            } else {
+                mode = HOP_FIND;   // (q: where the prediction left it)
+                trust = trust ? trust - 1 : 0;
+            }
         }
         // ---- the line end: record, next line ----
         if (found) {
@@ -467,7 +500,8 @@ VcfcLineIndexLayout vcfc_line_index_layout(uint64_t chunk_bytes, uint64_t n_line
 // output arrays of `x` hold up to n / 2 data lines (a data line has at least
 // one byte and its '\n') and n pass lines.
 hipError_t vcfc_line_index(const uint8_t *buf, uint64_t n, uint8_t *ws, const VcfcLineIndexLayout &L,
-                           const VcfcLineIndex &x, hipStream_t s, uint32_t S_hint) {
+                           const VcfcLineIndex &x, hipStream_t s, uint32_t S_hint, uint64_t hop_walkers,
+                           bool hop_learn) {
     // ws: phase 1 workspace (L.total1 bytes)
     uint32_t *seg_cnt = reinterpret_cast<uint32_t *>(ws + L.seg_cnt);
     uint64_t *seg_base = reinterpret_cast<uint64_t *>(ws + L.seg_base);
@@ -480,11 +514,15 @@ hipError_t vcfc_line_index(const uint8_t *buf, uint64_t n, uint8_t *ws, const Vc
     if (S_hint >= 32) {
         // spans of wseg segments: about HOP_WALKERS walkers, each over at
         // least 2 segments
-        const uint64_t wseg = std::max<uint64_t>(2, (n_seg + HOP_WALKERS - 1) / HOP_WALKERS);
+        const uint64_t hw = hop_walkers ? hop_walkers : HOP_WALKERS;
+        const uint64_t wseg = std::max<uint64_t>(2, (n_seg + hw - 1) / hw);
         const uint64_t walkers = (n_seg + wseg - 1) / wseg;
         const uint64_t per_block = (uint64_t)HOPW * IX_WAVES;
-        hipLaunchKernelGGL(k_nl_hop, dim3((unsigned)((walkers + per_block - 1) / per_block)), blk, 0, s, buf, n, n_seg,
-                           S_hint, (uint32_t)wseg, seg_cnt, slot);
+        const dim3 hg((unsigned)((walkers + per_block - 1) / per_block));
+        if (hop_learn)
+            hipLaunchKernelGGL(k_nl_hop<true>, hg, blk, 0, s, buf, n, n_seg, S_hint, (uint32_t)wseg, seg_cnt, slot);
+        else
+            hipLaunchKernelGGL(k_nl_hop<false>, hg, blk, 0, s, buf, n, n_seg, S_hint, (uint32_t)wseg, seg_cnt, slot);
     }
     else
         hipLaunchKernelGGL(k_nl_scan, sg, blk, 0, s, buf, n, n_seg, seg_cnt, slot);

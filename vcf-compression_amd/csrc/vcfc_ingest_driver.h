@@ -148,6 +148,8 @@ struct Config {
                                      // LEN header holds < 2^30 anyway, reference src/utils.hpp:160)
     int read_threads = 8;
     bool hop_index = true;           // compress_device: the hop line index (S from "#CHROM")
+    int hop_learn = -1;              // ... learning other region lengths: -1 = when the first data lines need it
+    uint64_t hop_walkers = 0;        // ... walkers (0: the kernel's count; tests)
     bool trace = false;              // stage totals / decisions to stderr (vcfc_ctx_set_trace)
     uint64_t *hop_redo = nullptr;    // compress_device: chunks indexed again after a wrong hop guess
 };
@@ -188,6 +190,28 @@ inline uint32_t header_samples(const uint8_t *p, uint64_t len, bool *more = null
     }
     if (more) *more = len > 0;   // the window ended at a line end inside the header
     return 0;
+}
+
+// Whether the complete data lines in p[0, len) after the "#CHROM" line hold
+// anything but S 3-byte tokens (genotype region != 4 S - 1 bytes): then the
+// hop line index learns other region lengths (vcfc_line_index hop_learn).
+// Only a guess, never trusted for the output.
+inline bool data_lines_irregular(const uint8_t *p, uint64_t len, uint32_t S) {
+    bool in_data = false;
+    for (uint64_t q = 0; q < len;) {
+        const uint8_t *nl = static_cast<const uint8_t *>(memchr(p + q, '\n', len - q));
+        if (!nl) break;
+        const uint64_t end = (uint64_t)(nl - p);
+        if (!in_data) {
+            in_data = end - q >= 7 && memcmp(p + q, "#CHROM\t", 7) == 0;
+        } else if (end > q && p[q] != '#') {
+            uint64_t k = q;
+            for (uint32_t t = 0; t < 9 && k < end; k++) t += p[k] == '\t';
+            if (end - k != 4ull * S - 1) return true;
+        }
+        q = end + 1;
+    }
+    return false;
 }
 
 namespace detail {
@@ -629,6 +653,7 @@ inline int compress_device(const uint8_t *d_in, uint64_t N, uint8_t *d_out, uint
     // indexed again from every byte.  cfg.hop_index false
     // (VCFC_LINE_INDEX_SCAN): always every byte.
     uint32_t S_hint = 0;
+    bool learn = false;
     {
         if (cfg.hop_index) {
             // 64 KiB of the file into pinned memory, 1 MiB if the header is longer
@@ -639,12 +664,15 @@ inline int compress_device(const uint8_t *d_in, uint64_t N, uint8_t *d_out, uint
                 bool more = false;
                 S_hint = header_samples(h, want, &more);
                 const uint64_t cap = std::min<uint64_t>(N, 1u << 20);
-                if (!more || want >= cap) break;
+                if (!more || want >= cap) {
+                    learn = S_hint && (cfg.hop_learn > 0 || (cfg.hop_learn < 0 && data_lines_irregular(h, want, S_hint)));
+                    break;
+                }
                 want = cap;
             }
             if (S_hint < 32) S_hint = 0;   // (the check reads 32 tokens)
         }
-        if (trace) fprintf(stderr, "compress_device: S_hint=%u\n", S_hint);
+        if (trace) fprintf(stderr, "compress_device: S_hint=%u learn=%d\n", S_hint, (int)learn);
     }
     uint64_t pos = 0, o = 0, line_base = 0;
     constexpr uint64_t WIN = 1ull << 16;
@@ -680,7 +708,8 @@ inline int compress_device(const uint8_t *d_in, uint64_t N, uint8_t *d_out, uint
         if (!d_ix1) return ST_E_HIP;
         VcfcLineIndex x;
         x.counts = d_small;
-        if (vcfc_line_index(d_c, n, d_ix1, L1, x, s, hop) != hipSuccess || !d2h(hsmall, d_small, 8) || !sync())
+        if (vcfc_line_index(d_c, n, d_ix1, L1, x, s, hop, cfg.hop_walkers, learn) != hipSuccess ||
+            !d2h(hsmall, d_small, 8) || !sync())
             return ST_E_HIP;
         const uint64_t n_lines = hsmall[0];
         // line numbers inside a chunk are 32-bit (k_line_place): a chunk of
