@@ -523,7 +523,8 @@ def bench_devfile(args, torch, vcfc, workload):
            "roofline": {"kernel": "line index + encoder (whole step)", "bound": "hbm",
                         "achieved": round(alg / (ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                        "traffic": None,
+                        "traffic": load_pmc("%s/%dx%d/%s" % (law_name(args.law), S, n, args.line_index),
+                                            "pmc_devfile.json"),
                         "algorithmic_bytes_per_step": alg,
                         "note": "file bytes read once + output written once (the scan index reads the file "
                                 "a second time)"},

@@ -62,6 +62,13 @@ for s in $STEPS; do
          python3 tools/pmc_encode_json.py "$O/pmcenc_l0_FETCH_SIZE" "$O/pmcenc_l0_WRITE_SIZE" "random_vcf-law/2504x1000000" "$O/pmc_k_encode_law0.json" "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes (tools/gpu_check.sh pmcenc, run $TAG)" > /dev/null &&
          python3 tools/pmc_encode_json.py "$O/pmcenc_l2_FETCH_SIZE" "$O/pmcenc_l2_WRITE_SIZE" "general-shapes (chrX haploid/GT:DP:GQ/missing)/2504x1000000" "$O/pmc_k_encode_law2.json" "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes (tools/gpu_check.sh pmcenc, run $TAG)" > /dev/null || { echo "pmc json failed"; exit 1; } ;;
     benchdev) timeout -k 10 300 python bench.py --mode devfile > "$O/bench_devfile.json" 2> "$O/bench_devfile.err" || { echo "benchdev failed"; tail -30 "$O/bench_devfile.err"; exit 1; } ; cat "$O/bench_devfile.json" ;;
+    pmcdev) # HBM bytes per devfile step (every kernel of one call), law ${LAW:-1} -> pmc_devfile_l<law>.json
+         for P in FETCH_SIZE WRITE_SIZE; do
+           (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 180 rocprofv3 --pmc $P --kernel-trace --output-format csv -d "$O/pmcdev_l${LAW:-1}_$P" -o run -- python3 "$R/bench.py" --mode devfile --law ${LAW:-1} --steps 3 --warmup 1 > "$O/pmcdev_l${LAW:-1}_$P.log" 2>&1) || { echo "pmcdev $P failed rc=$?"; tail -30 "$O/pmcdev_l${LAW:-1}_$P.log"; exit 1; }
+         done
+         python3 tools/pmc_step_json.py "$O/pmcdev_l${LAW:-1}_FETCH_SIZE" "$O/pmcdev_l${LAW:-1}_WRITE_SIZE" 4 "$(python3 -c "import bench,sys; print(bench.law_name(int(sys.argv[1])))" ${LAW:-1})/2504x1000000/hop" "$O/pmc_devfile_l${LAW:-1}.json" "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, bench.py --mode devfile --law ${LAW:-1} --steps 3 --warmup 1 (tools/gpu_check.sh pmcdev, run $TAG)" > /dev/null || { echo "pmcdev json failed"; exit 1; } ;;
+    benchdev2) timeout -k 10 300 python bench.py --mode devfile --law 2 > "$O/bench_devfile_law2.json" 2> "$O/bench_devfile_law2.err" || { echo "benchdev2 failed"; tail -30 "$O/bench_devfile_law2.err"; exit 1; } ; cat "$O/bench_devfile_law2.json" ;;
+    profdev2) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/profdev2" -o run -- python3 "$R/bench.py" --mode devfile --law 2 --steps 5 --warmup 1 > "$O/profdev2.log" 2>&1) || { echo "profdev2 failed rc=$?"; tail -30 "$O/profdev2.log"; exit 1; } ;;
     profdev) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/profdev" -o run -- python3 "$R/bench.py" --mode devfile --steps 5 --warmup 1 > "$O/profdev.log" 2>&1) || { echo "profdev failed rc=$?"; tail -30 "$O/profdev.log"; exit 1; } ;;
     rehearse2) VCFC_BENCH_REHEARSAL=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29623 bench.py --gpus 2 --steps 5 --warmup 1 --no-cpu-baseline > "$O/bench_n2_rehearsal.json" 2> "$O/bench_n2_rehearsal.err" || { echo "rehearse2 failed"; tail -30 "$O/bench_n2_rehearsal.err"; exit 1; } ; cat "$O/bench_n2_rehearsal.json" ;;
     *) echo "unknown step $s"; exit 2 ;;
