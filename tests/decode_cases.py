@@ -46,7 +46,7 @@ def encode_file(samples, lines):
 def valid_files(seed):
     rnd = random.Random(seed)
     files = []
-    for S in (1, 3, 64, 300, 2504):
+    for S in (1, 3, 64, 256, 300, 513, 2504):   # (tile edges: 256 tokens per decoder tile)
         n = 40 if S < 2504 else 12
         files.append(("S%d" % S, encode_file(S, rows(rnd, n, S))))
     files.append(("escapes", encode_file(200, rows(rnd, 30, 200, escapes=0.05))))

@@ -24,6 +24,7 @@ def lib():
         L.emu_encode_rows.argtypes = [vp, vp, vp, ctypes.c_uint64, vp, ctypes.c_uint64, vp,
                                       ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
                                       ctypes.POINTER(ctypes.c_uint32)]
+        L.emu_last_deferred.restype = ctypes.c_uint32
         L.emu_sparse_plan.argtypes = [vp, vp, ctypes.c_uint64, ctypes.c_uint64, vp, vp, vp]
         L.emu_decompress.argtypes = [ctypes.c_char_p, ctypes.c_uint64, vp, ctypes.c_uint64,
                                      ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint64]
@@ -71,6 +72,12 @@ def data_lines(vcf):
 
 
 LAST_RETRIES = [0]
+
+
+def last_deferred():
+    """Rows the last emu_encode call deferred (sized by k_encode_var, written
+    to out by k_encode_defer)."""
+    return int(lib().emu_last_deferred())
 
 
 def emu_encode(buf, line_off, line_len, cap=None):

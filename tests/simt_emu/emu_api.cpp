@@ -20,6 +20,10 @@ extern "C" unsigned long long emu_hop_read(int reset) {
     return v;
 }
 
+static uint32_t g_last_deferred = 0;
+// rows the last emu_encode_rows call deferred (VCFCD_DEFER: written by k_encode_defer)
+extern "C" uint32_t emu_last_deferred() { return g_last_deferred; }
+
 extern "C" int emu_encode_rows(const uint8_t *buf, const uint64_t *line_off, const uint32_t *line_len,
                                uint64_t n, uint8_t *out, uint64_t out_cap, uint64_t *rec_off,
                                uint64_t *err_word, uint64_t *switches, uint32_t *retries) {
@@ -38,6 +42,7 @@ extern "C" int emu_encode_rows(const uint8_t *buf, const uint64_t *line_off, con
     int st = (int)vcfc_encode_device(a, nullptr);
     *err_word = *a.err;
     if (retries) *retries = *a.retry_count;   // rows that took the general path
+    g_last_deferred = *a.defer_count;
     if (switches) *switches = emu::g.switches;
     free(ws);
     return st;

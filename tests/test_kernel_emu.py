@@ -366,6 +366,55 @@ def test_law2_synthetic_rows():
     assert gdg > 0 and E.LAST_RETRIES[0] == 0
 
 
+def test_deferred_records():
+    """Rows whose first genotype chunk is all escapes (GT:DP:GQ, all-1-byte,
+    a row that turns mixed after its first chunk, another whose later chunk
+    sends it to the general path) are deferred: k_encode_var only sizes
+    them, the compaction skips their bytes, k_encode_defer writes each record
+    straight into out after the size scan.  Byte-exact against the oracle
+    beside staged neighbours (records meeting inside 16-byte blocks) at
+    several alignments, and with out_cap cutting a deferred record."""
+    rnd = random.Random(123)
+    lines, expect_defer = [], 0
+    for i in range(40):
+        kind = i % 5
+        if kind == 0:     # GT:DP:GQ, 300..1200 samples (> one 2 KiB chunk)
+            S = rnd.choice([300, 301, 777, 1200])
+            ln = PFX_V + b"\t".join(b"%d|%d:%d:%d" % (rnd.randint(0, 1), rnd.randint(0, 1), rnd.randint(10, 99),
+                                                   rnd.randint(10, 99)) for _ in range(S))
+            expect_defer += 1
+        elif kind == 1:   # 1-byte tokens, then plain diploid ones (chunk 1 mixed)
+            ln = PFX_V + b"\t".join([rnd.choice([b"0", b"1", b"."]) for _ in range(1100)] +
+                                    [rnd.choice([b"0|0", b"0|1", b"1|1"]) for _ in range(rnd.randint(1, 700))])
+            expect_defer += 1
+        elif kind == 2:   # escapes first, an even-length token later: the general path (not deferred)
+            ln = PFX_V + b"\t".join([b"0"] * 1500 + [b"10"] + [b"1"] * 3)
+        elif kind == 3:   # one chunk only: staged
+            ln = PFX_V + b"\t".join(rnd.choice([b"0", b"0|1:5:9"]) for _ in range(rnd.randint(1, 150)))
+        else:             # 3-byte tokens: the fast kernel
+            ln = b"\t".join([b"1", b"%d" % i, b"a", b"b", b"c", b"d", b"e", b"f", b"GT"] +
+                            [rnd.choice([b"0|0", b"0|1", b"1|1", b"0|2"]) for _ in range(rnd.randint(1, 900))])
+        lines.append(ln)
+    want = [G.oracle_encode_line(x)[1] for x in lines]
+    for lead in (0, 3, 9):
+        st, out, ro, err = run(lines, lead)
+        assert err == (1 << 64) - 1
+        assert E.last_deferred() == expect_defer
+        for i, w in enumerate(want):
+            assert out[int(ro[i]):int(ro[i + 1])] == w, (lead, i)
+    buf = bytearray()
+    offs, lens = [], []
+    for ln in lines:
+        offs.append(len(buf))
+        lens.append(len(ln))
+        buf += ln + b"\n"
+    cut = 10   # a GT:DP:GQ row: out_cap ends inside its record
+    cap = int(ro[cut]) + 100
+    st2, out2, ro2, err2 = E.emu_encode(bytes(buf), np.array(offs, np.uint64), np.array(lens, np.uint32), cap=cap)
+    assert err2 == (cut << 8) | 4
+    assert out2[:int(ro[cut])] == out[:int(ro[cut])]
+
+
 @pytest.mark.parametrize("seed", [51, 52, 53, 54])
 def test_sparse_clean_ranges(seed):
     """Sparse clean chunks (the shape a sparse event path would take, round 4;

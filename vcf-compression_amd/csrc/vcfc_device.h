@@ -13,11 +13,18 @@
 // a row holding a '\n' byte, seen only when VcfcEncodeArgs::nl_check is set:
 // the hop line index (vcfc_line_index with S_hint) mispredicted a line end
 #define VCFCD_E_NEWLINE 9
+// a deferred record came out another size than it was sized (cannot happen;
+// reported as VCFC_E_HIP, a device failure)
+#define VCFCD_E_INTERNAL 6
 
 // error word: min over failing rows of (row << 8 | code); ~0 = no error
 #define VCFCD_NO_ERROR (~0ull)
 // rec_size value of a row the fast kernel leaves to k_encode_var
 #define VCFCD_RETRY 0xFFFFFFFFu
+// rec_size flag of a deferred row: k_encode_var only sized it (every chunk an
+// escape chunk), k_encode_defer writes its record straight to out after the
+// size scan (the size is the low 31 bits)
+#define VCFCD_DEFER 0x80000000u
 
 // Alignment: buf, the lines in it and out may start at any byte.  The
 // kernels address them with 16-byte loads and stores at the base's own
@@ -45,6 +52,8 @@ struct VcfcEncodeArgs {
     uint64_t *partials;        // scan partials
     uint64_t *err;             // 1 word
     uint32_t *retry_count;     // rows that took the general path (emulator builds only, diag hooks)
+    uint32_t *defer_count;     // deferred rows (VCFCD_DEFER), zeroed per encode with lb
+    uint32_t *defer_list;      // their row indices (any order), n entries
     uint8_t *lb;               // look-back scan state (tickets, tile flags; zeroed per encode)
     uint32_t *tile_first;      // per 4 KiB output tile: the row holding its first byte (compaction)
     uint8_t *prim;             // per-row primary staging: record bytes [0, prim_bytes) at prim + prim_bytes * row
@@ -72,7 +81,8 @@ __host__ __device__ inline uint32_t vcfc_prim_bytes(uint64_t n, uint64_t total_l
 }
 
 struct VcfcWorkspaceLayout {
-    uint64_t slot_off, rec_size, partials, err, lb, lb_bytes, retry_count, tile_first, prim, slots, dbg, total;
+    uint64_t slot_off, rec_size, partials, err, lb, lb_bytes, retry_count, defer_count, defer_list, tile_first, prim,
+        slots, dbg, total;
     uint32_t prim_bytes;
 };
 
@@ -97,6 +107,8 @@ inline void vcfc_encode_args_workspace(VcfcEncodeArgs &a, uint8_t *ws, const Vcf
     a.rec_size = reinterpret_cast<uint32_t *>(ws + L.rec_size);
     a.partials = reinterpret_cast<uint64_t *>(ws + L.partials);
     a.retry_count = reinterpret_cast<uint32_t *>(ws + L.retry_count);
+    a.defer_count = reinterpret_cast<uint32_t *>(ws + L.defer_count);
+    a.defer_list = reinterpret_cast<uint32_t *>(ws + L.defer_list);
     a.lb = ws + L.lb;
     a.tile_first = reinterpret_cast<uint32_t *>(ws + L.tile_first);
     a.prim = ws + L.prim;

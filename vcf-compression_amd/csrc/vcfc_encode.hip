@@ -89,12 +89,18 @@ __device__ __forceinline__ uint32_t umin32(uint32_t a, uint32_t b) { return a < 
 // LDS ring: record bytes [fpos, wpos) are pending.  Global staging: record
 // bytes [0, pb) at prim, the rest at slot (see vcfc_device.h; pb is a
 // multiple of BURST, so a burst lies wholly in one region).
+// mode: RING_STAGE (the staging), RING_SIZE (nothing leaves the ring: the
+// row is only sized, k_encode_var's deferred rows), RING_DIRECT (the record
+// goes straight to out: prim = its first byte, pb = ~0, and the last partial
+// burst stores exactly the record's bytes -- k_encode_defer)
+constexpr uint32_t RING_STAGE = 0, RING_SIZE = 1, RING_DIRECT = 2;
 struct Ring {
     uint8_t *lds;
     uint8_t *prim;
     uint8_t *slot;
     uint32_t wpos, fpos;
     uint32_t pb;   // prim_bytes
+    uint32_t mode;
 };
 
 __device__ __forceinline__ void ring_put(Ring &r, uint32_t pos, uint32_t b) {
@@ -118,6 +124,7 @@ __device__ __forceinline__ void ring_stage(Ring &r, uint32_t f, uint4 v) {
     if (f == 0x7FFFFFFFu) vw::gstore16_nt(r.prim, 0, v);
     return;
 #endif
+    if (r.mode == RING_SIZE) return;
     if (r.fpos < r.pb) vw::gstore16_nt(r.prim, f, v);
     else vw::gstore16_nt(r.slot, f - r.pb, v);
 }
@@ -142,7 +149,13 @@ __device__ __forceinline__ void ring_flush(Ring &r, bool final) {
         const uint32_t rem = r.wpos - r.fpos;  // < BURST
         if (16u * l < rem) {
             const uint4 v = *reinterpret_cast<const uint4 *>(r.lds + ((r.fpos + 16u * l) & RMASK));
-            ring_stage(r, r.fpos + 16u * l, v);
+            if (r.mode != RING_DIRECT || 16u * l + 16u <= rem) {
+                ring_stage(r, r.fpos + 16u * l, v);
+            } else {   // the record's last bytes in out: not one byte past them (the next record's)
+                const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+                for (uint32_t i = 0; 16u * l + i < rem; i++)
+                    r.prim[r.fpos + 16u * l + i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+            }
         }
         r.fpos = r.wpos;
     }
@@ -167,7 +180,7 @@ __device__ __forceinline__ void ring_unwrap(Ring &r, uint32_t end) {   // end: t
 // wrote its first 16 bytes during the flush, so program order keeps them).
 __device__ void ring_finish(Ring &r, uint32_t req) {
     ring_flush(r, true);
-    if (vw::lane_id() == 0) {
+    if (vw::lane_id() == 0 && r.mode != RING_SIZE) {
         const uint32_t L = r.wpos - 4;
         const uint32_t h0 = (((L >> 24) & 0xFFu) | 0xC0u) | (((L >> 16) & 0xFFu) << 8) |
                             (((L >> 8) & 0xFFu) << 16) | ((L & 0xFFu) << 24);
@@ -962,6 +975,8 @@ struct VarState : FastState {
     uint32_t ntok;   // tokens started so far
     uint32_t nlc;    // refuse a row holding a '\n' (VcfcEncodeArgs::nl_check: the hop line index guessed its end)
     uint32_t nlhit;  // ... and this one does
+    uint32_t defer;  // the row may be deferred (k_encode_var, genotype region over one chunk) ...
+    uint32_t sizeonly;   // ... and is: its chunk 0 was an escape chunk, the ring keeps its bytes (RING_SIZE)
 };
 
 struct Chunk8v {
@@ -1092,8 +1107,17 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
         const int32_t dmi = (int32_t)RING_DUMMY;
         int32_t ro = (int32_t)base - dmi;
         const uint32_t vm2 = vm & ~(lastin ? (1u << lastrel) : 0u);
+        // A row whose first chunk is all escapes (GT:DP:GQ, records about
+        // 1.1x the input) is deferred: sized here, its record written
+        // straight to out by k_encode_defer once the size scan has placed it,
+        // instead of staged and copied (deferred records).
+        if (f.defer && C == 0) {
+            f.sizeonly = 1;
+            r.mode = RING_SIZE;
+        }
 #ifndef VCFC_VAR_SIZE_ONLY   // (diagnostic: the cost of a size-only pass, wrong output)
-        if (vw::ballot(vm != 0xFFFFu) == 0) {
+        if (f.sizeonly) {
+        } else if (vw::ballot(vm != 0xFFFFu) == 0) {
             // Interior chunk (every half valid, none the row's last): half h's
             // two bytes sit at lane offset 2h + c_h, c_h = starts in halves
             // 0..h, and its 0xE1 (a start) just before them.  Half h's 0xE1
@@ -1281,8 +1305,10 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
     return true;
 }
 
+// defer_ok: the row may be deferred (*deferred: it was -- sized only, the
+// ring's bytes never left it; k_encode_var)
 __device__ bool encode_var(const uint8_t *__restrict__ line, uint32_t len, Ring &r, uint32_t *rec_bytes, bool nlc,
-                           bool *nlhit) {
+                           bool *nlhit, bool defer_ok, bool *deferred) {
     const uint32_t l = vw::lane_id();
     const uint32_t lead = (uint32_t)(reinterpret_cast<uintptr_t>(line) & 15);
     const uint8_t *A = line - lead;
@@ -1292,8 +1318,9 @@ __device__ bool encode_var(const uint8_t *__restrict__ line, uint32_t len, Ring 
     const uint32_t lo16 = BPL * l;
     VarState f;
     f.nf = 0; f.carryT = 1; f.gt0 = -1; f.T = 0; f.phi = 0; f.pcls = CLS_NONE; f.prs = 0; f.esc = 0; f.ntok = 0;
-    f.nlc = nlc ? 1u : 0u; f.nlhit = 0;
+    f.nlc = nlc ? 1u : 0u; f.nlhit = 0; f.defer = 0; f.sizeonly = 0;
     *nlhit = false;
+    *deferred = false;
     r.wpos = 8;
     r.fpos = 0;
     // prefix phase: as encode_fast
@@ -1314,6 +1341,7 @@ __device__ bool encode_var(const uint8_t *__restrict__ line, uint32_t len, Ring 
     const uint32_t phi = f.phi, NH = f.T;
     const vw::brsrc rsG = vw::make_rsrc(line + f.gt0 - phi, (phi + len - (uint32_t)f.gt0 + 3u) & ~3u);
     const uint32_t ncG = (NH + HPC - 1) / HPC;
+    f.defer = defer_ok && ncG > 1 ? 1u : 0u;
     const uint32_t lo32 = BPL8 * l;
     // three chunks in flight, a single loop exit (see encode_fast)
     Chunk8v b0 = load_chunk8v(rsG, 0, lo32);
@@ -1354,6 +1382,7 @@ __device__ bool encode_var(const uint8_t *__restrict__ line, uint32_t len, Ring 
     ring_flush_var(r);   // (< 512 pending: the final partial burst stays inside one staging region)
     ring_finish(r, (uint32_t)f.gt0);
     *rec_bytes = r.wpos;
+    *deferred = f.sizeonly != 0;
     return true;
 }
 
@@ -1611,6 +1640,7 @@ __device__ __forceinline__ bool row_setup(const VcfcEncodeArgs &a, uint64_t row,
     r.slot = a.slots + a.slot_off[row];
     r.wpos = 8;
     r.fpos = 0;
+    r.mode = RING_STAGE;
     if (a.slot_off[row + 1] > a.slots_cap) {
         if (vw::lane_id() == 0) {
             a.rec_size[row] = 0;
@@ -1684,6 +1714,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
     const uint64_t row0 = row_lo + ((uint64_t)blockIdx.x * K1_WAVES + wave) * VAR_ROWS;
     const bool flagged = l < VAR_ROWS && row0 + l < row_hi && a.rec_size[row0 + l] == VCFCD_RETRY;
     uint64_t todo = vw::ballot(flagged);
+    uint32_t dmask = 0;   // rows deferred (bit: row - row0)
     while (todo) {
         const uint64_t row = row0 + (uint64_t)__builtin_ctzll(todo);
         todo &= todo - 1;
@@ -1695,8 +1726,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
         // (round 4; a separate scan of every flagged row cost law 2 ~1 ms on
         // the device file), the general path scans the row first.
         uint32_t bytes = 0;
-        bool nlhit = false;
-        const bool var_ok = encode_var(a.buf + a.line_off[row], a.line_len[row], r, &bytes, a.nl_check, &nlhit);
+        bool nlhit = false, deferred = false;
+        const bool var_ok =
+            encode_var(a.buf + a.line_off[row], a.line_len[row], r, &bytes, a.nl_check, &nlhit, true, &deferred);
         if (!var_ok && !nlhit && a.nl_check) nlhit = row_has_nl(a.buf + a.line_off[row], a.line_len[row]);
         if (nlhit) {
             if (l == 0) {
@@ -1706,7 +1738,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
             continue;
         }
         if (var_ok) {
-            if (l == 0) a.rec_size[row] = bytes;
+            if (l == 0) a.rec_size[row] = deferred ? (bytes | VCFCD_DEFER) : bytes;
+            if (deferred) dmask |= 1u << (uint32_t)(row - row0);
             continue;
         }
         // not the variable-token shape: the general path, in this wave
@@ -1718,7 +1751,48 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
             if (st != VCFCD_OK) atomicMin((unsigned long long *)a.err, (unsigned long long)((row << 8) | st));
         }
     }
+    if (dmask) {   // one append per wave
+        uint32_t q0 = 0;
+        if (l == 0) q0 = atomicAdd(a.defer_count, (uint32_t)__builtin_popcount(dmask));
+        q0 = vw::readfirst(q0);
+        if (l < VAR_ROWS && ((dmask >> l) & 1u))
+            a.defer_list[q0 + (uint32_t)__builtin_popcount(dmask & ((1u << l) - 1u))] = (uint32_t)(row0 + l);
+    }
 }
+
+// Deferred rows (VCFCD_DEFER): after the size scan and the compaction, each
+// record is encoded again from its line straight into out at rec_off[row]
+// (RING_DIRECT; whole 16-byte blocks, the last few bytes one by one, so a
+// neighbour's bytes -- the compaction's -- are never touched).  A resident
+// grid strides over the deferred-row list; an empty list costs the launch.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) void k_encode_defer(VcfcEncodeArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[K1_WAVES * RING_STRIDE];
+    const uint32_t wave = vw::readfirst(threadIdx.x >> 6);
+    const uint32_t l = vw::lane_id();
+    const uint32_t cnt = vw::readfirst(*a.defer_count);
+    const uint32_t G = gridDim.x * K1_WAVES;
+    for (uint32_t q = blockIdx.x * K1_WAVES + wave; q < cnt; q += G) {
+        const uint64_t row = vw::readfirst(a.defer_list[q]);
+        const uint32_t size = a.rec_size[row] & ~VCFCD_DEFER;
+        const uint64_t o = a.rec_off[row];
+        if (o + size > a.out_cap) continue;   // (the size scan reported it)
+        Ring r;
+        r.lds = lds + wave * RING_STRIDE;
+        r.prim = a.out + o;
+        r.slot = nullptr;
+        r.pb = 0xFFFFFFFFu;
+        r.wpos = 8;
+        r.fpos = 0;
+        r.mode = RING_DIRECT;
+        uint32_t bytes = 0;
+        bool nlhit = false, deferred = false;
+        const bool ok = encode_var(a.buf + a.line_off[row], a.line_len[row], r, &bytes, false, &nlhit, false, &deferred);
+        if (l == 0 && (!ok || bytes != size))   // (cannot happen: the same code sized it)
+            atomicMin((unsigned long long *)a.err, (unsigned long long)((row << 8) | VCFCD_E_INTERNAL));
+    }
+}
+
+constexpr uint32_t DEFER_BLOCKS = 1280;   // 5 waves per SIMD over 256 CUs, 4 waves per block
 
 // blocks of k_encode_var to launch for m rows
 static uint64_t var_blocks(uint64_t m, uint32_t rows_per_wave = VAR_ROWS) {
@@ -1769,10 +1843,15 @@ __device__ __forceinline__ uint4 merge16(uint4 a, uint4 b, uint32_t s) {
                       (a.w & m3) | (sh.w & ~m3));
 }
 
+// Blocks wholly inside deferred records (VCFCD_DEFER) are skipped: k_encode_defer
+// writes those records afterwards (a block shared with a staged record is
+// written here with whatever the deferred record's staging holds, and
+// k_encode_defer then rewrites the deferred record's bytes of it).
 __global__ __launch_bounds__(256) void k_compact_out(const uint8_t *__restrict__ prims,
                                                      const uint8_t *__restrict__ slots,
                                                      const uint64_t *__restrict__ slot_off,
-                                                     const uint64_t *__restrict__ rec_off, uint64_t n,
+                                                     const uint64_t *__restrict__ rec_off,
+                                                     const uint32_t *__restrict__ rec_size, uint64_t n,
                                                      const uint32_t *__restrict__ tile_first,
                                                      uint8_t *__restrict__ out, uint64_t out_cap, uint32_t pb) {
     const uint32_t l = vw::lane_id();
@@ -1788,6 +1867,9 @@ __global__ __launch_bounds__(256) void k_compact_out(const uint8_t *__restrict__
         // past n start "at infinity"
         const uint64_t ro = r0 + l <= n ? rec_off[r0 + l] : ~0ull;
         const uint64_t so = r0 + l < n ? slot_off[r0 + l] : 0;
+        // deferred rows among them (a tile meeting more than 63 rows holds
+        // only short records, never a deferred one)
+        const uint64_t dfm = vw::ballot(r0 + l < n && (rec_size[r0 + l] & VCFCD_DEFER));
         // rows that start before the tile ends; a tile over more than 63
         // rows (records of < 64 B on average) takes the rows in batches
         uint64_t base = r0;   // row of lane 0's values
@@ -1826,6 +1908,7 @@ __global__ __launch_bounds__(256) void k_compact_out(const uint8_t *__restrict__
             const uint64_t o = o0 + 16u * (l + 64u * k);
             if (o >= lim) continue;
             const uint64_t r = r0 + idx[k];
+            if (idx2[k] < 64 && ((dfm >> idx[k]) & (dfm >> idx2[k]) & 1u)) continue;   // (idx <= idx2)
             const uint64_t x = o - st[k];   // offset in the record
             const uint8_t *prim = prims + (uint64_t)pb * r;
             const uint8_t *slot = slots + sl[k];
@@ -1850,11 +1933,11 @@ __global__ __launch_bounds__(256) void k_compact_out(const uint8_t *__restrict__
 
 // ---------------------------------------------------------------------------
 // Exclusive scan u32 -> u64 (n + 1 outputs).  MODE 0: identity, MODE 1:
-// vcfc_slot_bytes(len).  4096 items per 256-thread block.
+// vcfc_slot_bytes(len), MODE 2: record sizes (VCFCD_DEFER masked).  4096 items per 256-thread block.
 constexpr int SCAN_ITEMS = 16, SCAN_THREADS = 256, SCAN_TILE = SCAN_ITEMS * SCAN_THREADS;
 
 template <int MODE> __device__ __forceinline__ uint64_t scan_xf(uint32_t v) {
-    return MODE == 1 ? vcfc_slot_bytes(v) : (uint64_t)v;
+    return MODE == 1 ? vcfc_slot_bytes(v) : MODE == 2 ? (uint64_t)(v & ~VCFCD_DEFER) : (uint64_t)v;
 }
 
 __device__ uint64_t block_excl_scan_u64(uint64_t v, uint64_t *sh, uint64_t *total) {
@@ -2050,8 +2133,10 @@ VcfcWorkspaceLayout vcfc_encode_workspace_layout(uint64_t n, uint64_t total_line
     const uint64_t nt = (n + SCAN_TILE - 1) / SCAN_TILE + 1;
     L.lb = o;
     L.retry_count = o + 8;
+    L.defer_count = o + 12;
     L.lb_bytes = 16 + 16 * nt;
     o = al(o + L.lb_bytes);
+    L.defer_list = o; o = al(o + 4 * n);
     L.tile_first = o; o = al(o + 4 * (vcfc_record_bound(n, total_line_bytes) / CT + 2));
     L.prim_bytes = vcfc_prim_bytes(n, total_line_bytes);
     L.prim = o; o = al(o + (uint64_t)L.prim_bytes * n);
@@ -2087,7 +2172,7 @@ hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t s, hipEvent_t
     hipLaunchKernelGGL(k_encode_var, dim3((unsigned)var_blocks(a.n)), dim3(64 * K1_WAVES), 0, s, a, (uint64_t)0, a.n);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[2], s);
-    hipLaunchKernelGGL((k_scan_lb<0, true>), dim3((unsigned)nt), dim3(SCAN_THREADS), 0, s, a.rec_size, a.n,
+    hipLaunchKernelGGL((k_scan_lb<2, true>), dim3((unsigned)nt), dim3(SCAN_THREADS), 0, s, a.rec_size, a.n,
                        tickets + 1, flags_b, a.rec_off, a.tile_first, a.out_cap, a.err);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[3], s);
@@ -2095,7 +2180,13 @@ hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t s, hipEvent_t
     const uint64_t tiles = vcfc_record_bound(a.n, a.line_bytes_hint) / CT + 1;
     const uint64_t cblocks = tiles < 8192 ? (tiles + 3) / 4 : 2048;
     hipLaunchKernelGGL(k_compact_out, dim3((unsigned)cblocks), dim3(256), 0, s, a.prim, a.slots, a.slot_off,
-                       a.rec_off, a.n, a.tile_first, a.out, a.out_cap, a.prim_bytes);
+                       a.rec_off, a.rec_size, a.n, a.tile_first, a.out, a.out_cap, a.prim_bytes);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    // the deferred rows' records, straight into out (a resident grid; exits
+    // at once when k_encode_var deferred none)
+    const uint64_t dblocks = (a.n + K1_WAVES - 1) / K1_WAVES;
+    hipLaunchKernelGGL(k_encode_defer, dim3((unsigned)(dblocks < DEFER_BLOCKS ? dblocks : DEFER_BLOCKS)),
+                       dim3(64 * K1_WAVES), 0, s, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[4], s);
     return hipSuccess;
