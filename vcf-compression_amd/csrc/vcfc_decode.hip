@@ -56,7 +56,7 @@ __device__ __forceinline__ uint32_t umin32(uint32_t a, uint32_t b) { return a < 
 // bit i set <=> byte i of w is zero (exact)
 __device__ __forceinline__ uint32_t zero_bytes4(uint32_t w) {
     const uint32_t t = ~(((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w | 0x7F7F7F7Fu);
-    return ((t >> 7) & 1u) | ((t >> 14) & 2u) | ((t >> 21) & 4u) | ((t >> 28) & 8u);
+    return vw::gather4(t >> 7);
 }
 
 __device__ __forceinline__ uint32_t be30(const uint8_t *h) {
@@ -162,7 +162,7 @@ struct ItemLane {
 
 // bit j <- bit 8j + 7 of x (one flag per byte, as 0x80 in that byte)
 __device__ __forceinline__ uint32_t msb4(uint32_t x) {
-    return ((x >> 7) & 1u) | ((x >> 14) & 2u) | ((x >> 21) & 4u) | ((x >> 28) & 8u);
+    return vw::gather4((x >> 7) & 0x01010101u);
 }
 // bits [lo, hi) of a 4-bit mask (0 <= lo, hi <= 4)
 __device__ __forceinline__ uint32_t bits4(uint32_t lo, uint32_t hi) {
