@@ -1857,6 +1857,7 @@ __global__ __launch_bounds__(256) void k_compact_out(const uint8_t *__restrict__
     const uint32_t l = vw::lane_id();
     const uint64_t g = (uint64_t)blockIdx.x * 4 + vw::readfirst(threadIdx.x >> 6);
     const uint64_t G = (uint64_t)gridDim.x * 4;
+    const uint32_t pbs = 31u - (uint32_t)__builtin_clz(pb);   // prim_bytes is a power of two (vcfc_prim_bytes)
     const uint64_t total = rec_off[n];
     const uint64_t lim = total < out_cap ? total : out_cap;
     const uint64_t ntile = (lim + CT - 1) / CT;
@@ -1910,12 +1911,12 @@ __global__ __launch_bounds__(256) void k_compact_out(const uint8_t *__restrict__
             const uint64_t r = r0 + idx[k];
             if (idx2[k] < 64 && ((dfm >> idx[k]) & (dfm >> idx2[k]) & 1u)) continue;   // (idx <= idx2)
             const uint64_t x = o - st[k];   // offset in the record
-            const uint8_t *prim = prims + (uint64_t)pb * r;
+            const uint8_t *prim = prims + (r << pbs);
             const uint8_t *slot = slots + sl[k];
             uint4 v = x + 16 <= pb ? vw::uload16(prim + x) : x >= pb ? vw::uload16(slot + (x - pb)) : vw::uload16(prim + x);
             if (x < pb && x + 16 > pb) v = merge16(v, vw::uload16(slot), (uint32_t)(pb - x));
             if (o + 16 > en[k] && en[k] < lim)   // the next non-empty record starts at en
-                v = merge16(v, vw::uload16(prims + (uint64_t)pb * (r0 + idx2[k])), (uint32_t)(en[k] - o));
+                v = merge16(v, vw::uload16(prims + ((r0 + idx2[k]) << pbs)), (uint32_t)(en[k] - o));
             if (o + 16 <= lim) {
                 // non-temporal: the records leave the chip (D2H, a file, the
                 // next stage), and the next batch's encode keeps L2 / MALL to
