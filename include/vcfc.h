@@ -115,8 +115,10 @@ int vcfc_encode_rows_device(const uint8_t *d_buf, const uint64_t *d_line_off,
 /* Per-stage timing of vcfc_encode_rows_device (HIP events on the same
  * stream).  vcfc_timer_read synchronises and returns the per-stage totals in
  * ms summed over the timed calls since the last read:
- *   ms[0] slot-offset scan, ms[1] k_encode, ms[2] record-offset scan,
- *   ms[3] k_compact;  *calls = number of timed calls. */
+ *   ms[0] slot-offset scan, ms[1] k_encode (the fast and variable-token
+ *   kernels, plus k_encode_defer's deferred records after the compaction),
+ *   ms[2] record-offset scan, ms[3] k_compact;  *calls = number of timed
+ *   calls. */
 typedef struct vcfc_timer vcfc_timer;
 int vcfc_timer_create(vcfc_timer **t);
 void vcfc_timer_destroy(vcfc_timer *t);

@@ -8,7 +8,7 @@ import json
 import sys
 from collections import defaultdict
 
-KERNELS = ("k_encode_fast", "k_encode_var", "k_encode_general", "k_compact_out")
+KERNELS = ("k_encode_fast", "k_encode_var", "k_encode_general", "k_encode_defer", "k_compact_out")
 
 
 def per_kernel(d, counter):
@@ -28,7 +28,7 @@ def main():
         fb, wb = int(f.get(k, 0) * 1024 * 2), int(w.get(k, 0) * 1024)
         kern[k] = {"fetch_bytes": fb, "write_bytes": wb, "hbm_bytes": fb + wb}
     enc = [k for k in KERNELS if k != "k_compact_out"]
-    res = {"workload": key, "kernel": "k_encode (k_encode_fast + k_encode_var)", "source": note,
+    res = {"workload": key, "kernel": "k_encode (k_encode_fast + k_encode_var + k_encode_defer)", "source": note,
            "fetch_bytes_per_launch": sum(kern[k]["fetch_bytes"] for k in enc),
            "write_bytes_per_launch": sum(kern[k]["write_bytes"] for k in enc),
            "hbm_bytes_per_launch": sum(kern[k]["hbm_bytes"] for k in enc),

@@ -119,8 +119,9 @@ inline void vcfc_encode_args_workspace(VcfcEncodeArgs &a, uint8_t *ws, const Vcf
 }
 
 // Enqueue the whole encode on `stream` (no host synchronisation, capturable).
-// If `ev` is non-null, ev[0..4] are recorded before the slot scan, after it,
-// after k_encode, after the size scan and after k_compact.
+// If `ev` is non-null, ev[0..5] are recorded before the slot scan, after it,
+// after k_encode (fast + variable-token kernels), after the size scan, after
+// k_compact and after k_encode_defer.
 hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t stream, hipEvent_t *ev = nullptr);
 
 // ---------------------------------------------------------------------------

@@ -2183,13 +2183,14 @@ hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t s, hipEvent_t
     hipLaunchKernelGGL(k_compact_out, dim3((unsigned)cblocks), dim3(256), 0, s, a.prim, a.slots, a.slot_off,
                        a.rec_off, a.rec_size, a.n, a.tile_first, a.out, a.out_cap, a.prim_bytes);
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (ev) (void)hipEventRecord(ev[4], s);
     // the deferred rows' records, straight into out (a resident grid; exits
     // at once when k_encode_var deferred none)
     const uint64_t dblocks = (a.n + K1_WAVES - 1) / K1_WAVES;
     hipLaunchKernelGGL(k_encode_defer, dim3((unsigned)(dblocks < DEFER_BLOCKS ? dblocks : DEFER_BLOCKS)),
                        dim3(64 * K1_WAVES), 0, s, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    if (ev) (void)hipEventRecord(ev[4], s);
+    if (ev) (void)hipEventRecord(ev[5], s);
     return hipSuccess;
 }
 
