@@ -74,12 +74,6 @@ inline uint32_t alignbit(uint32_t hi, uint32_t lo, uint32_t s) {
 }
 inline int32_t sext24(int32_t v) { return (int32_t)((uint32_t)v << 8) >> 8; }
 inline int32_t mad24(int32_t a, int32_t b, int32_t x) { return (int32_t)((uint32_t)x + (uint32_t)(sext24(a) * sext24(b))); }
-// bit `bit` of x sign-extended: 0 or -1 (v_bfe_i32 width 1)
-inline int32_t bitmask(uint32_t x, uint32_t bit) { return ((x >> bit) & 1u) ? -1 : 0; }
-// dot product of the bytes of x with (1, 2, 4, 8) (v_dot4_u32_u8)
-inline uint32_t gather4(uint32_t x) {
-    return (x & 0xFFu) + 2u * ((x >> 8) & 0xFFu) + 4u * ((x >> 16) & 0xFFu) + 8u * (x >> 24);
-}
 inline void wave_sync() { emu::collective(emu::OP_WAVESYNC, 0, 0, 0); }
 // lowest set bit index; value unspecified for 0 (v_ffbl_b32: callers must not use it)
 inline uint32_t ffbl(uint32_t x) { return (uint32_t)__builtin_ctz(x); }

@@ -11,3 +11,4 @@ VCFC_LAW2_KIND=1 AB_ARGS="--law 2" bash tools/ab.sh ab_defer_kind1 build_ab/head
 VCFC_LAW2_KIND=0 AB_ARGS="--law 2" bash tools/ab.sh ab_mask_kind0 build_ab/head/libvcfc.so build_ab/mask/libvcfc.so || exit 1
 bash tools/abdec.sh ab_dec128 build_ab/head/libvcfc.so build_ab/dec128/libvcfc.so build_ab/mask/libvcfc.so || exit 1
 AB_ARGS="--law 2" bash tools/abdev.sh ab_defer_dev2 build_ab/head/libvcfc.so build_ab/mask/libvcfc.so || exit 1
+bash tools/ab.sh ab_warm_law1 build_ab/mask/libvcfc.so build_ab/warm/libvcfc.so || exit 1

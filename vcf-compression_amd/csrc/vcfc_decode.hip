@@ -56,7 +56,7 @@ __device__ __forceinline__ uint32_t umin32(uint32_t a, uint32_t b) { return a < 
 // bit i set <=> byte i of w is zero (exact)
 __device__ __forceinline__ uint32_t zero_bytes4(uint32_t w) {
     const uint32_t t = ~(((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w | 0x7F7F7F7Fu);
-    return vw::gather4(t >> 7);
+    return ((t >> 7) & 1u) | ((t >> 14) & 2u) | ((t >> 21) & 4u) | ((t >> 28) & 8u);
 }
 
 __device__ __forceinline__ uint32_t be30(const uint8_t *h) {
@@ -162,7 +162,7 @@ struct ItemLane {
 
 // bit j <- bit 8j + 7 of x (one flag per byte, as 0x80 in that byte)
 __device__ __forceinline__ uint32_t msb4(uint32_t x) {
-    return vw::gather4((x >> 7) & 0x01010101u);
+    return ((x >> 7) & 1u) | ((x >> 14) & 2u) | ((x >> 21) & 4u) | ((x >> 28) & 8u);
 }
 // bits [lo, hi) of a 4-bit mask (0 <= lo, hi <= 4)
 __device__ __forceinline__ uint32_t bits4(uint32_t lo, uint32_t hi) {
@@ -394,7 +394,7 @@ __global__ __launch_bounds__(256) void k_dec_seq(VcfcDecodeArgs a) {
     }
 }
 
-__device__ __forceinline__ void write_one(const VcfcDecodeArgs &a, uint64_t i, uint8_t *sb, uint32_t *W, uint32_t *O) {
+__device__ __forceinline__ void write_one(const VcfcDecodeArgs &a, uint64_t i, uint8_t *sb, uint32_t *W) {
     const uint32_t l = vw::lane_id();
     const uint64_t rs_abs = a.rec_start[i];
     const uint64_t L0 = a.line_off[i];
@@ -453,48 +453,9 @@ __device__ __forceinline__ void write_one(const VcfcDecodeArgs &a, uint64_t i, u
     // in-lane, then across lanes by a max-scan of lane indices and one
     // ds_bpermute) and goes out as contiguous 16-byte stores.  Work per tile
     // does not depend on run lengths.
-    constexpr uint32_t PL = TB / 64;   // slots per lane (4: one 16-byte group)
+    constexpr uint32_t PL = TB / 64;   // slots per lane
     for (uint32_t q = 0; q < PL; q += 4) *reinterpret_cast<uint4 *>(W + PL * l + q) = make_uint4(0, 0, 0, 0);
     uint32_t j0 = 0, carry = 0;   // tile start; word of the item holding token j0
-    // 128-byte aligned stores (round 4): the tile's 1 KiB goes out as the
-    // 1 KiB window starting M groups and r bytes (m = 16 M + r = the token
-    // stream's misalignment mod 128) before it -- its first m bytes the
-    // previous tile's last, kept in the 128 bytes below O -- so no store
-    // instruction splits a 128-byte line inside the line (tools/write_probe:
-    // 2.05 ms against 2.18 for the stores at the line's own alignment).
-    // Stream bytes outside [0, 4S) (REQ' before, the next line after) are
-    // never written: the blocks that meet them store byte by byte.
-    const uint32_t m = (uint32_t)(reinterpret_cast<uintptr_t>(tok) & 127u);
-    const uint32_t Mg = m >> 4, rb = m & 15u;
-    const uint8_t *Ob = reinterpret_cast<const uint8_t *>(O);   // the filled tile (W keeps collecting item words)
-    // the block at tile-relative byte b (16-aligned relative to the window):
-    // groups g - 1 and g of the tile (g = l - Mg; negative: the previous
-    // tile's tail), realigned by rb bytes
-    auto block = [&](int32_t g) -> uint4 {
-        const uint4 lo = *reinterpret_cast<const uint4 *>(Ob + 16 * (g - 1));
-        const uint4 hi = *reinterpret_cast<const uint4 *>(Ob + 16 * g);
-        if (rb == 0) return hi;
-        const uint32_t s4 = 16u - rb, q = s4 >> 2, sb = s4 & 3u;
-        const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-        uint32_t o[5];
-#pragma unroll
-        for (int i = 0; i < 5; i++) {
-            const int a0 = i, a1 = i + 1 < 8 ? i + 1 : 7, a2 = i + 2 < 8 ? i + 2 : 7, a3 = i + 3 < 8 ? i + 3 : 7;
-            o[i] = q == 0 ? w[a0] : q == 1 ? w[a1] : q == 2 ? w[a2] : w[a3];
-        }
-        return make_uint4(vw::alignbyte(o[1], o[0], sb), vw::alignbyte(o[2], o[1], sb),
-                          vw::alignbyte(o[3], o[2], sb), vw::alignbyte(o[4], o[3], sb));
-    };
-    // store block v at stream byte sp: whole when inside [0, end), else its bytes inside
-    auto put = [&](int64_t sp, uint4 v, int64_t end) {
-        if (sp >= 0 && sp + 16 <= end) {
-            vw::gstore16(tok, (uint64_t)sp, v);
-        } else if (sp + 16 > 0 && sp < end) {
-            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-            for (int32_t i = 0; i < 16; i++)
-                if (sp + i >= 0 && sp + i < end) tok[sp + i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
-        }
-    };
     // LAST: the line's last tile (n_tok tokens, its LF replacing the last
     // TAB, partial stores); the others are whole tiles of TB tokens
     auto tile_out = [&](auto last_tag, uint32_t n_tok) {
@@ -520,23 +481,27 @@ __device__ __forceinline__ void write_one(const VcfcDecodeArgs &a, uint64_t i, u
 #pragma unroll
         for (uint32_t q = 0; q < PL; q++) w[q] = w[q] ? w[q] : enter;
         const uint32_t t0 = j0 + PL * l;
-        if (LAST) {
+        if (!LAST) {
+#pragma unroll
+            for (uint32_t q = 0; q < PL; q += 4)
+                // plain stores: 2.645 -> 2.49 ms against non-temporal ones in
+                // an A/B (profiles/r03/ab/ab_dec_plain.txt; tools/write_probe.hip:
+                // one wave per 10 KB line writes 10.19 GB in 2.07 ms plain,
+                // 2.25 ms non-temporal)
+                vw::gstore16(tok, 4ull * (t0 + q), make_uint4(w[q], w[q + 1], w[q + 2], w[q + 3]));
+        } else {
 #pragma unroll
             for (uint32_t q = 0; q < PL; q++)
                 if (t0 + q + 1 == S) w[q] = (w[q] & 0x00FFFFFFu) | 0x0A000000u;
+            if (t0 + PL <= j0 + n_tok) {
+#pragma unroll
+                for (uint32_t q = 0; q < PL; q += 4)
+                    vw::gstore16(tok, 4ull * (t0 + q), make_uint4(w[q], w[q + 1], w[q + 2], w[q + 3]));
+            } else {
+                for (uint32_t q = 0; q < PL; q++)
+                    if (t0 + q < j0 + n_tok) *reinterpret_cast<uint32_t *>(tok + 4ull * (t0 + q)) = w[q];
+            }
         }
-        // the filled tile to O, then each lane's 128-B-window block (plain
-        // stores: 2.645 -> 2.49 ms against non-temporal ones in an A/B,
-        // profiles/r03/ab/ab_dec_plain.txt)
-        *reinterpret_cast<uint4 *>(O + PL * l) = make_uint4(w[0], w[1], w[2], w[3]);
-        vw::wave_sync();
-        const int64_t end = LAST ? 4ll * S : (int64_t)1 << 62;
-        const int32_t g = (int32_t)l - (int32_t)Mg;
-        put(4ll * j0 + 16ll * g - rb, block(g), end);
-        if (LAST && g < 1) put(4ll * j0 + 1024 + 16ll * g - rb, block(g + 64), end);   // the tile's last m bytes
-        vw::wave_sync();
-        // this tile's last 128 bytes below O for the next tile's first window
-        if (!LAST && l >= 56) *reinterpret_cast<uint4 *>(O + 4 * ((int32_t)l - 64)) = make_uint4(w[0], w[1], w[2], w[3]);
         carry = vw::readlane(w[PL - 1], 63);
         vw::wave_sync();
     };
@@ -596,23 +561,19 @@ template <bool SEL>
 __global__ __launch_bounds__(256) void k_dec_write(VcfcDecodeArgs a, uint64_t first, uint64_t last) {
     __shared__ __attribute__((aligned(16))) uint8_t sbuf[DEC_WAVES * SBUF];
     __shared__ __attribute__((aligned(16))) uint32_t tbuf[DEC_WAVES * (TB + 4)];   // tile + the shared dummy word (16-B padded)
-    // per wave: the previous tile's last 128 bytes, the filled tile, the
-    // aligned stores' 16-byte overhang
-    __shared__ __attribute__((aligned(16))) uint32_t obuf[DEC_WAVES * (32 + TB + 4)];
     const uint32_t wave = vw::readfirst(threadIdx.x >> 6);
     uint8_t *sb = sbuf + wave * SBUF;
     uint32_t *W = tbuf + wave * (TB + 4);
-    uint32_t *O = obuf + wave * (32 + TB + 4) + 32;
     const uint64_t g = (uint64_t)blockIdx.x * DEC_WAVES + wave;
     if (!SEL) {
-        if (first + g < last) write_one(a, first + g, sb, W, O);
+        if (first + g < last) write_one(a, first + g, sb, W);
         return;
     }
     const uint64_t G = (uint64_t)gridDim.x * DEC_WAVES;
     const uint32_t l = vw::lane_id();
     const uint64_t il = first + g + (uint64_t)l * G;
     for (uint64_t m = vw::ballot(l < SEL_R && il < last && a.select[il]); m; m &= m - 1)
-        write_one(a, first + g + (uint64_t)__builtin_ctzll(m) * G, sb, W, O);
+        write_one(a, first + g + (uint64_t)__builtin_ctzll(m) * G, sb, W);
 }
 
 // Byte-serial decode of [p, n), at most max_lines lines: out == nullptr

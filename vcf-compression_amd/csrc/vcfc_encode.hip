@@ -73,7 +73,7 @@ __device__ __forceinline__ uint32_t cls_of(uint32_t k) {
 __device__ __forceinline__ uint32_t zero_bytes4(uint32_t w) {
     uint32_t t = ((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w | 0x7F7F7F7Fu;
     t = ~t;  // 0x80 in every zero byte
-    return vw::gather4(t >> 7);
+    return ((t >> 7) * 0x00204081u >> 21) & 0xFu;
 }
 __device__ __forceinline__ uint32_t tab_mask16(uint4 v) {
     return zero_bytes4(v.x ^ 0x09090909u) | (zero_bytes4(v.y ^ 0x09090909u) << 4) |
@@ -710,8 +710,8 @@ __device__ __forceinline__ void esc8(const uint32_t (&d)[TPL8], int32_t t0, int3
     // run begun at the previous start: lead = mask(class) + length, where the
     // class table gives 0x08 for an escape predecessor, whose run has length
     // 1 (0x09 = TAB).  Per slot: the byte's address is dm + s * (lb + o - dm)
-    // (s, e in {0, 1}; a sign-extended bit ANDed with the offset, one
-    // full-rate VALU), and the offsets advance by s and 4 e.
+    // (s, e in {0, 1}; one 24-bit multiply-add instead of a compare and a
+    // select), and the offsets advance by s and 4 e.
     *(lead1 ? lb + o : dm) = (uint8_t)b1;
     o += lead1 ? 1u : 0u;
     const uint32_t sbr = sb & (sb - 1u);   // starts after the first
@@ -720,17 +720,17 @@ __device__ __forceinline__ void esc8(const uint32_t (&d)[TPL8], int32_t t0, int3
     const uint32_t mL = vw::perm(0x08u, 0x80C0A000u, cpL & 0x07070707u) + 0x03020100u;   // mask + slot index
     const uint32_t mH = vw::perm(0x08u, 0x80C0A000u, cpH & 0x07070707u) + 0x07060504u;
     int32_t njp = -(int32_t)j1;   // minus the previous start
-    int32_t ro = ldm + (int32_t)o;   // base + o - dummy
 #pragma unroll
     for (int j = 0; j < (int)TPL8; j++) {
-        const int32_t ms = vw::bitmask(sbr, 4 * j), me = vw::bitmask(eb, 4 * j);   // 0 / -1
+        const int32_t s = (int32_t)((sbr >> (4 * j)) & 1u);
+        const int32_t e = (int32_t)((eb >> (4 * j)) & 1u);
         const uint32_t b = ((((j < 4) ? mL : mH) >> (8 * (j & 3))) & 0xFFu) + (uint32_t)njp;
-        r.lds[dmi + (uint32_t)(ro & ms)] = (uint8_t)b;
-        ro -= ms;
+        r.lds[(uint32_t)vw::mad24(s, ldm + (int32_t)o, (int32_t)dmi)] = (uint8_t)b;
+        o += (uint32_t)s;
         const uint32_t pay = (d[j] << 8) | 0xE1u;   // 0xE1, then the token's three bytes
-        __builtin_memcpy(r.lds + (dmi + (uint32_t)(ro & me)), &pay, 4);
-        ro += me & 4;
-        njp = (njp & ~ms) | (-j & ms);
+        __builtin_memcpy(r.lds + (uint32_t)vw::mad24(e, ldm + (int32_t)o, (int32_t)dmi), &pay, 4);
+        o += 4u * (uint32_t)e;
+        njp = s ? -j : njp;
     }
     ring_unwrap(r, base + cnt);
     r.wpos += vw::readlane(incl2, 63);
@@ -1146,13 +1146,14 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
         } else {
 #pragma unroll
         for (int h = 0; h < 16; h++) {
-            const int32_t ms = vw::bitmask(S, h), m1 = vw::bitmask(vm, h), m2 = vw::bitmask(vm2, h);
+            const int32_t es = (int32_t)((S >> h) & 1u);
+            const int32_t e1 = (int32_t)((vm >> h) & 1u), e2 = (int32_t)((vm2 >> h) & 1u);
             const uint32_t pay = d[h >> 1] >> (16 * (h & 1));
-            r.lds[dmi + (ro & ms)] = (uint8_t)0xE1u;
-            ro -= ms;
-            r.lds[dmi + (ro & m1)] = (uint8_t)pay;
-            r.lds[dmi + ((ro + 1) & m2)] = (uint8_t)(pay >> 8);
-            ro -= m1 + m2;
+            r.lds[(uint32_t)vw::mad24(es, ro, dmi)] = (uint8_t)0xE1u;
+            ro += es;
+            r.lds[(uint32_t)vw::mad24(e1, ro, dmi)] = (uint8_t)pay;
+            r.lds[(uint32_t)vw::mad24(e2, ro + 1, dmi)] = (uint8_t)(pay >> 8);
+            ro += e1 + e2;
         }
         }
 #endif
@@ -1174,7 +1175,7 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
     // byte after each half, i.e. the next half's first; bit 0 of the bytes
     // of A / B gathered by one multiply)
     uint32_t p3 = 0, am = 0, bm = 0;
-    auto bits0 = [](uint32_t x) { return vw::gather4(x & 0x01010101u); };
+    auto bits0 = [](uint32_t x) { return (((x & 0x01010101u) * 0x01020408u) >> 24) & 0xFu; };
     uint32_t An = vw::perm(d[1], d[0], 0x06040200u);
 #pragma unroll
     for (int k = 0; k < 4; k++) {
@@ -1272,22 +1273,21 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
     uint32_t tk = 0, ptk = 0;   // token index (in the lane) of half h; of the run start before it
 #pragma unroll
     for (int h = 0; h < 16; h++) {
-        // 0 / -1 masks of the half's bits (stores addressed dummy + (ro & mask))
-        const int32_t ml = vw::bitmask(LEAD, h), mes = vw::bitmask(XE, h), mr = vw::bitmask(LEADr, h);
-        const int32_t m1 = vw::bitmask(EH, h), m2 = vw::bitmask(EH2, h);
+        const int32_t hl = (int32_t)((LEAD >> h) & 1u), es = (int32_t)((XE >> h) & 1u);
+        const int32_t hr = (int32_t)((LEADr >> h) & 1u);
+        const int32_t e1 = (int32_t)((EH >> h) & 1u), e2 = (int32_t)((EH2 >> h) & 1u);
         const uint32_t pc = (pcw >> (2 * h)) & 3u;    // predecessor class (plain when hr)
         const uint32_t lb = vw::perm(0x80C0A000u, 0x80C0A000u, pc) | (tk - ptk);
-        const uint32_t mrs = (uint32_t)vw::bitmask(RS, h);
-        ptk = (tk & mrs) | (ptk & ~mrs);
+        ptk = (RS >> h) & 1u ? tk : ptk;
         tk += (S >> h) & 1u;
         const uint32_t pay = d[h >> 1] >> (16 * (h & 1));
-        r.lds[dmi + (ro & mr)] = (uint8_t)lb;
-        ro -= ml;
-        r.lds[dmi + (ro & mes)] = (uint8_t)0xE1u;
-        ro -= mes;
-        r.lds[dmi + (ro & m1)] = (uint8_t)pay;
-        r.lds[dmi + ((ro + 1) & m2)] = (uint8_t)(pay >> 8);
-        ro -= m1 + m2;
+        r.lds[(uint32_t)vw::mad24(hr, ro, dmi)] = (uint8_t)lb;
+        ro += hl;
+        r.lds[(uint32_t)vw::mad24(es, ro, dmi)] = (uint8_t)0xE1u;
+        ro += es;
+        r.lds[(uint32_t)vw::mad24(e1, ro, dmi)] = (uint8_t)pay;
+        r.lds[(uint32_t)vw::mad24(e2, ro + 1, dmi)] = (uint8_t)(pay >> 8);
+        ro += e1 + e2;
     }
 #endif
     ring_unwrap(r, base + cnt);
@@ -1830,6 +1830,7 @@ __device__ __forceinline__ uint4 realign16(uint4 lo, uint4 hi, uint32_t sh) {
 // first byte.  (4 KiB tiles: 2 KiB the same, 8 KiB +45 %, ab_compact_tile.txt;
 // the round-1 row-ordered kernel was 12 % slower, ab_compact_out.txt.)
 constexpr uint32_t CTB = 4;                // 16-B blocks per lane per tile
+constexpr uint32_t TILE_DEFERRED = 0x80000000u;   // tile_first flag: the tile lies inside a deferred record
 constexpr uint32_t CT = 1024 * CTB;        // output bytes per tile
 
 // bytes [0, s) of a, then b's first 16 - s bytes (0 < s < 16)
@@ -1863,7 +1864,9 @@ __global__ __launch_bounds__(256) void k_compact_out(const uint8_t *__restrict__
     const uint64_t ntile = (lim + CT - 1) / CT;
     for (uint64_t t = g; t < ntile; t += G) {
         const uint64_t o0 = t * CT;
-        const uint64_t r0 = tile_first[t];
+        const uint32_t tfr = tile_first[t];
+        if (tfr & TILE_DEFERRED) continue;   // inside one deferred record (k_encode_defer's)
+        const uint64_t r0 = tfr;
         // rows r0 .. r0 + 63: their starts (lane j holds row r0 + j); rows
         // past n start "at infinity"
         const uint64_t ro = r0 + l <= n ? rec_off[r0 + l] : ~0ull;
@@ -2096,7 +2099,11 @@ __global__ __launch_bounds__(256) void k_scan_lb(const uint32_t *__restrict__ in
             if (TILES) {
                 const uint64_t b = run + vals[i];
                 if (b > out_cap) atomicMin((unsigned long long *)err, (unsigned long long)((r << 8) | VCFCD_E_NOSPACE));
-                for (uint64_t t = (run + CT - 1) / CT; t * CT < b; t++) tile_first[t] = (uint32_t)r;
+                // (a tile wholly inside a deferred record: flagged, the
+                // compaction skips it -- k_encode_defer writes those bytes)
+                const uint32_t dfl = MODE == 2 && (in[r] & VCFCD_DEFER) ? TILE_DEFERRED : 0u;
+                for (uint64_t t = (run + CT - 1) / CT; t * CT < b; t++)
+                    tile_first[t] = (uint32_t)r | ((t + 1) * CT <= b ? dfl : 0u);
             }
             if (r + 1 == n) out[n] = run + vals[i];
         }

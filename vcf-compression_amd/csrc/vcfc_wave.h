@@ -124,14 +124,6 @@ __device__ __forceinline__ uint32_t alignbit(uint32_t hi, uint32_t lo, uint32_t 
 }
 // x + a*b on the low 24 bits of a and b, signed (v_mad_i32_i24)
 __device__ __forceinline__ int32_t mad24(int32_t a, int32_t b, int32_t x) { return x + __mul24(a, b); }
-// bit `bit` of x sign-extended: 0 or -1 (v_bfe_i32 width 1).  A store
-// address picked by `dummy + (offset & bitmask(...))` costs one v_and_b32;
-// `mad24(flag, offset, dummy)` with a 0/1 flag is turned by the compiler
-// into v_mul_lo_u32 / v_mad_u64_u32, quarter-rate instructions
-__device__ __forceinline__ int32_t bitmask(uint32_t x, uint32_t bit) { return __builtin_amdgcn_sbfe((int32_t)x, bit, 1); }
-// bytes of x each 0 or 1 -> 4-bit mask (bit i = byte i): one v_dot4_u32_u8
-// (a gather by multiplication, x * 0x01020408 >> 24, is v_mul_lo_u32: quarter rate)
-__device__ __forceinline__ uint32_t gather4(uint32_t x) { return __builtin_amdgcn_udot4(x, 0x08040201u, 0u, false); }
 // ((hi:lo) >> 8*s)[31:0]
 __device__ __forceinline__ uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t s) {
     return __builtin_amdgcn_alignbyte(hi, lo, s);
