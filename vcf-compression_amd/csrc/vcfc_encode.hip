@@ -1844,15 +1844,15 @@ __device__ __forceinline__ uint4 merge16(uint4 a, uint4 b, uint32_t s) {
                       (a.w & m3) | (sh.w & ~m3));
 }
 
-// Blocks wholly inside deferred records (VCFCD_DEFER) are skipped: k_encode_defer
-// writes those records afterwards (a block shared with a staged record is
-// written here with whatever the deferred record's staging holds, and
-// k_encode_defer then rewrites the deferred record's bytes of it).
+// Tiles wholly inside a deferred record (VCFCD_DEFER; the size scan flags
+// them in tile_first) are skipped: k_encode_defer writes those records
+// afterwards (a tile shared with a staged record is written here with
+// whatever the deferred record's staging holds, and k_encode_defer then
+// rewrites the deferred record's bytes of it).
 __global__ __launch_bounds__(256) void k_compact_out(const uint8_t *__restrict__ prims,
                                                      const uint8_t *__restrict__ slots,
                                                      const uint64_t *__restrict__ slot_off,
-                                                     const uint64_t *__restrict__ rec_off,
-                                                     const uint32_t *__restrict__ rec_size, uint64_t n,
+                                                     const uint64_t *__restrict__ rec_off, uint64_t n,
                                                      const uint32_t *__restrict__ tile_first,
                                                      uint8_t *__restrict__ out, uint64_t out_cap, uint32_t pb) {
     const uint32_t l = vw::lane_id();
@@ -1871,9 +1871,6 @@ __global__ __launch_bounds__(256) void k_compact_out(const uint8_t *__restrict__
         // past n start "at infinity"
         const uint64_t ro = r0 + l <= n ? rec_off[r0 + l] : ~0ull;
         const uint64_t so = r0 + l < n ? slot_off[r0 + l] : 0;
-        // deferred rows among them (a tile meeting more than 63 rows holds
-        // only short records, never a deferred one)
-        const uint64_t dfm = vw::ballot(r0 + l < n && (rec_size[r0 + l] & VCFCD_DEFER));
         // rows that start before the tile ends; a tile over more than 63
         // rows (records of < 64 B on average) takes the rows in batches
         uint64_t base = r0;   // row of lane 0's values
@@ -1912,7 +1909,6 @@ __global__ __launch_bounds__(256) void k_compact_out(const uint8_t *__restrict__
             const uint64_t o = o0 + 16u * (l + 64u * k);
             if (o >= lim) continue;
             const uint64_t r = r0 + idx[k];
-            if (idx2[k] < 64 && ((dfm >> idx[k]) & (dfm >> idx2[k]) & 1u)) continue;   // (idx <= idx2)
             const uint64_t x = o - st[k];   // offset in the record
             const uint8_t *prim = prims + (r << pbs);
             const uint8_t *slot = slots + sl[k];
@@ -2188,7 +2184,7 @@ hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t s, hipEvent_t
     const uint64_t tiles = vcfc_record_bound(a.n, a.line_bytes_hint) / CT + 1;
     const uint64_t cblocks = tiles < 8192 ? (tiles + 3) / 4 : 2048;
     hipLaunchKernelGGL(k_compact_out, dim3((unsigned)cblocks), dim3(256), 0, s, a.prim, a.slots, a.slot_off,
-                       a.rec_off, a.rec_size, a.n, a.tile_first, a.out, a.out_cap, a.prim_bytes);
+                       a.rec_off, a.n, a.tile_first, a.out, a.out_cap, a.prim_bytes);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[4], s);
     // the deferred rows' records, straight into out (a resident grid; exits
