@@ -61,6 +61,8 @@ def parse():
                          "file -> file compress (row e: every rank its byte range, outputs held and placed at "
                          "the all-gathered offsets), --ingest-rows rows per rank")
     ap.add_argument("--dist-dir", default="/tmp/vcfc_distfile", help="--mode distfile: where the files go")
+    ap.add_argument("--deferred-records", action="store_true",
+                    help="devfile: vcfc_ctx_set_deferred_records (GT:DP:GQ-like rows written straight to the output)")
     ap.add_argument("--line-index", choices=["hop", "scan"], default="hop",
                     help="--mode devfile: the line index (hop: line ends guessed from the header's sample count "
                          "and checked; scan: every byte)")
@@ -496,6 +498,7 @@ def bench_devfile(args, torch, vcfc, workload):
     if args.dev_chunk:
         ctx.set_ingest_chunk(args.dev_chunk)
     ctx.set_line_index(args.line_index)
+    ctx.set_deferred_records(args.deferred_records)
     for _ in range(args.warmup):
         st, k, _ = ctx.compress_device(d_file.data_ptr(), N, d_out.data_ptr(), cap)
         assert st == 0 and k == want_len, (st, k, want_len)
@@ -516,6 +519,7 @@ def bench_devfile(args, torch, vcfc, workload):
            "config": {"workload": "%s %d samples x %d variants, %.2f GB file in HBM (BASELINE configs[1])"
                                   % (law_name(args.law), S, n, N / 1e9),
                       "file_bytes": N, "output_bytes": want_len,
+                      "deferred_records": args.deferred_records,
                       "chunk": ("%d bytes of whole lines per line index + encode" % args.dev_chunk) if args.dev_chunk
                                else "the whole file (one line index, one encode)",
                       "line_index": ("hop (line ends guessed from the header's sample count, ~1.2 KiB read per "
@@ -523,7 +527,8 @@ def bench_devfile(args, torch, vcfc, workload):
            "roofline": {"kernel": "line index + encoder (whole step)", "bound": "hbm",
                         "achieved": round(alg / (ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                        "traffic": load_pmc("%s/%dx%d/%s" % (law_name(args.law), S, n, args.line_index),
+                        "traffic": load_pmc("%s/%dx%d/%s%s" % (law_name(args.law), S, n, args.line_index,
+                                                                  "/deferred" if args.deferred_records else ""),
                                             "pmc_devfile.json"),
                         "algorithmic_bytes_per_step": alg,
                         "note": "file bytes read once + output written once (the scan index reads the file "

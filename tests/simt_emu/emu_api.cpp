@@ -38,6 +38,7 @@ extern "C" int emu_encode_rows(const uint8_t *buf, const uint64_t *line_off, con
     vcfc_encode_args_workspace(a, ws, L);
     a.line_bytes_hint = getenv("EMU_WIDE_COMPACT") ? (~0ull >> 1) : total;   // (tests force the 64-lane compaction)
     a.err = (uint64_t *)(ws + L.err);
+    a.defer_records = getenv("EMU_DEFER") ? 1u : 0u;   // (tests: deferred records)
     emu::g.switches = 0;
     int st = (int)vcfc_encode_device(a, nullptr);
     *err_word = *a.err;
@@ -188,6 +189,7 @@ extern "C" int emu_compress_device(const uint8_t *in, uint64_t n, uint8_t *out, 
     cfg.hop_index = hop != 0;            // hop: 0 scan, 1 hop (learning when the first lines need it),
     cfg.hop_learn = hop == 2 ? 1 : hop == 3 ? 0 : -1;   // 2 hop learning, 3 hop without learning
     cfg.hop_redo = hop_redo;
+    cfg.defer_records = getenv("EMU_DEFER") != nullptr;
     return vcfc_ing::compress_device(in, n, out, cap, out_len, M, nullptr, cfg, err_line);
 }
 

@@ -206,6 +206,21 @@ def test_hop_index_law2_rows(S, dp_width):
         assert st == st_o == OK and got == want, hop
 
 
+def test_law2_rows_deferred_records(monkeypatch):
+    """compress_device with deferred records on (vcfc_ctx_set_deferred_records):
+    law-2-shaped files whose GT:DP:GQ rows are sized first and written straight
+    into the output after the size scan, with the hop index's '\n' checks
+    on -- the oracle's output."""
+    monkeypatch.setenv("EMU_DEFER", "1")
+    for S, dp in ((700, 2), (300, 0)):
+        rnd = random.Random(S * 7 + dp)
+        vcf = law2_like(rnd, 120, S, dp_width=dp)
+        st_o, want, _ = G.oracle_compress(vcf)
+        for chunk in (1 << 16, 1 << 22):
+            st, got, _ = E.emu_compress_device(vcf, chunk=chunk)
+            assert st == st_o == OK and got == want, (S, dp, chunk)
+
+
 def test_hop_learn_choice():
     """compress_device turns the learned candidates on when the first data
     lines are not all S 3-byte tokens (vcfc_ingest_driver.h

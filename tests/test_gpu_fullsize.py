@@ -217,7 +217,7 @@ def test_range_query_full_batch(torch, vcfc):
         assert olines == b"".join(x + b"\n" for x in host), name
 
 
-@pytest.mark.parametrize("law,line_index", [(1, "hop"), (1, "scan"), (2, "hop")])
+@pytest.mark.parametrize("law,line_index", [(1, "hop"), (1, "scan"), (2, "hop"), (2, "hop-deferred")])
 def test_full_file_compress_device(torch, vcfc, law, line_index):
     """BASELINE configs[2] at config size: the whole-file compress()
     (reference src/compress.cpp:205-257) of a 2504 x 1M VCF file (header +
@@ -246,7 +246,8 @@ def test_full_file_compress_device(torch, vcfc, law, line_index):
     d_out = torch.empty(cap, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize(dev)
     with vcfc.Context(0) as ctx:
-        ctx.set_line_index(line_index)
+        ctx.set_line_index(line_index.split("-")[0])
+        ctx.set_deferred_records(line_index.endswith("-deferred"))   # (GT:DP:GQ rows written after the size scan)
         st, k, el = ctx.compress_device(d_file.data_ptr(), N, d_out.data_ptr(), cap)
     assert (st, el) == (0, -1) and k == H + rec_bytes
     assert bool(torch.equal(d_out[:H], d_file[:H]))

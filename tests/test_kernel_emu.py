@@ -366,8 +366,8 @@ def test_law2_synthetic_rows():
     assert gdg > 0 and E.LAST_RETRIES[0] == 0
 
 
-def test_deferred_records():
-    """Rows whose first genotype chunk is all escapes (GT:DP:GQ, all-1-byte,
+def test_deferred_records(monkeypatch):
+    """With deferred records on (VcfcEncodeArgs::defer_records), rows whose first genotype chunk is all escapes (GT:DP:GQ, all-1-byte,
     a row that turns mixed after its first chunk, another whose later chunk
     sends it to the general path) are deferred: k_encode_var only sizes
     them, the compaction skips their bytes, k_encode_defer writes each record
@@ -396,6 +396,9 @@ def test_deferred_records():
                             [rnd.choice([b"0|0", b"0|1", b"1|1", b"0|2"]) for _ in range(rnd.randint(1, 900))])
         lines.append(ln)
     want = [G.oracle_encode_line(x)[1] for x in lines]
+    st, out, ro, err = run(lines)   # (off by default: nothing deferred, the same records)
+    assert err == (1 << 64) - 1 and E.last_deferred() == 0 and out == b"".join(want)
+    monkeypatch.setenv("EMU_DEFER", "1")
     for lead in (0, 3, 9):
         st, out, ro, err = run(lines, lead)
         assert err == (1 << 64) - 1

@@ -87,6 +87,7 @@ struct vcfc_ctx {
     HostBuf dec_host[vcfc_dec::Buffers::N_HOST];
     uint64_t ingest_chunk = 0;   // 0: default (128 MiB)
     int line_index = VCFC_LINE_INDEX_HOP;
+    int defer_records = 0;       // vcfc_ctx_set_deferred_records
     unsigned trace = 0;          // VCFC_TRACE_* flags
 };
 
@@ -219,6 +220,7 @@ vcfc_ing::Config ingest_config(const vcfc_ctx *c, uint64_t n) {
     const uint64_t want = c->ingest_chunk ? c->ingest_chunk : (128ull << 20);
     cfg.chunk = std::min<uint64_t>(want, std::max<uint64_t>((n + 4095) & ~4095ull, 4096));
     cfg.trace = (c->trace & VCFC_TRACE_INGEST) != 0;
+    cfg.defer_records = c->defer_records != 0;
     return cfg;
 }
 
@@ -281,6 +283,12 @@ int vcfc_ctx_set_ingest_chunk(vcfc_ctx *c, uint64_t chunk_bytes) {
 int vcfc_ctx_set_line_index(vcfc_ctx *c, int mode) {
     if (!c || (mode != VCFC_LINE_INDEX_HOP && mode != VCFC_LINE_INDEX_SCAN)) return VCFC_E_ARG;
     c->line_index = mode;
+    return VCFC_OK;
+}
+
+int vcfc_ctx_set_deferred_records(vcfc_ctx *c, int on) {
+    if (!c || (on != 0 && on != 1)) return VCFC_E_ARG;
+    c->defer_records = on;
     return VCFC_OK;
 }
 
@@ -672,6 +680,7 @@ int vcfc_compress_device(vcfc_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *
     const uint64_t want = c->ingest_chunk ? c->ingest_chunk : cfg.max_chunk;
     cfg.chunk = std::min<uint64_t>(want, std::max<uint64_t>((n + 4095) & ~4095ull, 4096));
     cfg.hop_index = c->line_index == VCFC_LINE_INDEX_HOP;
+    cfg.defer_records = c->defer_records != 0;
     cfg.trace = (c->trace & VCFC_TRACE_DEVICE) != 0;
     return vcfc_ing::compress_device(d_in, n, d_out, out_cap, out_len, M, c->stream, cfg, err_line);
 }

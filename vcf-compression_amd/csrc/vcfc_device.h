@@ -65,6 +65,11 @@ struct VcfcEncodeArgs {
     // VCFCD_E_NEWLINE (k_encode_var scans the rows k_encode_fast hands back;
     // k_encode_fast accepts none)
     uint32_t nl_check = 0;
+    // deferred records (k_encode_var sizes the rows whose first genotype
+    // chunk is all escapes, k_encode_defer writes them to out after the size
+    // scan): off by default -- they pay on GT:DP:GQ-heavy batches only
+    // (DESIGN.md §3 item 6); vcfc_ctx_set_deferred_records
+    uint32_t defer_records = 0;
 };
 
 // Record staging: the first prim_bytes bytes of every record go to a dense

@@ -119,38 +119,43 @@ __device__ __forceinline__ void ring_put(Ring &r, uint32_t pos, uint32_t b) {
 // k_compact: k_compact unchanged at 0.283 ms, k_encode +0.4 %; the staging's
 // 0.68 GB are written amid the 10 GB input stream, so it does not stay
 // resident -- profiles/r03/ab/ab_staging_cache_policy.txt)
+// DYN: the ring's mode is read (the variable-token and deferred paths); the
+// fast and general paths always stage and compile without the checks
+template <bool DYN = false>
 __device__ __forceinline__ void ring_stage(Ring &r, uint32_t f, uint4 v) {
 #ifdef VCFC_DIAG_NOSTORE   // (diagnostic, wrong output: no staging stores)
     if (f == 0x7FFFFFFFu) vw::gstore16_nt(r.prim, 0, v);
     return;
 #endif
-    if (r.mode == RING_SIZE) return;
+    if (DYN && r.mode == RING_SIZE) return;
     if (r.fpos < r.pb) vw::gstore16_nt(r.prim, f, v);
     else vw::gstore16_nt(r.slot, f - r.pb, v);
 }
+template <bool DYN = false>
 __device__ __forceinline__ void ring_burst(Ring &r, uint32_t l) {
     const uint4 v = *reinterpret_cast<const uint4 *>(r.lds + ((r.fpos + 16u * l) & RMASK));
-    ring_stage(r, r.fpos + 16u * l, v);
+    ring_stage<DYN>(r, r.fpos + 16u * l, v);
     r.fpos += BURST;
 }
+template <bool DYN = false>
 __device__ __forceinline__ void ring_flush(Ring &r, bool final) {
     const uint32_t l = vw::lane_id();
     r.wpos = vw::readfirst(r.wpos);
     r.fpos = vw::readfirst(r.fpos);
     vw::wave_sync();
     if (r.wpos - r.fpos >= BURST) {
-        ring_burst(r, l);
+        ring_burst<DYN>(r, l);
         if (r.wpos - r.fpos >= BURST) {
-            ring_burst(r, l);
-            if (r.wpos - r.fpos >= BURST) ring_burst(r, l);
+            ring_burst<DYN>(r, l);
+            if (r.wpos - r.fpos >= BURST) ring_burst<DYN>(r, l);
         }
     }
     if (final && r.wpos > r.fpos) {
         const uint32_t rem = r.wpos - r.fpos;  // < BURST
         if (16u * l < rem) {
             const uint4 v = *reinterpret_cast<const uint4 *>(r.lds + ((r.fpos + 16u * l) & RMASK));
-            if (r.mode != RING_DIRECT || 16u * l + 16u <= rem) {
-                ring_stage(r, r.fpos + 16u * l, v);
+            if (!DYN || r.mode != RING_DIRECT || 16u * l + 16u <= rem) {
+                ring_stage<DYN>(r, r.fpos + 16u * l, v);
             } else {   // the record's last bytes in out: not one byte past them (the next record's)
                 const uint32_t w[4] = {v.x, v.y, v.z, v.w};
                 for (uint32_t i = 0; 16u * l + i < rem; i++)
@@ -178,9 +183,10 @@ __device__ __forceinline__ void ring_unwrap(Ring &r, uint32_t end) {   // end: t
 
 // Finish a record: header words go straight to the staging (lane 0 also
 // wrote its first 16 bytes during the flush, so program order keeps them).
+template <bool DYN = false>
 __device__ void ring_finish(Ring &r, uint32_t req) {
-    ring_flush(r, true);
-    if (vw::lane_id() == 0 && r.mode != RING_SIZE) {
+    ring_flush<DYN>(r, true);
+    if (vw::lane_id() == 0 && (!DYN || r.mode != RING_SIZE)) {
         const uint32_t L = r.wpos - 4;
         const uint32_t h0 = (((L >> 24) & 0xFFu) | 0xC0u) | (((L >> 16) & 0xFFu) << 8) |
                             (((L >> 8) & 0xFFu) << 16) | ((L & 0xFFu) << 24);
@@ -1003,32 +1009,41 @@ __device__ __forceinline__ uint32_t odd2(uint32_t z) { return ((z >> 1) & 1u) | 
 // the next chunk (<= 49 bytes per lane, < 3.2 KiB) fits the 4 KiB ring.  No
 // burst straddles the staging regions (fpos stays a multiple of 512 and a
 // full burst starts on a 1 KiB boundary).
+template <bool DYN>
 __device__ __forceinline__ void ring_half_burst(Ring &r, uint32_t l) {
     if (l < 32) {
         const uint4 v = *reinterpret_cast<const uint4 *>(r.lds + ((r.fpos + 16u * l) & RMASK));
-        ring_stage(r, r.fpos + 16u * l, v);
+        ring_stage<DYN>(r, r.fpos + 16u * l, v);
     }
     r.fpos += BURST / 2;
 }
+template <bool DYN>
 __device__ __forceinline__ void ring_flush_var(Ring &r) {
     const uint32_t l = vw::lane_id();
     r.wpos = vw::readfirst(r.wpos);
     r.fpos = vw::readfirst(r.fpos);
     vw::wave_sync();
-    if ((r.fpos & (BURST / 2)) && r.wpos - r.fpos >= BURST / 2) ring_half_burst(r, l);
+    if ((r.fpos & (BURST / 2)) && r.wpos - r.fpos >= BURST / 2) ring_half_burst<DYN>(r, l);
     if (r.wpos - r.fpos >= BURST) {
-        ring_burst(r, l);
+        ring_burst<DYN>(r, l);
         if (r.wpos - r.fpos >= BURST) {
-            ring_burst(r, l);
-            if (r.wpos - r.fpos >= BURST) ring_burst(r, l);
+            ring_burst<DYN>(r, l);
+            if (r.wpos - r.fpos >= BURST) ring_burst<DYN>(r, l);
         }
     }
-    if (r.wpos - r.fpos >= BURST / 2) ring_half_burst(r, l);
+    if (r.wpos - r.fpos >= BURST / 2) ring_half_burst<DYN>(r, l);
     vw::wave_sync();
 }
 
+// Variable-token path modes: VAR_PLAIN (the default encode: every record
+// staged), VAR_DEFER (k_encode_var with deferred records enabled: a row may
+// switch its ring to RING_SIZE), VAR_DIRECT (k_encode_defer: the ring writes
+// the record into out).  Plain builds none of the mode checks.
+constexpr int VAR_PLAIN = 0, VAR_DEFER = 1, VAR_DIRECT = 2;
+
 // One 2 KiB chunk C of a variable-token row.  false: not this shape (the
 // row takes the general path; nothing of it is kept).
+template <int VM>
 __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState &f, Ring &r) {
     const uint32_t l = vw::lane_id();
     const uint32_t NH = f.T, phi = f.phi;
@@ -1111,12 +1126,12 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
         // 1.1x the input) is deferred: sized here, its record written
         // straight to out by k_encode_defer once the size scan has placed it,
         // instead of staged and copied (deferred records).
-        if (f.defer && C == 0) {
+        if (VM == VAR_DEFER && f.defer && C == 0) {
             f.sizeonly = 1;
             r.mode = RING_SIZE;
         }
 #ifndef VCFC_VAR_SIZE_ONLY   // (diagnostic: the cost of a size-only pass, wrong output)
-        if (f.sizeonly) {
+        if (VM == VAR_DEFER && f.sizeonly) {
         } else if (vw::ballot(vm != 0xFFFFu) == 0) {
             // Interior chunk (every half valid, none the row's last): half h's
             // two bytes sit at lane offset 2h + c_h, c_h = starts in halves
@@ -1164,7 +1179,7 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
         if (tot) f.prs = f.ntok;   // every escape starts a run: the last token's
         f.pcls = CLS_ESC;
         f.carryT = vw::readlane((tb1 >> 15) & 1u, 63);
-        ring_flush_var(r);
+        ring_flush_var<VM != VAR_PLAIN>(r);
         return true;
     }
     // tokens longer than 3 bytes beside 3-byte ones (or after a plain token)
@@ -1301,14 +1316,15 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
     f.pcls = vw::readlane(lcls, src);
     f.carryT = vw::readlane((tb1 >> 15) & 1u, 63);
     f.prs = vw::umax(vw::readlane(incl, 63), f.prs);
-    ring_flush_var(r);
+    ring_flush_var<VM != VAR_PLAIN>(r);
     return true;
 }
 
 // defer_ok: the row may be deferred (*deferred: it was -- sized only, the
 // ring's bytes never left it; k_encode_var)
+template <int VM>
 __device__ bool encode_var(const uint8_t *__restrict__ line, uint32_t len, Ring &r, uint32_t *rec_bytes, bool nlc,
-                           bool *nlhit, bool defer_ok, bool *deferred) {
+                           bool *nlhit, bool *deferred) {
     const uint32_t l = vw::lane_id();
     const uint32_t lead = (uint32_t)(reinterpret_cast<uintptr_t>(line) & 15);
     const uint8_t *A = line - lead;
@@ -1337,11 +1353,11 @@ __device__ bool encode_var(const uint8_t *__restrict__ line, uint32_t len, Ring 
     }
     if (st == 2) return false;
     f.carryT = 1;   // token 0 starts the genotype region
-    ring_flush_var(r);   // < 512 bytes pending before the first chunk
+    ring_flush_var<VM != VAR_PLAIN>(r);   // < 512 bytes pending before the first chunk
     const uint32_t phi = f.phi, NH = f.T;
     const vw::brsrc rsG = vw::make_rsrc(line + f.gt0 - phi, (phi + len - (uint32_t)f.gt0 + 3u) & ~3u);
     const uint32_t ncG = (NH + HPC - 1) / HPC;
-    f.defer = defer_ok && ncG > 1 ? 1u : 0u;
+    f.defer = VM == VAR_DEFER && ncG > 1 ? 1u : 0u;
     const uint32_t lo32 = BPL8 * l;
     // three chunks in flight, a single loop exit (see encode_fast)
     Chunk8v b0 = load_chunk8v(rsG, 0, lo32);
@@ -1351,13 +1367,13 @@ __device__ bool encode_var(const uint8_t *__restrict__ line, uint32_t len, Ring 
     uint32_t C = 0;
     bool ok = true;
     for (;;) {
-        ok = vw::readfirst(gt_var8(b0, C, f, r));
+        ok = vw::readfirst(gt_var8<VM>(b0, C, f, r));
         b0 = load_chunk8v(rsG, C + 3, lo32);
         vw::pin_loads();
-        if (ok && C + 1 < ncG) ok = vw::readfirst(gt_var8(b1, C + 1, f, r));
+        if (ok && C + 1 < ncG) ok = vw::readfirst(gt_var8<VM>(b1, C + 1, f, r));
         b1 = load_chunk8v(rsG, C + 4, lo32);
         vw::pin_loads();
-        if (ok && C + 2 < ncG) ok = vw::readfirst(gt_var8(b2, C + 2, f, r));
+        if (ok && C + 2 < ncG) ok = vw::readfirst(gt_var8<VM>(b2, C + 2, f, r));
         b2 = load_chunk8v(rsG, C + 5, lo32);
         vw::pin_loads();
         C = vw::readfirst(C + 3);
@@ -1379,10 +1395,10 @@ __device__ bool encode_var(const uint8_t *__restrict__ line, uint32_t len, Ring 
         ring_put(r, r.wpos + extra, 0x0Au);
     }
     r.wpos += extra + 1;
-    ring_flush_var(r);   // (< 512 pending: the final partial burst stays inside one staging region)
-    ring_finish(r, (uint32_t)f.gt0);
+    ring_flush_var<VM != VAR_PLAIN>(r);   // (< 512 pending: the final partial burst stays inside one staging region)
+    ring_finish<VM != VAR_PLAIN>(r, (uint32_t)f.gt0);
     *rec_bytes = r.wpos;
-    *deferred = f.sizeonly != 0;
+    *deferred = VM == VAR_DEFER && f.sizeonly != 0;
     return true;
 }
 
@@ -1707,6 +1723,7 @@ constexpr uint32_t VAR_ROWS = 32;
 // (round 2 ran it as a kernel of its own, k_encode_general: one more launch,
 // ~4.5 us on the headline rows, which flag none).  A resident grid striding
 // over rows was 13.6 % slower on law 2 (profiles/r02/ab/ab_gen_persist.txt).
+template <int VM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) void k_encode_var(VcfcEncodeArgs a, uint64_t row_lo, uint64_t row_hi) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[K1_WAVES * RING_STRIDE];
     const uint32_t wave = vw::readfirst(threadIdx.x >> 6);
@@ -1728,7 +1745,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
         uint32_t bytes = 0;
         bool nlhit = false, deferred = false;
         const bool var_ok =
-            encode_var(a.buf + a.line_off[row], a.line_len[row], r, &bytes, a.nl_check, &nlhit, true, &deferred);
+            encode_var<VM>(a.buf + a.line_off[row], a.line_len[row], r, &bytes, a.nl_check, &nlhit, &deferred);
         if (!var_ok && !nlhit && a.nl_check) nlhit = row_has_nl(a.buf + a.line_off[row], a.line_len[row]);
         if (nlhit) {
             if (l == 0) {
@@ -1739,7 +1756,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
         }
         if (var_ok) {
             if (l == 0) a.rec_size[row] = deferred ? (bytes | VCFCD_DEFER) : bytes;
-            if (deferred) dmask |= 1u << (uint32_t)(row - row0);
+            if (VM == VAR_DEFER && deferred) dmask |= 1u << (uint32_t)(row - row0);
             continue;
         }
         // not the variable-token shape: the general path, in this wave
@@ -1751,7 +1768,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
             if (st != VCFCD_OK) atomicMin((unsigned long long *)a.err, (unsigned long long)((row << 8) | st));
         }
     }
-    if (dmask) {   // one append per wave
+    if (VM == VAR_DEFER && dmask) {   // one append per wave
         uint32_t q0 = 0;
         if (l == 0) q0 = atomicAdd(a.defer_count, (uint32_t)__builtin_popcount(dmask));
         q0 = vw::readfirst(q0);
@@ -1786,13 +1803,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
         r.mode = RING_DIRECT;
         uint32_t bytes = 0;
         bool nlhit = false, deferred = false;
-        const bool ok = encode_var(a.buf + a.line_off[row], a.line_len[row], r, &bytes, false, &nlhit, false, &deferred);
+        const bool ok =
+            encode_var<VAR_DIRECT>(a.buf + a.line_off[row], a.line_len[row], r, &bytes, false, &nlhit, &deferred);
         if (l == 0 && (!ok || bytes != size))   // (cannot happen: the same code sized it)
             atomicMin((unsigned long long *)a.err, (unsigned long long)((row << 8) | VCFCD_E_INTERNAL));
     }
 }
 
-constexpr uint32_t DEFER_BLOCKS = 1280;   // 5 waves per SIMD over 256 CUs, 4 waves per block
+constexpr uint32_t DEFER_BLOCKS = 1280;   // 5 waves per SIMD over 256 CUs, 4 waves per block (640: law 2 +1.6 %)
 
 // blocks of k_encode_var to launch for m rows
 static uint64_t var_blocks(uint64_t m, uint32_t rows_per_wave = VAR_ROWS) {
@@ -2173,11 +2191,20 @@ hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t s, hipEvent_t
     hipLaunchKernelGGL(k_encode_fast, dim3((unsigned)((a.n + K1_WAVES - 1) / K1_WAVES)), dim3(64 * K1_WAVES), 0, s, a,
                        (uint64_t)0, a.n);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_encode_var, dim3((unsigned)var_blocks(a.n)), dim3(64 * K1_WAVES), 0, s, a, (uint64_t)0, a.n);
+    if (a.defer_records)
+        hipLaunchKernelGGL(k_encode_var<VAR_DEFER>, dim3((unsigned)var_blocks(a.n)), dim3(64 * K1_WAVES), 0, s, a,
+                           (uint64_t)0, a.n);
+    else
+        hipLaunchKernelGGL(k_encode_var<VAR_PLAIN>, dim3((unsigned)var_blocks(a.n)), dim3(64 * K1_WAVES), 0, s, a,
+                           (uint64_t)0, a.n);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[2], s);
-    hipLaunchKernelGGL((k_scan_lb<2, true>), dim3((unsigned)nt), dim3(SCAN_THREADS), 0, s, a.rec_size, a.n,
-                       tickets + 1, flags_b, a.rec_off, a.tile_first, a.out_cap, a.err);
+    if (a.defer_records)   // (sizes flagged VCFCD_DEFER: masked, and their tiles flagged for the compaction)
+        hipLaunchKernelGGL((k_scan_lb<2, true>), dim3((unsigned)nt), dim3(SCAN_THREADS), 0, s, a.rec_size, a.n,
+                           tickets + 1, flags_b, a.rec_off, a.tile_first, a.out_cap, a.err);
+    else
+        hipLaunchKernelGGL((k_scan_lb<0, true>), dim3((unsigned)nt), dim3(SCAN_THREADS), 0, s, a.rec_size, a.n,
+                           tickets + 1, flags_b, a.rec_off, a.tile_first, a.out_cap, a.err);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[3], s);
     // a grid of 8 waves per SIMD striding over the output tiles (uniform work)
@@ -2189,10 +2216,12 @@ hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t s, hipEvent_t
     if (ev) (void)hipEventRecord(ev[4], s);
     // the deferred rows' records, straight into out (a resident grid; exits
     // at once when k_encode_var deferred none)
-    const uint64_t dblocks = (a.n + K1_WAVES - 1) / K1_WAVES;
-    hipLaunchKernelGGL(k_encode_defer, dim3((unsigned)(dblocks < DEFER_BLOCKS ? dblocks : DEFER_BLOCKS)),
-                       dim3(64 * K1_WAVES), 0, s, a);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (a.defer_records) {
+        const uint64_t dblocks = (a.n + K1_WAVES - 1) / K1_WAVES;
+        hipLaunchKernelGGL(k_encode_defer, dim3((unsigned)(dblocks < DEFER_BLOCKS ? dblocks : DEFER_BLOCKS)),
+                           dim3(64 * K1_WAVES), 0, s, a);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     if (ev) (void)hipEventRecord(ev[5], s);
     return hipSuccess;
 }

@@ -151,6 +151,7 @@ struct Config {
     int hop_learn = -1;              // ... learning other region lengths: -1 = when the first data lines need it
     uint64_t hop_walkers = 0;        // ... walkers (0: the kernel's count; tests)
     bool trace = false;              // stage totals / decisions to stderr (vcfc_ctx_set_trace)
+    bool defer_records = false;      // VcfcEncodeArgs::defer_records (vcfc_ctx_set_deferred_records)
     uint64_t *hop_redo = nullptr;    // compress_device: chunks indexed again after a wrong hop guess
 };
 
@@ -562,6 +563,7 @@ inline int compress_stream(Source &src, const Sink &sink, Memory &M, hipStream_t
             a.out = d_out; a.out_cap = cap; a.rec_off = d_rec_off;
             vcfc_encode_args_workspace(a, ws, W);
             a.err = d_small + 4;
+            a.defer_records = cfg.defer_records ? 1u : 0u;
             oc.rec_off.resize(n_data + 1);
             if (vcfc_encode_device(a, s) != hipSuccess ||
                 hipMemcpyAsync(oc.rec_off.data(), d_rec_off, 8 * (n_data + 1), hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -832,6 +834,7 @@ inline int compress_device(const uint8_t *d_in, uint64_t N, uint8_t *d_out, uint
             vcfc_encode_args_workspace(a, ws, W);
             a.err = d_small + 4;
             a.nl_check = hop != 0;
+            a.defer_records = cfg.defer_records ? 1u : 0u;
             if (vcfc_encode_device(a, s) != hipSuccess || !d2h(hsmall + 4, d_small + 4, 8) || !sync())
                 return ST_E_HIP;
             const uint64_t errw = hsmall[4];

@@ -38,6 +38,7 @@ EXPORTS = [
     "vcfc_sparsify_shard", "vcfc_ctx_set_ingest_chunk", "vcfc_record_hash_device",
     "vcfc_compress_range", "vcfc_compress_device", "vcfc_compress_range_held", "vcfc_held_place",
     "vcfc_held_sizes", "vcfc_held_free", "vcfc_ctx_set_line_index", "vcfc_ctx_set_trace",
+    "vcfc_ctx_set_deferred_records",
 ]
 LINE_INDEX_HOP, LINE_INDEX_SCAN = 0, 1                       # include/vcfc.h VCFC_LINE_INDEX_*
 TRACE_INGEST, TRACE_DEVICE, TRACE_SPARSE_QUERY = 1, 2, 4     # include/vcfc.h VCFC_TRACE_*
@@ -71,6 +72,7 @@ def lib():
     L.vcfc_ctx_set_ingest_chunk.argtypes = [vp, u64]
     L.vcfc_ctx_set_line_index.argtypes = [vp, ctypes.c_int]
     L.vcfc_ctx_set_trace.argtypes = [vp, ctypes.c_uint]
+    L.vcfc_ctx_set_deferred_records.argtypes = [vp, ctypes.c_int]
     L.vcfc_record_hash_device.argtypes = [vp, vp, u64, vp, vp]
     L.vcfc_compress_range.argtypes = [vp, ctypes.c_char_p, u64, u64, ctypes.c_int, u64, ctypes.POINTER(u64),
                                       ctypes.POINTER(i64), ctypes.POINTER(u64)]
@@ -259,6 +261,13 @@ class Context:
         """compress_device's line index: "hop" (default; guessed line ends,
         checked) or "scan" (every byte).  The output does not depend on it."""
         raise_for(lib().vcfc_ctx_set_line_index(self._h, {"hop": LINE_INDEX_HOP, "scan": LINE_INDEX_SCAN}[mode]))
+
+    def set_deferred_records(self, on):
+        """Deferred records for the file / device compress calls (off by
+        default): rows whose first genotype chunk is all escapes are sized
+        first and written straight into the output (include/vcfc.h).  The
+        output does not depend on it."""
+        raise_for(lib().vcfc_ctx_set_deferred_records(self._h, 1 if on else 0))
 
     def set_trace(self, flags):
         """Stage timings of the host drivers to stderr (TRACE_* flags)."""
