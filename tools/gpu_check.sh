@@ -64,9 +64,9 @@ for s in $STEPS; do
     benchdev) timeout -k 10 300 python bench.py --mode devfile > "$O/bench_devfile.json" 2> "$O/bench_devfile.err" || { echo "benchdev failed"; tail -30 "$O/bench_devfile.err"; exit 1; } ; cat "$O/bench_devfile.json" ;;
     pmcdev) # HBM bytes per devfile step (every kernel of one call), law ${LAW:-1} -> pmc_devfile_l<law>.json
          for P in FETCH_SIZE WRITE_SIZE; do
-           (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 180 rocprofv3 --pmc $P --kernel-trace --output-format csv -d "$O/pmcdev_l${LAW:-1}_$P" -o run -- python3 "$R/bench.py" --mode devfile --law ${LAW:-1} --steps 3 --warmup 1 > "$O/pmcdev_l${LAW:-1}_$P.log" 2>&1) || { echo "pmcdev $P failed rc=$?"; tail -30 "$O/pmcdev_l${LAW:-1}_$P.log"; exit 1; }
+           (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 180 rocprofv3 --pmc $P --kernel-trace --output-format csv -d "$O/pmcdev_l${LAW:-1}${DEV_TAG}_$P" -o run -- python3 "$R/bench.py" --mode devfile --law ${LAW:-1} --steps 3 --warmup 1 ${DEV_ARGS} > "$O/pmcdev_l${LAW:-1}${DEV_TAG}_$P.log" 2>&1) || { echo "pmcdev $P failed rc=$?"; tail -30 "$O/pmcdev_l${LAW:-1}${DEV_TAG}_$P.log"; exit 1; }
          done
-         python3 tools/pmc_step_json.py "$O/pmcdev_l${LAW:-1}_FETCH_SIZE" "$O/pmcdev_l${LAW:-1}_WRITE_SIZE" 4 "$(python3 -c "import bench,sys; print(bench.law_name(int(sys.argv[1])))" ${LAW:-1})/2504x1000000/hop" "$O/pmc_devfile_l${LAW:-1}.json" "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, bench.py --mode devfile --law ${LAW:-1} --steps 3 --warmup 1 (tools/gpu_check.sh pmcdev, run $TAG)" > /dev/null || { echo "pmcdev json failed"; exit 1; } ;;
+         python3 tools/pmc_step_json.py "$O/pmcdev_l${LAW:-1}${DEV_TAG}_FETCH_SIZE" "$O/pmcdev_l${LAW:-1}${DEV_TAG}_WRITE_SIZE" 4 "$(python3 -c "import bench,sys; print(bench.law_name(int(sys.argv[1])))" ${LAW:-1})/2504x1000000/hop${DEV_KEY}" "$O/pmc_devfile_l${LAW:-1}${DEV_TAG}.json" "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, bench.py --mode devfile --law ${LAW:-1} --steps 3 --warmup 1 ${DEV_ARGS} (tools/gpu_check.sh pmcdev, run $TAG)" > /dev/null || { echo "pmcdev json failed"; exit 1; } ;;
     benchdev2) timeout -k 10 300 python bench.py --mode devfile --law 2 > "$O/bench_devfile_law2.json" 2> "$O/bench_devfile_law2.err" || { echo "benchdev2 failed"; tail -30 "$O/bench_devfile_law2.err"; exit 1; } ; cat "$O/bench_devfile_law2.json" ;;
     profdev2) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/profdev2" -o run -- python3 "$R/bench.py" --mode devfile --law 2 --steps 5 --warmup 1 > "$O/profdev2.log" 2>&1) || { echo "profdev2 failed rc=$?"; tail -30 "$O/profdev2.log"; exit 1; } ;;
     profdev) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/profdev" -o run -- python3 "$R/bench.py" --mode devfile --steps 5 --warmup 1 > "$O/profdev.log" 2>&1) || { echo "profdev failed rc=$?"; tail -30 "$O/profdev.log"; exit 1; } ;;
