@@ -14,7 +14,7 @@ KERNELS = ("k_encode_fast", "k_encode_var", "k_encode_general", "k_encode_defer"
 def per_kernel(d, counter):
     vals = defaultdict(list)
     for r in csv.DictReader(open(d + "/run_counter_collection.csv")):
-        name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
+        name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].split("<")[0].split()[-1]
         if r["Counter_Name"] == counter and name in KERNELS:
             vals[name].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in vals.items()}
