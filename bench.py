@@ -72,9 +72,9 @@ def parse():
                     help="--mode biobank: encode the rank's whole share of this many rows (5M = configs[3]) "
                          "as back-to-back --rows batches, every record digested and sampled rows re-encoded "
                          "by the CPU checker; a step is the whole shard")
-    ap.add_argument("--sample-rows", type=int, default=1000,
+    ap.add_argument("--sample-rows", type=int, default=1100,
                     help="--mode biobank --rows-total: random rows of every other batch digest-checked against "
-                         "the oracle per pass (besides one whole batch per pass)")
+                         "the oracle per pass (besides one whole batch per pass): 49 x 1100 + 100k > 150k rows per pass")
     ap.add_argument("--sparse-rows", type=int, default=200_000, help="rows of the --mode sparse file")
     ap.add_argument("--ingest-rows", type=int, default=200_000, help="rows of the --mode ingest file")
     ap.add_argument("--query-frac", type=float, default=0.125, help="rows selected by the --mode query range")
