@@ -1958,20 +1958,22 @@ template <int MODE> __device__ __forceinline__ uint64_t scan_xf(uint32_t v) {
     return MODE == 1 ? vcfc_slot_bytes(v) : MODE == 2 ? (uint64_t)(v & ~VCFCD_DEFER) : (uint64_t)v;
 }
 
+// Exclusive block scan of u64 values: each wave scans four 16-bit limbs with
+// DPP add-scans (exact: 64 x 0xFFFF < 2^22), the four wave totals go through
+// LDS (one barrier), instead of an 8-step LDS scan with 16 barriers.
 __device__ uint64_t block_excl_scan_u64(uint64_t v, uint64_t *sh, uint64_t *total) {
-    const uint32_t t = threadIdx.x;
-    sh[t] = v;
+    static_assert(SCAN_THREADS == 256, "four waves per block");
+    const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+    const uint64_t inc = (uint64_t)vw::scan_add(lo & 0xFFFFu) + ((uint64_t)vw::scan_add(lo >> 16) << 16) +
+                         ((uint64_t)vw::scan_add(hi & 0xFFFFu) << 32) + ((uint64_t)vw::scan_add(hi >> 16) << 48);
+    const uint32_t w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63u) == 63u) sh[w] = inc;   // wave totals
     __syncthreads();
-    for (uint32_t o = 1; o < SCAN_THREADS; o <<= 1) {
-        const uint64_t a = t >= o ? sh[t - o] : 0;
-        __syncthreads();
-        sh[t] += a;
-        __syncthreads();
-    }
-    const uint64_t inc = sh[t];
-    *total = sh[SCAN_THREADS - 1];
-    __syncthreads();
-    return inc - v;
+    const uint64_t t0 = sh[0], t1 = sh[1], t2 = sh[2], t3 = sh[3];
+    __syncthreads();   // (sh is reused by the caller's next scan)
+    *total = t0 + t1 + t2 + t3;
+    const uint64_t before = (w > 0 ? t0 : 0) + (w > 1 ? t1 : 0) + (w > 2 ? t2 : 0);
+    return before + inc - v;
 }
 
 template <int MODE>
