@@ -215,3 +215,22 @@ def test_hop_index_wrong_guess_in_dense_segment_on_gpu(ctx):
     st_o, want, _ = G.oracle_compress(data)
     assert st_o == 0
     assert both_paths(ctx, data, 1 << 20) == (0, want, -1)
+
+
+@pytest.mark.parametrize("chunk", [1 << 16, 16 << 20])
+def test_law2_like_deferred_records_on_gpu(ctx, chunk):
+    """Deferred records (vcfc_ctx_set_deferred_records) through all three
+    ingest paths -- buffer, file, device-resident bytes -- on law-2-shaped
+    files (GT:DP:GQ rows of fixed and of random widths beside haploid and
+    missing rows): the oracle's output, and the same bytes as without."""
+    from hop_cases import law2_like
+    for S, dp in ((700, 2), (2504, 0)):
+        vcf = law2_like(random.Random(S + dp), 40, S, dp_width=dp)
+        st_o, want, _ = G.oracle_compress(vcf)
+        assert st_o == 0
+        ctx.set_deferred_records(True)
+        try:
+            st, out, el = both_paths(ctx, vcf, chunk)
+        finally:
+            ctx.set_deferred_records(False)
+        assert (st, el) == (0, -1) and out == want, (S, dp, chunk)
