@@ -1167,7 +1167,7 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
             r.lds[(uint32_t)vw::mad24(es, ro, dmi)] = (uint8_t)0xE1u;
             ro += es;
             r.lds[(uint32_t)vw::mad24(e1, ro, dmi)] = (uint8_t)pay;
-            r.lds[(uint32_t)vw::mad24(e2, ro + 1, dmi)] = (uint8_t)(pay >> 8);
+            r.lds[(uint32_t)(dmi + e2 * (ro + 1))] = (uint8_t)(pay >> 8);   // (a plain multiply: mad24 on ro + 1 costs two shifts to sign-extend it)
             ro += e1 + e2;
         }
         }
@@ -1301,7 +1301,7 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
         r.lds[(uint32_t)vw::mad24(es, ro, dmi)] = (uint8_t)0xE1u;
         ro += es;
         r.lds[(uint32_t)vw::mad24(e1, ro, dmi)] = (uint8_t)pay;
-        r.lds[(uint32_t)vw::mad24(e2, ro + 1, dmi)] = (uint8_t)(pay >> 8);
+        r.lds[(uint32_t)(dmi + e2 * (ro + 1))] = (uint8_t)(pay >> 8);   // (a plain multiply: mad24 on ro + 1 costs two shifts to sign-extend it)
         ro += e1 + e2;
     }
 #endif
