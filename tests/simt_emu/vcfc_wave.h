@@ -74,6 +74,9 @@ inline uint32_t alignbit(uint32_t hi, uint32_t lo, uint32_t s) {
 }
 inline int32_t sext24(int32_t v) { return (int32_t)((uint32_t)v << 8) >> 8; }
 inline int32_t mad24(int32_t a, int32_t b, int32_t x) { return (int32_t)((uint32_t)x + (uint32_t)(sext24(a) * sext24(b))); }
+inline int32_t mulsel(int32_t f, int32_t x) { return (int32_t)((uint32_t)sext24(f) * (uint32_t)sext24(x)); }
+inline uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) { return (a & m) | (b & ~m); }
+inline int32_t sbit(uint32_t x, uint32_t bit) { return ((x >> bit) & 1u) ? -1 : 0; }
 inline void wave_sync() { emu::collective(emu::OP_WAVESYNC, 0, 0, 0); }
 // lowest set bit index; value unspecified for 0 (v_ffbl_b32: callers must not use it)
 inline uint32_t ffbl(uint32_t x) { return (uint32_t)__builtin_ctz(x); }

@@ -1293,10 +1293,10 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
         const int32_t e1 = (int32_t)((EH >> h) & 1u), e2 = (int32_t)((EH2 >> h) & 1u);
         const uint32_t pc = (pcw >> (2 * h)) & 3u;    // predecessor class (plain when hr)
         const uint32_t lb = vw::perm(0x80C0A000u, 0x80C0A000u, pc) | (tk - ptk);
-        ptk = (RS >> h) & 1u ? tk : ptk;
+        ptk = vw::bfi((uint32_t)vw::sbit(RS, h), tk, ptk);   // (a select: bit test, compare, v_cndmask)
         tk += (S >> h) & 1u;
         const uint32_t pay = d[h >> 1] >> (16 * (h & 1));
-        r.lds[(uint32_t)vw::mad24(hr, ro, dmi)] = (uint8_t)lb;
+        r.lds[(uint32_t)(dmi + vw::mulsel(hr, ro))] = (uint8_t)lb;   // (mad24: and, cmp, add, cndmask)
         ro += hl;
         r.lds[(uint32_t)vw::mad24(es, ro, dmi)] = (uint8_t)0xE1u;
         ro += es;

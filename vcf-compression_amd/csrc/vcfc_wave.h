@@ -124,6 +124,23 @@ __device__ __forceinline__ uint32_t alignbit(uint32_t hi, uint32_t lo, uint32_t 
 }
 // x + a*b on the low 24 bits of a and b, signed (v_mad_i32_i24)
 __device__ __forceinline__ int32_t mad24(int32_t a, int32_t b, int32_t x) { return x + __mul24(a, b); }
+// f * x for a flag f in {0, 1} and x in signed 24 bits, as one v_mul_i32_i24
+// (left to itself the compiler turns some of these selects into a bit test,
+// a compare, an add and a v_cndmask)
+// bits of a where m is set, of b elsewhere (v_bfi_b32), m a 0 / ~0 flag:
+// one instruction where the compiler's select takes a compare and a v_cndmask
+__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) {
+    uint32_t r;
+    __asm__("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+    return r;
+}
+// bit `bit` of x sign-extended: 0 or ~0 (v_bfe_i32)
+__device__ __forceinline__ int32_t sbit(uint32_t x, uint32_t bit) { return __builtin_amdgcn_sbfe((int32_t)x, bit, 1); }
+__device__ __forceinline__ int32_t mulsel(int32_t f, int32_t x) {
+    int32_t r;
+    __asm__("v_mul_i32_i24 %0, %1, %2" : "=v"(r) : "v"(f), "v"(x));
+    return r;
+}
 // ((hi:lo) >> 8*s)[31:0]
 __device__ __forceinline__ uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t s) {
     return __builtin_amdgcn_alignbyte(hi, lo, s);
