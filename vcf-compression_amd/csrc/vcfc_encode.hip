@@ -1290,7 +1290,7 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
     for (int h = 0; h < 16; h++) {
         const int32_t hl = (int32_t)((LEAD >> h) & 1u), es = (int32_t)((XE >> h) & 1u);
         const int32_t hr = (int32_t)((LEADr >> h) & 1u);
-        const int32_t e1 = (int32_t)((EH >> h) & 1u), e2 = (int32_t)((EH2 >> h) & 1u);
+        const int32_t e1 = (int32_t)((EH >> h) & 1u);
         const uint32_t pc = (pcw >> (2 * h)) & 3u;    // predecessor class (plain when hr)
         const uint32_t lb = vw::perm(0x80C0A000u, 0x80C0A000u, pc) | (tk - ptk);
         ptk = vw::bfi((uint32_t)vw::sbit(RS, h), tk, ptk);   // (a select: bit test, compare, v_cndmask)
@@ -1301,8 +1301,13 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
         r.lds[(uint32_t)vw::mad24(es, ro, dmi)] = (uint8_t)0xE1u;
         ro += es;
         r.lds[(uint32_t)vw::mad24(e1, ro, dmi)] = (uint8_t)pay;
-        r.lds[(uint32_t)(dmi + e2 * (ro + 1))] = (uint8_t)(pay >> 8);   // (a plain multiply: mad24 on ro + 1 costs two shifts to sign-extend it)
-        ro += e1 + e2;
+        // The second byte goes out with the first: the row's last half has
+        // none (its line end), and the byte written there is the row end's
+        // own slot -- lane 0 writes the pending chunk and '\n' over it after
+        // the last step (cnt does not count it).  One bit extraction fewer
+        // per half than testing EH2.
+        r.lds[(uint32_t)(dmi + e1 * (ro + 1))] = (uint8_t)(pay >> 8);   // (a plain multiply: mad24 on ro + 1 costs two shifts to sign-extend it)
+        ro += 2 * e1;
     }
 #endif
     ring_unwrap(r, base + cnt);
