@@ -1268,15 +1268,13 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
     if (full) r.lds[base] = (uint8_t)(cls_mask_f(cin) | cap);
     ro += full ? 1 : 0;
     const uint32_t EH2 = EH & ~(lastrel >= 0 && lastrel < 16 ? (1u << lastrel) : 0u);
-    // The first run start's lead byte (b1v) is stored on its own: only
-    // payload bytes of the entering escape precede it (no lead or 0xE1 bit
-    // lies below the first run start); the loop's leads are the later starts'.
-    {
-        const uint32_t bl = lrbit - 1u;   // (lrbit 0: no start, lead1 false)
-        const int32_t at = ro + (int32_t)__builtin_popcount(EH & bl) + (int32_t)__builtin_popcount(EH2 & bl);
-        r.lds[(uint32_t)vw::mad24(lead1 ? 1 : 0, at, dmi)] = (uint8_t)b1v;
-    }
-    const uint32_t LEADr = LEAD & ~lrbit;
+    // The first run start's lead byte (b1v) is stored on its own, after the
+    // loop: only payload bytes of the entering escape precede it (no lead or
+    // 0xE1 bit lies below the first run start).  The loop writes every lead
+    // (LEAD), the first one with the wrong length, and this store replaces it
+    // -- one bit test per half fewer than skipping the first start there.
+    const uint32_t bl = lrbit - 1u;   // (lrbit 0: no start, lead1 false)
+    const int32_t at1 = ro + (int32_t)__builtin_popcount(EH & bl) + (int32_t)__builtin_popcount(EH2 & bl);
     // predecessor classes, 2 bits per half (class mask byte by one v_perm)
     auto spread = [](uint32_t x) {   // bit i -> bit 2 i (16 bits)
         x = (x | (x << 8)) & 0x00FF00FFu;
@@ -1285,18 +1283,18 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
         return (x | (x << 1)) & 0x55555555u;
     };
     const uint32_t pcw = spread(q0 & 0xFFFFu) | (spread(q1 & 0xFFFFu) << 1);
-    uint32_t tk = 0, ptk = 0;   // token index (in the lane) of half h; of the run start before it
+    uint32_t rl = 0;   // tokens of the lane from the last run start before half h to h (a lead byte's length)
 #pragma unroll
     for (int h = 0; h < 16; h++) {
         const int32_t hl = (int32_t)((LEAD >> h) & 1u), es = (int32_t)((XE >> h) & 1u);
-        const int32_t hr = (int32_t)((LEADr >> h) & 1u);
         const int32_t e1 = (int32_t)((EH >> h) & 1u);
         const uint32_t pc = (pcw >> (2 * h)) & 3u;    // predecessor class (plain when hr)
-        const uint32_t lb = vw::perm(0x80C0A000u, 0x80C0A000u, pc) | (tk - ptk);
-        ptk = vw::bfi((uint32_t)vw::sbit(RS, h), tk, ptk);   // (a select: bit test, compare, v_cndmask)
-        tk += (S >> h) & 1u;
+        const uint32_t lb = vw::perm(0x80C0A000u, 0x80C0A000u, pc) | rl;
+        // restart at a run start, then count the half's token start (bfi:
+        // the compiler's select takes a bit test, a compare and a v_cndmask)
+        rl = vw::bfi((uint32_t)vw::sbit(RS, h), 0u, rl) + ((S >> h) & 1u);
         const uint32_t pay = d[h >> 1] >> (16 * (h & 1));
-        r.lds[(uint32_t)(dmi + vw::mulsel(hr, ro))] = (uint8_t)lb;   // (mad24: and, cmp, add, cndmask)
+        r.lds[(uint32_t)(dmi + vw::mulsel(hl, ro))] = (uint8_t)lb;   // (mad24: and, cmp, add, cndmask)
         ro += hl;
         r.lds[(uint32_t)vw::mad24(es, ro, dmi)] = (uint8_t)0xE1u;
         ro += es;
@@ -1309,6 +1307,7 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
         r.lds[(uint32_t)(dmi + e1 * (ro + 1))] = (uint8_t)(pay >> 8);   // (a plain multiply: mad24 on ro + 1 costs two shifts to sign-extend it)
         ro += 2 * e1;
     }
+    r.lds[(uint32_t)vw::mad24(lead1 ? 1 : 0, at1, dmi)] = (uint8_t)b1v;   // (program order: after the loop's store there)
 #endif
     ring_unwrap(r, base + cnt);
     r.wpos += vw::readlane(incl2, 63);
