@@ -373,7 +373,9 @@ def bench_query(args, torch, vcfc, workload):
                       "record_bytes": rec_bytes, "selected_record_bytes": sel_rec, "line_bytes": total},
            "roofline": {"kernel": "k_query_match + k_dec_plan + k_dec_write", "bound": "hbm",
                         "achieved": round(alg / (ev_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(alg / (ev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                        "frac": round(alg / (ev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                        "traffic": load_pmc("%s/%dx%d/%s" % (law_name(args.law), S, n, args.query_frac),
+                                            "pmc_k_query.json"),
                         "algorithmic_bytes_per_launch": alg, "avg_launch_ms": round(ev_ms, 4)},
            "output_identical_to_selected_rows": identical}
     if not args.no_cpu_baseline:
@@ -654,12 +656,14 @@ def bench_biobank_shard(args):
     torch.cuda.set_device(dev)
     cdev = torch.device("cpu") if rehearsal else dev
     if world > 1:
-        dist.init_process_group("gloo" if rehearsal else "nccl", **({} if rehearsal else {"device_id": dev}))
+        init_dist(dist, rehearsal, dev)
     rccl = rccl_report(torch, dist, dev, cdev, world, rehearsal)
     R, B, S = args.rows_total, args.rows, args.samples
     lo, hi = R * rank // world, R * (rank + 1) // world
     nb = (hi - lo + B - 1) // B
-    rows = workload.DeviceRows(torch, vcfc, B, S, args.law, seed=5000, device=dev, row0=lo)
+    import dist_compress as D
+    rows = D.setup_all_or_none(rank, lambda v: gather_ints(torch, dist, cdev, world, v),
+                               lambda: workload.DeviceRows(torch, vcfc, B, S, args.law, seed=5000, device=dev, row0=lo))
     ll = rows.line_len_host.astype(np.int64)
     lb_prefix = np.concatenate([[0], np.cumsum(ll)])          # line bytes of the first k rows
     gt_prefix = np.concatenate([[0], np.cumsum(rows.gt_row)])  # GT bytes of the first k rows
@@ -826,7 +830,7 @@ def bench_distfile(args):
     torch.cuda.set_device(dev)
     cdev = torch.device("cpu") if rehearsal else dev
     if world > 1:
-        dist.init_process_group("gloo" if rehearsal else "nccl", **({} if rehearsal else {"device_id": dev}))
+        init_dist(dist, rehearsal, dev)
     rccl = rccl_report(torch, dist, dev, cdev, world, rehearsal)
 
     def allgather(vals):
@@ -842,7 +846,9 @@ def bench_distfile(args):
             dist.barrier()
 
     n, S = args.ingest_rows, args.samples
-    rows = workload.DeviceRows(torch, vcfc, n, S, args.law, seed=2000 + rank, device=dev, row0=rank * n)
+    rows = D.setup_all_or_none(rank, allgather, lambda: workload.DeviceRows(torch, vcfc, n, S, args.law,
+                                                                            seed=2000 + rank, device=dev,
+                                                                            row0=rank * n))
     ws_bytes = vcfc.workspace_size(n, rows.line_bytes)
     cap = vcfc.encode_bound(n, rows.line_bytes)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
@@ -989,6 +995,24 @@ def check_world(args, torch, world, local, rehearsal):
             raise RuntimeError("LOCAL_RANK %d out of range" % local)
 
 
+def init_dist(dist, rehearsal, dev):
+    """One process group per run: RCCL on the rank's device (gloo with host
+    tensors in the one-GPU rehearsal), every collective bounded by
+    dist_compress.dist_timeout() (120 s), so a rank that dies ends the run
+    with an error, not a wait past the driver's limit."""
+    import dist_compress as D
+    D.init_group(dist, "gloo" if rehearsal else "nccl", None if rehearsal else dev)
+
+
+def gather_ints(torch, dist, cdev, world, vals):
+    if world == 1:
+        return [list(vals)]
+    t = torch.tensor(vals, dtype=torch.int64, device=cdev)
+    o = torch.empty(world * len(vals), dtype=torch.int64, device=cdev)
+    dist.all_gather_into_tensor(o, t)
+    return o.view(world, len(vals)).cpu().tolist()
+
+
 def world_devices(torch, dist, dev, cdev, world):
     """PCI (domain, bus, device) of every rank's GPU, all-gathered: the run's
     proof that its N ranks sit on N distinct devices."""
@@ -1045,10 +1069,7 @@ def main():
     torch.cuda.set_device(dev)
     cdev = torch.device("cpu") if rehearsal else dev   # collective tensors
     if world > 1:
-        if rehearsal:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=dev)
+        init_dist(dist, rehearsal, dev)
     rccl = rccl_report(torch, dist, dev, cdev, world, rehearsal)
     S = args.samples
     if args.scaling == "strong":
@@ -1058,13 +1079,21 @@ def main():
     else:
         r0, r1 = rank * args.rows, (rank + 1) * args.rows
     n = r1 - r0
-    rows = workload.DeviceRows(torch, vcfc, n, S, args.law, seed=1000 + rank, device=dev, row0=r0)
-    ws_bytes = vcfc.workspace_size(n, rows.line_bytes)
-    cap = vcfc.encode_bound(n, rows.line_bytes)
-    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
-    out = torch.empty(cap, dtype=torch.uint8, device=dev)
-    rec = torch.empty(n + 1, dtype=torch.int64, device=dev)
-    err = torch.empty(1, dtype=torch.int64, device=dev)
+
+    def setup():
+        rows = workload.DeviceRows(torch, vcfc, n, S, args.law, seed=1000 + rank, device=dev, row0=r0)
+        ws_bytes = vcfc.workspace_size(n, rows.line_bytes)
+        cap = vcfc.encode_bound(n, rows.line_bytes)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+        out = torch.empty(cap, dtype=torch.uint8, device=dev)
+        rec = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        err = torch.empty(1, dtype=torch.int64, device=dev)
+        return rows, ws_bytes, cap, ws, out, rec, err
+    # a rank whose setup fails (out of memory, no device) makes every rank
+    # exit non-zero here, before the first all-gather of shard sizes
+    import dist_compress as D
+    rows, ws_bytes, cap, ws, out, rec, err = D.setup_all_or_none(
+        rank, lambda v: gather_ints(torch, dist, cdev, world, v), setup)
     counts = torch.empty(world, dtype=torch.int64, device=cdev)
     timer = vcfc.StageTimer()
     stream = torch.cuda.current_stream(dev).cuda_stream

@@ -95,3 +95,27 @@ def test_links_the_real_hip_runtime_with_no_undefined_symbols(lib):
             % os.path.join(REPO, "vcf-compression_amd"))
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300).stdout
     assert out.count("libamdhip64") == 1, out
+
+
+DIAG_SWITCHES = ["VCFC_DIAG_NOSTORE", "VCFC_DIAG_NOSTEP", "VCFC_DIAG_CLEAN_SKIP", "VCFC_VAR_SIZE_ONLY",
+                 "VCFC_DIAG_DEC_NOSCAN"]
+
+
+@pytest.mark.parametrize("sw", DIAG_SWITCHES)
+def test_diag_switches_refused(sw, tmp_path):
+    """the kernels' wrong-output diagnostic switches can
+    never reach libvcfc.so.  `make` refuses them without VCFC_DIAG_BUILD and
+    refuses any diagnostic build into build/; the kernel sources refuse them
+    at preprocessing (vcfc_device.h #error) without VCFC_DIAG_BUILD."""
+    mk = os.path.join(REPO, "vcf-compression_amd")
+    r = subprocess.run(["make", "-n", "-C", mk, "EXTRA=-D%s" % sw], capture_output=True, text=True)
+    assert r.returncode != 0 and "wrong output" in r.stderr
+    r = subprocess.run(["make", "-n", "-C", mk, "EXTRA=-D%s -DVCFC_DIAG_BUILD" % sw], capture_output=True, text=True)
+    assert r.returncode != 0 and "may not replace the product library" in r.stderr
+    src = "vcfc_decode.hip" if "DEC" in sw else "vcfc_encode.hip"
+    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-std=c++17", "-I", os.path.join(mk, "csrc"),
+           "-I", os.path.join(REPO, "include"), "-D" + sw, "-E", os.path.join(mk, "csrc", src), "-o", os.devnull]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "diagnostic builds only" in r.stderr
+    r = subprocess.run(cmd[:-4] + ["-DVCFC_DIAG_BUILD"] + cmd[-4:], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-400:]

@@ -418,6 +418,33 @@ def test_deferred_records(monkeypatch):
     assert out2[:int(ro[cut])] == out[:int(ro[cut])]
 
 
+@pytest.mark.parametrize("defer", [False, True])
+def test_escape_rows_ending_on_a_chunk_end(defer, monkeypatch):
+    """rows whose genotype region is a whole number of 2 KiB
+    chunks (1024 / 2048 half-slots: 1024 or 2048 one-byte tokens, 1024
+    GT:DP:GQ tokens = 5 x 1024 halves) end on lane 63's half 15 of their
+    last chunk, the one place where the interior all-escape store path
+    writes a byte into the row end's slot (lane 0's row end rewrites it).
+    Byte-exact with and without deferred records, beside rows one half
+    shorter and longer."""
+    if defer:
+        monkeypatch.setenv("EMU_DEFER", "1")
+    rnd = random.Random(2024)
+    lines = []
+    for S in (1023, 1024, 1025, 2047, 2048, 2049):
+        lines.append(PFX_V + b"\t".join(rnd.choice([b"0", b"1", b"."]) for _ in range(S)))
+    for S in (1023, 1024, 1025):
+        lines.append(PFX_V + b"\t".join(b"%d|%d:%d:%d" % (rnd.randint(0, 1), rnd.randint(0, 1), rnd.randint(10, 99),
+                                                         rnd.randint(10, 99)) for _ in range(S)))
+    want = [G.oracle_encode_line(x)[1] for x in lines]
+    for lead in (0, 5):
+        st, out, ro, err = run(lines, lead)
+        assert err == (1 << 64) - 1
+        for i, w in enumerate(want):
+            assert out[int(ro[i]):int(ro[i + 1])] == w, (lead, i)
+        assert E.LAST_RETRIES[0] == 0
+
+
 @pytest.mark.parametrize("seed", [51, 52, 53, 54])
 def test_sparse_clean_ranges(seed):
     """Sparse clean chunks (the shape a sparse event path would take, round 4;

@@ -190,3 +190,63 @@ def test_held_releases_on_exit_and_gc():
     h = H(99)
     del h
     assert freed == [1234, None, 99]
+
+
+def _failing_worker(rank, world, port, mode):
+    """One rank of a gloo job in which rank 1 fails before the data-path
+    all-gather: `raise` (its setup raises, as an out-of-memory allocation
+    would) or `die` (the process is gone, as after the OOM killer)."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      VCFC_DIST_TIMEOUT_S="15")
+    D.init_group(dist, "gloo")
+
+    def allgather(vals):
+        out = [None] * world
+        dist.all_gather_object(out, vals)
+        return out
+
+    def setup():
+        if rank == 1 and mode == "raise":
+            raise MemoryError("HBM allocation failed")
+        if rank == 1 and mode == "die":
+            os._exit(3)
+        return 7
+    try:
+        assert D.setup_all_or_none(rank, allgather, setup) == 7
+        allgather([1])   # the all-gather of shard sizes
+        code = 0
+    except D.RankFailed:
+        code = 11
+    except Exception:   # the backend's error for a peer that is gone
+        code = 12
+    sys.stdout.flush()
+    os._exit(code)
+
+
+@pytest.mark.parametrize("mode", ["raise", "die"])
+def test_rank_failing_before_the_allgather_ends_every_rank(mode):
+    """a rank that fails before the all-gather must make
+    the others exit non-zero within the collectives' timeout (here 15 s),
+    never hang.  A raising rank reports through the status all-gather (every
+    rank raises RankFailed); a dead rank surfaces as the backend's error."""
+    import time
+    ctx = mp.get_context("spawn")
+    port = 29530 + (mode == "die")
+    t0 = time.time()
+    ps = [ctx.Process(target=_failing_worker, args=(r, 2, port, mode)) for r in range(2)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(90)
+    dt = time.time() - t0
+    alive = [p for p in ps if p.is_alive()]
+    for p in alive:
+        p.kill()
+    assert not alive, "a rank was still waiting after 90 s"
+    # exit codes: 11 = RankFailed, 12 = the backend's error, 3 = the dead rank
+    if mode == "raise":
+        assert [p.exitcode for p in ps] == [11, 11]
+    else:
+        assert ps[1].exitcode == 3 and ps[0].exitcode in (11, 12)
+    assert dt < 75

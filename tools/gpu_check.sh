@@ -26,6 +26,11 @@ for s in $STEPS; do
     benchsp) timeout -k 10 900 python bench.py --mode sparse --steps 5 --warmup 1 > "$O/bench_sparse.json" 2> "$O/bench_sparse.err" || { echo "benchsp failed"; tail -30 "$O/bench_sparse.err"; exit 1; } ; cat "$O/bench_sparse.json" ;;
     benchq) timeout -k 10 600 python bench.py --mode query > "$O/bench_query.json" 2> "$O/bench_query.err" || { echo "benchq failed"; tail -30 "$O/bench_query.err"; exit 1; } ; cat "$O/bench_query.json" ;;
     profq) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/profq" -o run -- python3 "$R/bench.py" --mode query --steps 10 --warmup 2 --no-cpu-baseline > "$O/profq.log" 2>&1) || { echo "profq failed rc=$?"; tail -30 "$O/profq.log"; exit 1; } ;;
+    pmcq) # HBM bytes per query step (k_query_match + selected decode) -> pmc_k_query.json
+         for P in FETCH_SIZE WRITE_SIZE; do
+           (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 180 rocprofv3 --pmc $P --kernel-trace --output-format csv -d "$O/pmcq_$P" -o run -- python3 "$R/bench.py" --mode query --steps 3 --warmup 1 --no-cpu-baseline > "$O/pmcq_$P.log" 2>&1) || { echo "pmcq $P failed rc=$?"; tail -30 "$O/pmcq_$P.log"; exit 1; }
+         done
+         python3 tools/pmc_step_json.py "$O/pmcq_FETCH_SIZE" "$O/pmcq_WRITE_SIZE" 4 "chr22-shaped/2504x1000000/0.125" "$O/pmc_k_query.json" "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, bench.py --mode query --steps 3 --warmup 1 (tools/gpu_check.sh pmcq, run $TAG)" k_query_match "range query step (k_query_match + selected k_dec_plan / scan / k_dec_write)" > /dev/null || { echo "pmcq json failed"; exit 1; } ;;
     qtests) timeout -k 10 900 python -m pytest tests/test_gpu_query.py tests/test_gpu_decode.py -x -q -p no:cacheprovider > "$O/pytest_q.log" 2>&1 || { echo "qtests failed rc=$?"; tail -40 "$O/pytest_q.log"; exit 1; } ;;
     benching) timeout -k 10 900 python bench.py --mode ingest --steps 3 --warmup 1 > "$O/bench_ingest.json" 2> "$O/bench_ingest.err" || { echo "benching failed"; tail -30 "$O/bench_ingest.err"; exit 1; } ; cat "$O/bench_ingest.json" ;;
     itests) timeout -k 10 900 python -m pytest tests/test_gpu_encode.py -x -q -p no:cacheprovider > "$O/pytest_i.log" 2>&1 || { echo "itests failed rc=$?"; tail -40 "$O/pytest_i.log"; exit 1; } ;;

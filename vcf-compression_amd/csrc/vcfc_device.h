@@ -1,6 +1,15 @@
 // vcfc_device.h -- device-side launch interface shared by the C-ABI
 // (vcfc_api.cpp) and the kernels (vcfc_encode.hip).  Plain pointers only.
 #pragma once
+// The kernels' diagnostic switches make libvcfc.so write WRONG .vcfc bytes
+// (they remove steps to price them: profiles/r04/ab/*bisect*).  They exist for
+// the A/B builds under build_ab/ only, which must also define
+// VCFC_DIAG_BUILD; a product build with any of them is refused here (and by
+// the Makefile, tests/test_capi.py::test_diag_switches_refused).
+#if (defined(VCFC_DIAG_NOSTORE) || defined(VCFC_DIAG_NOSTEP) || defined(VCFC_DIAG_CLEAN_SKIP) || \
+     defined(VCFC_VAR_SIZE_ONLY) || defined(VCFC_DIAG_DEC_NOSCAN)) && !defined(VCFC_DIAG_BUILD)
+#error "VCFC_DIAG_* / VCFC_VAR_SIZE_ONLY produce wrong output: diagnostic builds only (define VCFC_DIAG_BUILD)"
+#endif
 #include <stddef.h>
 #include <stdint.h>
 #include <hip/hip_runtime.h>

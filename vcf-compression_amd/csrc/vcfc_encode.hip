@@ -1133,7 +1133,11 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
 #ifndef VCFC_VAR_SIZE_ONLY   // (diagnostic: the cost of a size-only pass, wrong output)
         if (VM == VAR_DEFER && f.sizeonly) {
         } else if (vw::ballot(vm != 0xFFFFu) == 0) {
-            // Interior chunk (every half valid, none the row's last): half h's
+            // Interior chunk (every half valid; the row's last half can only be
+            // lane 63's half 15, when the region is a whole number of chunks:
+            // its second byte, the line end, is then stored at a + 31, the
+            // row end's own slot, which cnt leaves out and lane 0's row-end
+            // ring_put rewrites -- test_escape_rows_ending_on_a_chunk_end): half h's
             // two bytes sit at lane offset 2h + c_h, c_h = starts in halves
             // 0..h, and its 0xE1 (a start) just before them.  Half h's 0xE1
             // store is issued before half h-1's second byte: when h starts
@@ -1852,7 +1856,10 @@ __device__ __forceinline__ uint4 realign16(uint4 lo, uint4 hi, uint32_t sh) {
 // first byte.  (4 KiB tiles: 2 KiB the same, 8 KiB +45 %, ab_compact_tile.txt;
 // the round-1 row-ordered kernel was 12 % slower, ab_compact_out.txt.)
 constexpr uint32_t CTB = 4;                // 16-B blocks per lane per tile
-constexpr uint32_t TILE_DEFERRED = 0x80000000u;   // tile_first flag: the tile lies inside a deferred record
+// tile_first flag: the tile lies inside a deferred record.  It shares the
+// word with the row index, so deferral needs rows < 2^31 (vcfc_encode_device
+// turns it off for larger batches; without it the bound is 2^32 rows)
+constexpr uint32_t TILE_DEFERRED = 0x80000000u;
 constexpr uint32_t CT = 1024 * CTB;        // output bytes per tile
 
 // bytes [0, s) of a, then b's first 16 - s bytes (0 < s < 16)
@@ -2180,6 +2187,13 @@ hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t s, hipEvent_t
     if (a.n == 0) {
         if ((e = hipMemsetAsync(a.err, 0xFF, 8, s)) != hipSuccess) return e;
         return hipMemsetAsync(a.rec_off, 0, 8, s);
+    }
+    // Deferred records need the row index below TILE_DEFERRED (tile_first
+    // carries both): batches of 2^31 rows or more encode without deferral.
+    if (a.defer_records && a.n >= (uint64_t)TILE_DEFERRED) {
+        VcfcEncodeArgs b = a;
+        b.defer_records = 0;
+        return vcfc_encode_device(b, s, ev);
     }
     const uint64_t nt = (a.n + SCAN_TILE - 1) / SCAN_TILE;   // scan tiles
     // lb: tickets (slot scan, size scan), retry counter, slot-scan flags

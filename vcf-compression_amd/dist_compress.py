@@ -23,6 +23,50 @@ import os
 import sys
 
 E_IO = 7   # include/vcfc.h VCFC_E_IO
+# Bound on every collective (init, all-gather, barrier): a rank that dies
+# before a collective must not leave its peers waiting for the backend's
+# default (about 10 minutes for NCCL), past a driver's run limit.
+DIST_TIMEOUT_S = 120
+
+
+class RankFailed(RuntimeError):
+    """Raised on every rank when some rank's setup failed (setup_all_or_none)."""
+
+
+def dist_timeout():
+    """The collectives' timeout (timedelta): VCFC_DIST_TIMEOUT_S, default 120 s."""
+    from datetime import timedelta
+    return timedelta(seconds=float(os.environ.get("VCFC_DIST_TIMEOUT_S", DIST_TIMEOUT_S)))
+
+
+def init_group(dist, backend, device_id=None):
+    """dist.init_process_group with the bounded timeout (and the rank's device
+    for RCCL), so a missing or dead peer ends the job with an error instead of
+    a hang."""
+    kw = {"timeout": dist_timeout()}
+    if device_id is not None:
+        kw["device_id"] = device_id
+    dist.init_process_group(backend, **kw)
+
+
+def setup_all_or_none(rank, allgather, fn):
+    """Run this rank's setup fn() (allocations, input generation) and put its
+    outcome through one all-gather before any data-path collective: if any
+    rank failed, every rank raises RankFailed naming the failed ranks (the
+    failing rank chains its own exception), so all exit non-zero together
+    instead of the healthy ranks waiting in a later collective for a rank
+    that is gone.  Returns fn()'s value."""
+    err, val = None, None
+    try:
+        val = fn()
+    except Exception as e:   # reported through the all-gather
+        err = e
+        print("vcfc rank %d: setup failed: %r" % (rank, e), file=sys.stderr, flush=True)
+    g = allgather([0 if err is None else 1])
+    bad = [r for r, x in enumerate(g) if x[0]]
+    if bad:
+        raise RankFailed("setup failed on rank(s) %s" % bad) from err
+    return val
 # Output a rank holds in host memory until its offset is known (the rest
 # spills to a temporary file beside the output): vcfc.hold_bytes(), this
 # rank's share of the host's MemAvailable, capped by VCFC_HOLD_GB (32 GiB).
@@ -169,7 +213,7 @@ def main():
     dev = torch.device("cuda:%d" % local)
     torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        init_group(dist, "nccl", device_id=dev)
     if rank == 0:
         open(out_path, "wb").close()
     if world > 1:

@@ -72,8 +72,7 @@ def lib():
     L.vcfc_ctx_set_ingest_chunk.argtypes = [vp, u64]
     L.vcfc_ctx_set_line_index.argtypes = [vp, ctypes.c_int]
     L.vcfc_ctx_set_trace.argtypes = [vp, ctypes.c_uint]
-    if hasattr(L, "vcfc_ctx_set_deferred_records"):   # (A/B runs load older builds; tests check the export)
-        L.vcfc_ctx_set_deferred_records.argtypes = [vp, ctypes.c_int]
+    L.vcfc_ctx_set_deferred_records.argtypes = [vp, ctypes.c_int]
     L.vcfc_record_hash_device.argtypes = [vp, vp, u64, vp, vp]
     L.vcfc_compress_range.argtypes = [vp, ctypes.c_char_p, u64, u64, ctypes.c_int, u64, ctypes.POINTER(u64),
                                       ctypes.POINTER(i64), ctypes.POINTER(u64)]
