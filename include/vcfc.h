@@ -72,13 +72,15 @@ int vcfc_ctx_set_line_index(vcfc_ctx *ctx, int mode);
 #define VCFC_TRACE_DEVICE 2u        /* vcfc_compress_device: chunks, sample count, re-indexes */
 #define VCFC_TRACE_SPARSE_QUERY 4u  /* vcfc_sparse_query*: stage totals */
 int vcfc_ctx_set_trace(vcfc_ctx *ctx, unsigned flags);
-/* Deferred records (0 = off, the default; 1 = on) for the context's file
- * and device compress calls: rows of odd-length tokens whose first genotype
- * chunk is all escapes (GT:DP:GQ and the like, records ~1.1x their lines)
- * are only sized by the first pass and encoded straight into the output
- * after the record offsets are known, instead of staged and copied.  Output
- * identical either way; faster on GT:DP:GQ-heavy input (1M such rows
- * -15 %), ~1 % slower on rows of other shapes. */
+/* Deferred records (1 = on, the default since round 5; 0 = off) for the
+ * context's file and device compress calls (vcfc_encode_rows_device and the
+ * one-line / host-batch calls always use them): a row of odd-length tokens
+ * whose first genotype chunk is all escapes (GT:DP:GQ and the like, records
+ * ~1.1x their lines) and that spans more than one 2 KiB chunk is only sized
+ * by the first pass and encoded straight into the output once the record
+ * offsets are known, instead of staged and copied.  The choice is made per
+ * row by the kernel from the row's bytes; a batch without such rows pays
+ * one empty launch.  Output identical either way. */
 int vcfc_ctx_set_deferred_records(vcfc_ctx *ctx, int on);
 
 /* ---- one line: replaces compress_data_line (src/compress.hpp:20-23) --------
@@ -119,6 +121,12 @@ int vcfc_encode_rows_device(const uint8_t *d_buf, const uint64_t *d_line_off,
                             const uint32_t *d_line_len, uint64_t n, uint64_t total_line_bytes,
                             uint8_t *d_out, uint64_t out_cap, uint64_t *d_rec_off,
                             void *d_ws, uint64_t ws_bytes, uint64_t *d_err, void *stream);
+
+/* Rows the last vcfc_encode_rows_device call on workspace d_ws (sized for
+ * n, total_line_bytes) deferred (see vcfc_ctx_set_deferred_records); waits
+ * for `stream`. */
+int vcfc_encode_deferred_rows(const void *d_ws, uint64_t n_rows, uint64_t total_line_bytes, void *stream,
+                              uint64_t *rows);
 
 /* Per-stage timing of vcfc_encode_rows_device (HIP events on the same
  * stream).  vcfc_timer_read synchronises and returns the per-stage totals in

@@ -21,6 +21,11 @@ extern "C" unsigned long long emu_hop_read(int reset) {
 }
 
 static uint32_t g_last_deferred = 0;
+// deferred records: EMU_DEFER=0 / 1 forces them off / on, else the product default
+static uint32_t emu_defer() {
+    const char *e = getenv("EMU_DEFER");
+    return e ? (atoi(e) != 0 ? 1u : 0u) : (uint32_t)VCFC_DEFER_DEFAULT;
+}
 // rows the last emu_encode_rows call deferred (VCFCD_DEFER: written by k_encode_defer)
 extern "C" uint32_t emu_last_deferred() { return g_last_deferred; }
 
@@ -38,7 +43,7 @@ extern "C" int emu_encode_rows(const uint8_t *buf, const uint64_t *line_off, con
     vcfc_encode_args_workspace(a, ws, L);
     a.line_bytes_hint = getenv("EMU_WIDE_COMPACT") ? (~0ull >> 1) : total;   // (tests force the 64-lane compaction)
     a.err = (uint64_t *)(ws + L.err);
-    a.defer_records = getenv("EMU_DEFER") ? 1u : 0u;   // (tests: deferred records)
+    a.defer_records = emu_defer();   // (tests: deferred records; the product default unless EMU_DEFER is set)
     emu::g.switches = 0;
     int st = (int)vcfc_encode_device(a, nullptr);
     *err_word = *a.err;
@@ -189,7 +194,7 @@ extern "C" int emu_compress_device(const uint8_t *in, uint64_t n, uint8_t *out, 
     cfg.hop_index = hop != 0;            // hop: 0 scan, 1 hop (learning when the first lines need it),
     cfg.hop_learn = hop == 2 ? 1 : hop == 3 ? 0 : -1;   // 2 hop learning, 3 hop without learning
     cfg.hop_redo = hop_redo;
-    cfg.defer_records = getenv("EMU_DEFER") != nullptr;
+    cfg.defer_records = emu_defer() != 0;
     return vcfc_ing::compress_device(in, n, out, cap, out_len, M, nullptr, cfg, err_line);
 }
 

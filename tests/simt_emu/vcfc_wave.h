@@ -74,7 +74,16 @@ inline uint32_t alignbit(uint32_t hi, uint32_t lo, uint32_t s) {
 }
 inline int32_t sext24(int32_t v) { return (int32_t)((uint32_t)v << 8) >> 8; }
 inline int32_t mad24(int32_t a, int32_t b, int32_t x) { return (int32_t)((uint32_t)x + (uint32_t)(sext24(a) * sext24(b))); }
+inline uint32_t umul24(uint32_t a, uint32_t b) { return (uint32_t)((uint64_t)(a & 0xFFFFFFu) * (b & 0xFFFFFFu)); }
 inline int32_t mulsel(int32_t f, int32_t x) { return (int32_t)((uint32_t)sext24(f) * (uint32_t)sext24(x)); }
+inline uint32_t dot4u(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r = c;
+    for (int i = 0; i < 4; i++) r += ((a >> (8 * i)) & 0xFFu) * ((b >> (8 * i)) & 0xFFu);
+    return r;
+}
+struct ldsp { uint8_t *a; };
+inline ldsp lds_sel(uint8_t *lds, int32_t f, int32_t x, int32_t dm) { return ldsp{lds + mad24(f, x, dm)}; }
+template <int OFF, bool HI> inline void lds_st8(ldsp p, uint32_t v) { p.a[OFF] = (uint8_t)(HI ? (v >> 16) : v); }
 inline uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) { return (a & m) | (b & ~m); }
 inline int32_t sbit(uint32_t x, uint32_t bit) { return ((x >> bit) & 1u) ? -1 : 0; }
 inline void wave_sync() { emu::collective(emu::OP_WAVESYNC, 0, 0, 0); }

@@ -376,8 +376,8 @@ def test_deferred_records(monkeypatch):
     several alignments, and with out_cap cutting a deferred record."""
     rnd = random.Random(123)
     lines, expect_defer = [], 0
-    for i in range(40):
-        kind = i % 5
+    for i in range(56):
+        kind = i % 7
         if kind == 0:     # GT:DP:GQ, 300..1200 samples (> one 2 KiB chunk)
             S = rnd.choice([300, 301, 777, 1200])
             ln = PFX_V + b"\t".join(b"%d|%d:%d:%d" % (rnd.randint(0, 1), rnd.randint(0, 1), rnd.randint(10, 99),
@@ -391,13 +391,27 @@ def test_deferred_records(monkeypatch):
             ln = PFX_V + b"\t".join([b"0"] * 1500 + [b"10"] + [b"1"] * 3)
         elif kind == 3:   # one chunk only: staged
             ln = PFX_V + b"\t".join(rnd.choice([b"0", b"0|1:5:9"]) for _ in range(rnd.randint(1, 150)))
-        else:             # 3-byte tokens: the fast kernel
+        elif kind == 4:   # 3-byte tokens: the fast kernel
             ln = b"\t".join([b"1", b"%d" % i, b"a", b"b", b"c", b"d", b"e", b"f", b"GT"] +
                             [rnd.choice([b"0|0", b"0|1", b"1|1", b"0|2"]) for _ in range(rnd.randint(1, 900))])
+        elif kind == 5:   # every token an unphased / missing escape over > 512 tokens: k_encode_fast hands
+            # the row on after its first chunk, k_encode_var defers it (mixed 0|1 tokens later on)
+            S = rnd.choice([513, 700, 1100])
+            toks = [rnd.choice([b"0/0", b"0/1", b"1/1", b"./."]) for _ in range(S)]
+            if i % 2:
+                toks[600:] = [rnd.choice([b"0|0", b"0|1"]) for _ in toks[600:]]
+            ln = PFX_V + b"\t".join(toks)
+            expect_defer += 1
+        else:             # the same within one chunk (<= 512 tokens): staged by the fast kernel
+            ln = PFX_V + b"\t".join(rnd.choice([b"0/0", b"0/1", b"./."]) for _ in range(rnd.randint(1, 512)))
         lines.append(ln)
     want = [G.oracle_encode_line(x)[1] for x in lines]
-    st, out, ro, err = run(lines)   # (off by default: nothing deferred, the same records)
+    monkeypatch.setenv("EMU_DEFER", "0")
+    st, out, ro, err = run(lines)   # (off: nothing deferred, the same records)
     assert err == (1 << 64) - 1 and E.last_deferred() == 0 and out == b"".join(want)
+    monkeypatch.delenv("EMU_DEFER")   # (the default since round 5: on)
+    st, out, ro, err = run(lines)
+    assert err == (1 << 64) - 1 and E.last_deferred() == expect_defer and out == b"".join(want)
     monkeypatch.setenv("EMU_DEFER", "1")
     for lead in (0, 3, 9):
         st, out, ro, err = run(lines, lead)
@@ -411,14 +425,14 @@ def test_deferred_records(monkeypatch):
         offs.append(len(buf))
         lens.append(len(ln))
         buf += ln + b"\n"
-    cut = 10   # a GT:DP:GQ row: out_cap ends inside its record
+    cut = 14   # a GT:DP:GQ row: out_cap ends inside its record
     cap = int(ro[cut]) + 100
     st2, out2, ro2, err2 = E.emu_encode(bytes(buf), np.array(offs, np.uint64), np.array(lens, np.uint32), cap=cap)
     assert err2 == (cut << 8) | 4
     assert out2[:int(ro[cut])] == out[:int(ro[cut])]
 
 
-@pytest.mark.parametrize("defer", [False, True])
+@pytest.mark.parametrize("defer", ["0", "1"])
 def test_escape_rows_ending_on_a_chunk_end(defer, monkeypatch):
     """rows whose genotype region is a whole number of 2 KiB
     chunks (1024 / 2048 half-slots: 1024 or 2048 one-byte tokens, 1024
@@ -427,8 +441,7 @@ def test_escape_rows_ending_on_a_chunk_end(defer, monkeypatch):
     writes a byte into the row end's slot (lane 0's row end rewrites it).
     Byte-exact with and without deferred records, beside rows one half
     shorter and longer."""
-    if defer:
-        monkeypatch.setenv("EMU_DEFER", "1")
+    monkeypatch.setenv("EMU_DEFER", defer)
     rnd = random.Random(2024)
     lines = []
     for S in (1023, 1024, 1025, 2047, 2048, 2049):

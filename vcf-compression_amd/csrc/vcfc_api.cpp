@@ -87,7 +87,7 @@ struct vcfc_ctx {
     HostBuf dec_host[vcfc_dec::Buffers::N_HOST];
     uint64_t ingest_chunk = 0;   // 0: default (128 MiB)
     int line_index = VCFC_LINE_INDEX_HOP;
-    int defer_records = 0;       // vcfc_ctx_set_deferred_records
+    int defer_records = VCFC_DEFER_DEFAULT;   // vcfc_ctx_set_deferred_records (on by default)
     unsigned trace = 0;          // VCFC_TRACE_* flags
 };
 
@@ -334,6 +334,22 @@ int vcfc_encode_rows_device(const uint8_t *d_buf, const uint64_t *d_line_off, co
                             uint64_t *d_rec_off, void *d_ws, uint64_t ws_bytes, uint64_t *d_err, void *stream) {
     return encode_rows_device_impl(d_buf, d_line_off, d_line_len, n, total_line_bytes, d_out, out_cap, d_rec_off,
                                    d_ws, ws_bytes, d_err, stream, nullptr);
+}
+
+int vcfc_encode_deferred_rows(const void *d_ws, uint64_t n, uint64_t total_line_bytes, void *stream,
+                              uint64_t *rows) {
+    if (!rows || (n && !d_ws)) return VCFC_E_ARG;
+    *rows = 0;
+    if (n == 0) return VCFC_OK;
+    const VcfcWorkspaceLayout L = vcfc_encode_workspace_layout(n, total_line_bytes);
+    uint32_t v = 0;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (hipMemcpyAsync(&v, static_cast<const uint8_t *>(d_ws) + vcfc_defer_count_offset(L), 4, hipMemcpyDeviceToHost,
+                       s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return VCFC_E_HIP;
+    *rows = v;
+    return VCFC_OK;
 }
 
 int vcfc_timer_create(vcfc_timer **t) {

@@ -54,9 +54,11 @@ __device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a < 
 __device__ __forceinline__ uint32_t umin32(uint32_t a, uint32_t b) { return a < b ? a : b; }
 
 // bit i set <=> byte i of w is zero (exact)
+// (the four flags gathered by one v_dot4_u32_u8, round 5: 6 VALU fewer than
+// four shifts, masks and ors)
 __device__ __forceinline__ uint32_t zero_bytes4(uint32_t w) {
     const uint32_t t = ~(((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w | 0x7F7F7F7Fu);
-    return ((t >> 7) & 1u) | ((t >> 14) & 2u) | ((t >> 21) & 4u) | ((t >> 28) & 8u);
+    return vw::dot4u(t >> 7, 0x08040201u, 0u);
 }
 
 __device__ __forceinline__ uint32_t be30(const uint8_t *h) {
@@ -162,7 +164,7 @@ struct ItemLane {
 
 // bit j <- bit 8j + 7 of x (one flag per byte, as 0x80 in that byte)
 __device__ __forceinline__ uint32_t msb4(uint32_t x) {
-    return ((x >> 7) & 1u) | ((x >> 14) & 2u) | ((x >> 21) & 4u) | ((x >> 28) & 8u);
+    return vw::dot4u((x >> 7) & 0x01010101u, 0x08040201u, 0u);
 }
 // bits [lo, hi) of a 4-bit mask (0 <= lo, hi <= 4)
 __device__ __forceinline__ uint32_t bits4(uint32_t lo, uint32_t hi) {
@@ -199,16 +201,17 @@ __device__ __forceinline__ ItemLane scan_window(uint32_t v4, uint32_t b0, uint32
     const uint32_t bad = (P & ~T & (msb4(hb) | tabM | lfM)) | (T & ~tabM) |
                          (r.start & ((escM & ~e1M) | (e1M & overM) | zero_bytes4(c8)));
     st.bad = st.bad || vw::ballot((bad & valid) != 0) != 0;
-    const uint32_t s8 = (r.start & 1u) | ((r.start & 2u) << 7) | ((r.start & 4u) << 14) | ((r.start & 8u) << 21);
-    const uint32_t cs = c8 & (s8 * 0xFFu);          // counts of the starts
-    const uint32_t q0 = cs & 0xFFu, q1 = (cs >> 8) & 0xFFu, q2 = (cs >> 16) & 0xFFu, q3 = cs >> 24;
-    const uint32_t sum = q0 + q1 + q2 + q3;
+    // start bits -> 0xFF bytes (bit j -> bit 8j by one 24-bit multiply), the
+    // starts' counts, their sum and prefix sums by v_dot4_u32_u8
+    const uint32_t s8 = vw::umul24(r.start, 0x00204081u) & 0x01010101u;
+    const uint32_t cs = c8 & ((s8 << 8) - s8);      // counts of the starts
+    const uint32_t sum = vw::dot4u(cs, 0x01010101u, 0u);
     const uint32_t inc = vw::scan_add(sum);
     const uint32_t base = st.got + (inc - sum);
     r.gb[0] = base;
-    r.gb[1] = base + q0;
-    r.gb[2] = base + q0 + q1;
-    r.gb[3] = base + q0 + q1 + q2;
+    r.gb[1] = vw::dot4u(cs, 0x00000001u, base);
+    r.gb[2] = vw::dot4u(cs, 0x00000101u, base);
+    r.gb[3] = vw::dot4u(cs, 0x00010101u, base);
     st.got += vw::readlane(inc, 63);
     return r;
 }

@@ -11,6 +11,10 @@
 #error "VCFC_DIAG_* / VCFC_VAR_SIZE_ONLY produce wrong output: diagnostic builds only (define VCFC_DIAG_BUILD)"
 #endif
 #include <stddef.h>
+// deferred records on (1) or off (0) by default (A/B builds set 0)
+#ifndef VCFC_DEFER_DEFAULT
+#define VCFC_DEFER_DEFAULT 1
+#endif
 #include <stdint.h>
 #include <hip/hip_runtime.h>
 
@@ -75,10 +79,12 @@ struct VcfcEncodeArgs {
     // k_encode_fast accepts none)
     uint32_t nl_check = 0;
     // deferred records (k_encode_var sizes the rows whose first genotype
-    // chunk is all escapes, k_encode_defer writes them to out after the size
-    // scan): off by default -- they pay on GT:DP:GQ-heavy batches only
-    // (DESIGN.md §3 item 6); vcfc_ctx_set_deferred_records
-    uint32_t defer_records = 0;
+    // chunk is all escapes and that span more than one chunk, k_encode_defer
+    // writes them to out after the size scan): on by
+    // default since round 5 -- the choice is made per row by the kernel from
+    // the row's own bytes, and a batch without such rows pays one empty
+    // launch; vcfc_ctx_set_deferred_records(ctx, 0) turns it off
+    uint32_t defer_records = VCFC_DEFER_DEFAULT;
 };
 
 // Record staging: the first prim_bytes bytes of every record go to a dense
@@ -131,6 +137,10 @@ inline void vcfc_encode_args_workspace(VcfcEncodeArgs &a, uint8_t *ws, const Vcf
     a.slots_cap = L.dbg - L.slots;
     a.dbg = L.dbg < L.total ? reinterpret_cast<uint64_t *>(ws + L.dbg) : nullptr;
 }
+
+// Rows the last encode on this workspace deferred (the device word behind
+// VcfcEncodeArgs::defer_count; read by the caller after the stream is done).
+inline uint64_t vcfc_defer_count_offset(const VcfcWorkspaceLayout &L) { return L.defer_count; }
 
 // Enqueue the whole encode on `stream` (no host synchronisation, capturable).
 // If `ev` is non-null, ev[0..5] are recorded before the slot scan, after it,

@@ -73,7 +73,9 @@ __device__ __forceinline__ uint32_t cls_of(uint32_t k) {
 __device__ __forceinline__ uint32_t zero_bytes4(uint32_t w) {
     uint32_t t = ((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w | 0x7F7F7F7Fu;
     t = ~t;  // 0x80 in every zero byte
-    return ((t >> 7) * 0x00204081u >> 21) & 0xFu;
+    // gathered by one v_dot4_u32_u8 (a 32-bit multiply here is v_mul_lo_u32,
+    // which issues at a quarter of the rate)
+    return vw::dot4u(t >> 7, 0x08040201u, 0u);
 }
 __device__ __forceinline__ uint32_t tab_mask16(uint4 v) {
     return zero_bytes4(v.x ^ 0x09090909u) | (zero_bytes4(v.y ^ 0x09090909u) << 4) |
@@ -272,6 +274,8 @@ struct FastState {
     uint32_t T, phi;    // token count, gt0's byte phase mod 4
     uint32_t pcls, prs; // class / run start(+1) of the previous token
     uint32_t esc;       // the last genotype chunk held an escape: test the escape shape first
+    uint32_t hand;      // deferred records on and more than one genotype chunk: an all-escape chunk 0 hands the row on
+    uint32_t handoff;   // ... and it did (encode_fast returns false: k_encode_var takes the row and defers it)
 };
 
 // Prefix phase for chunk c: 0 = no sample yet, 1 = first sample starts in
@@ -836,6 +840,19 @@ __device__ __forceinline__ bool gt_step8(const Chunk8 &cur, uint32_t C, FastStat
             return true;
         }
         if (vw::ballot(shape3<false>(d, t0, T)) == 0) {
+            if (f.hand && C == 0) {
+                // every token of chunk 0 an escape (unphased "0/1", "./."):
+                // records ~1.25x the line, so with deferred records on the
+                // row goes to k_encode_var, which sizes it and has it
+                // written straight to out instead of staged and copied
+                bool plain = false;
+#pragma unroll
+                for (int j = 0; j < (int)TPL8; j++) plain |= ((d[j] ^ Z) & 0xFFFEFFFEu) == 0;
+                if (vw::ballot(plain) == 0) {
+                    f.handoff = 1;
+                    return false;
+                }
+            }
             esc8<false>(d, t0, tf, f, r);
             return true;
         }
@@ -860,7 +877,7 @@ __device__ __forceinline__ bool gt_step8(const Chunk8 &cur, uint32_t C, FastStat
     return false;   // tokens of another length or empty fields: the caller runs gt_general on this chunk
 }
 
-__device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring &r, uint32_t *rec_bytes) {
+__device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring &r, uint32_t *rec_bytes, bool defer) {
     const uint32_t l = vw::lane_id();
     const uint32_t lead = (uint32_t)(reinterpret_cast<uintptr_t>(line) & 15);
     const uint8_t *A = line - lead;
@@ -870,6 +887,7 @@ __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring
     const uint32_t lo16 = BPL * l;
     FastState f;
     f.nf = 0; f.carryT = 1; f.gt0 = -1; f.T = 0; f.phi = 0; f.pcls = CLS_NONE; f.prs = 0; f.esc = 0;
+    f.hand = 0; f.handoff = 0;
     r.wpos = 8;
     r.fpos = 0;
 
@@ -897,6 +915,7 @@ __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring
     const vw::brsrc rsG = vw::make_rsrc(line + f.gt0 - phi, (phi + len - (uint32_t)f.gt0 + 3u) & ~3u);
     const uint32_t ncG = (T + SLOTS8 - 1) / SLOTS8;
     const uint32_t lo32 = BPL8 * l;
+    f.hand = defer && ncG > 1 ? 1u : 0u;
     uint32_t C0 = 0;
     // three chunks in flight per wave (two: 8 waves/SIMD but +3 % on the
     // headline law, ab_depth_occupancy.txt; four: 5 waves/SIMD, slower,
@@ -922,6 +941,7 @@ __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring
             if (!ok || C >= ncG) break;
         }
         if (ok) break;
+        if (f.handoff) return false;   // (an all-escape chunk 0: k_encode_var's row)
         // chunk `gen`: the general step over its two 1 KiB halves
         for (uint32_t h = 0; h < 2; h++) {
             const Chunk hc = look_ahead(load_chunk(rsG, 2 * gen + h, lo16));
@@ -964,17 +984,17 @@ __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring
 //     so a half's predecessor class is the class of the half before it;
 //   - run starts, the entering run (wave max-scan) and its offset mod cap
 //     follow esc8's rules over token indices (a wave add-scan of starts);
-//   - emission per half: [lead][0xE1 at an escape start][both bytes of an
-//     escape half].  An escape's last half carries its trailing TAB, so a
-//     start after an escape emits no lead byte (the reference's '\t' after
+//   - emission (round 5): the run entering a lane is closed by the lead byte
+//     of the lane's first run start; every run that starts and ends inside
+//     the lane emits its pending byte at its last half (END).  Per half:
+//     [pending byte at an END half | 0xE1 at an escape start][both bytes of
+//     an escape half].  An escape's last half carries its trailing TAB, so a
+//     start after an escape needs no lead byte (the reference's '\t' after
 //     an escape, compress.cpp:181-184, is that TAB); the row's last half
-//     drops its second byte (the line end).
-// Bytes leave as one unaligned dword store per half, issued from the lane's
-// last half to its first with each dword holding the bytes that follow it,
-// so only a lane's last emitting half writes past its end (<= 3 bytes, into
-// the next lanes' first bytes); a final store rewrites every lane's first
-// min(count, 4) bytes.  Rows of other shapes stay flagged for
-// the general path.
+//     drops its second byte (the line end).  The pending byte's value runs
+//     along the halves in one register (class mask at the run start, + 1/2
+//     per half), and every byte is one ds_write_b8 at dummy + f * offset.
+// Rows of other shapes stay flagged for the general path.
 constexpr uint32_t HPC = 1024;   // half-slots per 2 KiB chunk
 
 struct VarState : FastState {
@@ -1105,12 +1125,15 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
     const uint32_t L3 = S & ~tb1 & (tb1 >> 1);                 // 3-byte tokens (plain or not)
     const uint32_t nt = (uint32_t)__builtin_popcount(S);
     const uint32_t tinc = vw::scan_add(nt);
-    if ((f.pcls == CLS_ESC || f.pcls == CLS_NONE) && vw::ballot(L3 != 0) == 0) {
-        // Escape chunk: no 3-byte token starts here and the token entering
-        // the chunk is an escape (or this is token 0: no lead byte), so
-        // every half belongs to an escape (1 byte, or 5 and more: GT:DP:GQ):
-        // each emits its bytes, a start 0xE1 first -- the input with 0xE1
-        // before every token.
+    // Escape chunk: the token entering the chunk is an escape (or this is
+    // token 0: no lead byte) and every token of the chunk is an escape -- no
+    // 3-byte token starts here (1-byte tokens, 5 and more: GT:DP:GQ), or,
+    // found after the classification below, none of its 3-byte tokens is
+    // plain (unphased "0/1", "./.": the rows k_encode_fast hands on with
+    // deferred records on).  Every half then belongs to an escape: each emits
+    // its bytes, a start 0xE1 first -- the input with 0xE1 before every token.
+    const bool pesc = f.pcls == CLS_ESC || f.pcls == CLS_NONE;
+    auto esc_chunk = [&]() {
         const bool lastin = lastrel >= 0 && lastrel < 16;
         const uint32_t cnt = nt + 2u * (uint32_t)__builtin_popcount(vm) - (lastin ? 1u : 0u);
         const uint32_t incl2 = vw::scan_add(cnt);
@@ -1184,17 +1207,19 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
         f.pcls = CLS_ESC;
         f.carryT = vw::readlane((tb1 >> 15) & 1u, 63);
         ring_flush_var<VM != VAR_PLAIN>(r);
+    };
+    if (pesc && vw::ballot(L3 != 0) == 0) {
+        esc_chunk();
         return true;
     }
-    // tokens longer than 3 bytes beside 3-byte ones (or after a plain token)
-    // are left to the general path
-    if (vw::ballot((S & ~tb1 & ~(tb1 >> 1)) != 0)) return false;
     // plain 3-byte candidates: bytes "a|b" from the half, a, b in {0,1}; a, b bits
     // (SWAR, four halves a word: A = first bytes, P = second bytes, B = the
     // byte after each half, i.e. the next half's first; bit 0 of the bytes
     // of A / B gathered by one multiply)
     uint32_t p3 = 0, am = 0, bm = 0;
-    auto bits0 = [](uint32_t x) { return (((x & 0x01010101u) * 0x01020408u) >> 24) & 0xFu; };
+    // bit 0 of each byte gathered by one v_dot4_u32_u8 (not a v_mul_lo_u32)
+    auto bits0 = [](uint32_t x) { return vw::dot4u(x & 0x01010101u, 0x08040201u, 0u); };
+    uint32_t Y[4];   // per half of word k (byte i: half 4k + i): 2a + b, the class index of a plain start
     uint32_t An = vw::perm(d[1], d[0], 0x06040200u);
 #pragma unroll
     for (int k = 0; k < 4; k++) {
@@ -1206,8 +1231,16 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
         p3 |= zero_bytes4(y) << (4 * k);
         am |= bits0(A) << (4 * k);
         bm |= bits0(B) << (4 * k);
+        Y[k] = ((A & 0x01010101u) << 1) | (B & 0x01010101u);
     }
     const uint32_t PL = S & p3 & ~tb1 & (tb1 >> 1);           // plain: exactly 3 bytes "a|b"
+    if (pesc && vw::ballot(PL != 0) == 0) {   // no plain token: the escape chunk (above)
+        esc_chunk();
+        return true;
+    }
+    // tokens longer than 3 bytes beside 3-byte ones (or after a plain token)
+    // are left to the general path
+    if (vw::ballot((S & ~tb1 & ~(tb1 >> 1)) != 0)) return false;
     const uint32_t X0 = PL & bm, X1 = PL & am, XE = S & ~PL;  // class bits at the starts (bit 2: escape)
     if (f.pcls == CLS_NONE) {
         // first chunk: token 0 continues a virtual run of its own class begun at token 0 (see clean8)
@@ -1251,67 +1284,65 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
     rr = umin32(rr, rr - cap);
     const bool lead1 = j1 < nt && cin < CLS_ESC && rr != cap - 1u;
     const uint32_t b1v = cls_mask_f(cin) | (rr + 1u);
-    // the lane's byte count from the masks: lead bytes (the first run start's
-    // if lead1, every later run start's unless its predecessor is an escape),
-    // 0xE1 per escape start, two bytes per escape half (one for the row's last)
+    // Emission.  The run entering the lane is closed by b1v, the lead byte
+    // of the lane's first run start (lr), as before.  Every run that starts
+    // in the lane at or after lr and ends in it -- its next token, a run
+    // start, lies at most at half 15 -- emits its pending byte at its last
+    // half (END: the second half of its last token; runs inside a lane are
+    // shorter than any cap, so the byte always exists).  The output is then
+    // per half [lead][p0 p1]: lead = the pending byte at an END half or 0xE1
+    // at an escape start (LX), p0 p1 the two bytes of an escape half (EH; the
+    // row's last half has only p0, its p1 lands on the row end's slot, which
+    // lane 0 rewrites).  Output order is the reference's: a pending byte, a
+    // TAB after an escape (its half's p1), 0xE1 and raw bytes.
     const uint32_t lrbit = RS & (0u - RS);
-    const uint32_t LEAD = ((RS & ~lrbit) & ~qe) | (lead1 ? lrbit : 0u);
+    const uint32_t END = (RS >> 1) & ~S & ~ce & vm & (0u - (lrbit << 1));   // (lrbit 0: none)
+    const uint32_t LX = END | XE;
     const bool lastin = lastrel >= 0 && lastrel < 16 && ((EH >> lastrel) & 1u);
-    const uint32_t cnt = (full ? 1u : 0u) + (uint32_t)__builtin_popcount(LEAD) + (uint32_t)__builtin_popcount(XE) +
+    const uint32_t cnt = (full ? 1u : 0u) + (lead1 ? 1u : 0u) + (uint32_t)__builtin_popcount(LX) +
                          2u * (uint32_t)__builtin_popcount(EH) - (lastin ? 1u : 0u);
     const uint32_t incl2 = vw::scan_add(cnt);
     const uint32_t base = (r.wpos + incl2 - cnt) & RMASK;
-    // Per half, in token order: [lead][0xE1][payload], one byte store each.
     // A byte goes to dummy + f * (base + o - dummy) (f in {0, 1}: one
-    // v_mad_u32_u24, as esc8); the stores that emit nothing land on the
-    // shared dummy word.  Payload bytes: the first of every escape half, the
-    // second of every escape half but the row's last (its line end).
+    // v_mad_i32_i24); the stores that emit nothing land on the shared dummy
+    // word.  The lead value runs along the halves in byte 2 of lv:
+    // lv = (mask << 16) + 0x8000 at a run start (mask = the run's class mask,
+    // 0xE1 for an escape) and + 0x8000 per half after it, so at a run's last
+    // half byte 2 holds mask | its length in tokens (two halves a token).
     const int32_t dmi = (int32_t)RING_DUMMY;
     int32_t ro = (int32_t)base - dmi;           // base + o - dummy
 #ifndef VCFC_VAR_SIZE_ONLY
     if (full) r.lds[base] = (uint8_t)(cls_mask_f(cin) | cap);
-    ro += full ? 1 : 0;
-    const uint32_t EH2 = EH & ~(lastrel >= 0 && lastrel < 16 ? (1u << lastrel) : 0u);
-    // The first run start's lead byte (b1v) is stored on its own, after the
-    // loop: only payload bytes of the entering escape precede it (no lead or
-    // 0xE1 bit lies below the first run start).  The loop writes every lead
-    // (LEAD), the first one with the wrong length, and this store replaces it
-    // -- one bit test per half fewer than skipping the first start there.
-    const uint32_t bl = lrbit - 1u;   // (lrbit 0: no start, lead1 false)
-    const int32_t at1 = ro + (int32_t)__builtin_popcount(EH & bl) + (int32_t)__builtin_popcount(EH2 & bl);
-    // predecessor classes, 2 bits per half (class mask byte by one v_perm)
-    auto spread = [](uint32_t x) {   // bit i -> bit 2 i (16 bits)
-        x = (x | (x << 8)) & 0x00FF00FFu;
-        x = (x | (x << 4)) & 0x0F0F0F0Fu;
-        x = (x | (x << 2)) & 0x33333333u;
-        return (x | (x << 1)) & 0x55555555u;
-    };
-    const uint32_t pcw = spread(q0 & 0xFFFFu) | (spread(q1 & 0xFFFFu) << 1);
-    uint32_t rl = 0;   // tokens of the lane from the last run start before half h to h (a lead byte's length)
+    r.lds[(uint32_t)vw::mad24(lead1 ? 1 : 0, ro + (full ? 1 : 0), dmi)] = (uint8_t)b1v;
+    ro += (full ? 1 : 0) + (lead1 ? 1 : 0);
+    // class masks of the run starts, byte i of MW[k] for half 4k + i: plain
+    // 2a + b -> 0x00 0xA0 0xC0 0x80, escape (index 4..7) -> 0xE1
+    uint32_t MW[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t xs = vw::umul24((XE >> (4 * k)) & 0xFu, 0x00204081u) & 0x01010101u;   // XE bits -> bytes
+        MW[k] = vw::perm(0xE1E1E1E1u, 0x80C0A000u, Y[k] | (xs << 2));
+    }
+    uint32_t lv = 0;
 #pragma unroll
     for (int h = 0; h < 16; h++) {
-        const int32_t hl = (int32_t)((LEAD >> h) & 1u), es = (int32_t)((XE >> h) & 1u);
-        const int32_t e1 = (int32_t)((EH >> h) & 1u);
-        const uint32_t pc = (pcw >> (2 * h)) & 3u;    // predecessor class (plain when hr)
-        const uint32_t lb = vw::perm(0x80C0A000u, 0x80C0A000u, pc) | rl;
-        // restart at a run start, then count the half's token start (bfi:
-        // the compiler's select takes a bit test, a compare and a v_cndmask)
-        rl = vw::bfi((uint32_t)vw::sbit(RS, h), 0u, rl) + ((S >> h) & 1u);
-        const uint32_t pay = d[h >> 1] >> (16 * (h & 1));
-        r.lds[(uint32_t)(dmi + vw::mulsel(hl, ro))] = (uint8_t)lb;   // (mad24: and, cmp, add, cndmask)
-        ro += hl;
-        r.lds[(uint32_t)vw::mad24(es, ro, dmi)] = (uint8_t)0xE1u;
-        ro += es;
-        r.lds[(uint32_t)vw::mad24(e1, ro, dmi)] = (uint8_t)pay;
-        // The second byte goes out with the first: the row's last half has
-        // none (its line end), and the byte written there is the row end's
-        // own slot -- lane 0 writes the pending chunk and '\n' over it after
-        // the last step (cnt does not count it).  One bit extraction fewer
-        // per half than testing EH2.
-        r.lds[(uint32_t)(dmi + e1 * (ro + 1))] = (uint8_t)(pay >> 8);   // (a plain multiply: mad24 on ro + 1 costs two shifts to sign-extend it)
-        ro += 2 * e1;
+        // (mask << 16) | 0x8000: byte h & 3 of MW to byte 2, 0x80 to byte 1
+        const uint32_t m3 = vw::perm(MW[h >> 2], 0x00008000u, 0x0C04010Cu + ((uint32_t)(h & 3) << 16));
+        lv = vw::bfi((uint32_t)vw::sbit(RS, h), m3, lv + 0x8000u);
+        const int32_t fl = (int32_t)((LX >> h) & 1u), fe = (int32_t)((EH >> h) & 1u);
+        const uint32_t w = d[h >> 1], wh = w >> 8;
+        vw::lds_st8<0, true>(vw::lds_sel(r.lds, fl, ro, dmi), lv);   // byte 2
+        ro += fl;
+        const vw::ldsp pa = vw::lds_sel(r.lds, fe, ro, dmi);
+        if (h & 1) {
+            vw::lds_st8<0, true>(pa, w);
+            vw::lds_st8<1, true>(pa, wh);
+        } else {
+            vw::lds_st8<0, false>(pa, w);
+            vw::lds_st8<1, false>(pa, wh);
+        }
+        ro += 2 * fe;
     }
-    r.lds[(uint32_t)vw::mad24(lead1 ? 1 : 0, at1, dmi)] = (uint8_t)b1v;   // (program order: after the loop's store there)
 #endif
     ring_unwrap(r, base + cnt);
     r.wpos += vw::readlane(incl2, 63);
@@ -1328,8 +1359,34 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
     return true;
 }
 
-// defer_ok: the row may be deferred (*deferred: it was -- sized only, the
-// ring's bytes never left it; k_encode_var)
+// The chunk loop of a variable-token row from chunk C on: x, y, z hold
+// chunks C, C + 1, C + 2 (three in flight, a single loop exit, see
+// encode_fast).  false: not this shape.
+template <int VM>
+__device__ __forceinline__ bool var_chunks(Chunk8v &x, Chunk8v &y, Chunk8v &z, uint32_t C, uint32_t ncG,
+                                           vw::brsrc rsG, uint32_t lo32, VarState &f, Ring &r) {
+    bool ok = true;
+    for (;;) {
+        ok = vw::readfirst(gt_var8<VM>(x, C, f, r));
+        x = load_chunk8v(rsG, C + 3, lo32);
+        vw::pin_loads();
+        if (ok && C + 1 < ncG) ok = vw::readfirst(gt_var8<VM>(y, C + 1, f, r));
+        y = load_chunk8v(rsG, C + 4, lo32);
+        vw::pin_loads();
+        if (ok && C + 2 < ncG) ok = vw::readfirst(gt_var8<VM>(z, C + 2, f, r));
+        z = load_chunk8v(rsG, C + 5, lo32);
+        vw::pin_loads();
+        C = vw::readfirst(C + 3);
+        if (!ok || C >= ncG) break;
+    }
+    return ok;
+}
+
+// k_encode_var with deferred records (VAR_DEFER) decides a row's fate on its
+// first genotype chunk (deferred when it is an escape chunk and more chunks
+// follow).  (A copy of the chunk loop per fate, so that staged rows would
+// run the default kernel's code, spilled 156 bytes per lane.)  *deferred:
+// the row was only sized (RING_SIZE), the ring's bytes never left it.
 template <int VM>
 __device__ bool encode_var(const uint8_t *__restrict__ line, uint32_t len, Ring &r, uint32_t *rec_bytes, bool nlc,
                            bool *nlhit, bool *deferred) {
@@ -1367,26 +1424,11 @@ __device__ bool encode_var(const uint8_t *__restrict__ line, uint32_t len, Ring 
     const uint32_t ncG = (NH + HPC - 1) / HPC;
     f.defer = VM == VAR_DEFER && ncG > 1 ? 1u : 0u;
     const uint32_t lo32 = BPL8 * l;
-    // three chunks in flight, a single loop exit (see encode_fast)
     Chunk8v b0 = load_chunk8v(rsG, 0, lo32);
     Chunk8v b1 = load_chunk8v(rsG, 1, lo32);
     Chunk8v b2 = load_chunk8v(rsG, 2, lo32);
     vw::pin_loads();
-    uint32_t C = 0;
-    bool ok = true;
-    for (;;) {
-        ok = vw::readfirst(gt_var8<VM>(b0, C, f, r));
-        b0 = load_chunk8v(rsG, C + 3, lo32);
-        vw::pin_loads();
-        if (ok && C + 1 < ncG) ok = vw::readfirst(gt_var8<VM>(b1, C + 1, f, r));
-        b1 = load_chunk8v(rsG, C + 4, lo32);
-        vw::pin_loads();
-        if (ok && C + 2 < ncG) ok = vw::readfirst(gt_var8<VM>(b2, C + 2, f, r));
-        b2 = load_chunk8v(rsG, C + 5, lo32);
-        vw::pin_loads();
-        C = vw::readfirst(C + 3);
-        if (!ok || C >= ncG) break;
-    }
+    const bool ok = var_chunks<VM>(b0, b1, b2, 0, ncG, rsG, lo32, f, r);
     if (!ok) {
         *nlhit = f.nlhit != 0;
         return false;
@@ -1689,7 +1731,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 6))) voi
     Ring r;
     if (!row_setup(a, row, lds + wave * RING_STRIDE, r)) return;
     uint32_t bytes = 0;
-    const bool ok = encode_fast(a.buf + a.line_off[row], a.line_len[row], r, &bytes);
+    const bool ok = encode_fast(a.buf + a.line_off[row], a.line_len[row], r, &bytes, a.defer_records != 0);
     VCFC_DIAG_ROW_END(a, row);
     if (vw::lane_id() == 0) {
         // not the fast shape: k_encode_var's wave for this row takes it

@@ -124,6 +124,13 @@ __device__ __forceinline__ uint32_t alignbit(uint32_t hi, uint32_t lo, uint32_t 
 }
 // x + a*b on the low 24 bits of a and b, signed (v_mad_i32_i24)
 __device__ __forceinline__ int32_t mad24(int32_t a, int32_t b, int32_t x) { return x + __mul24(a, b); }
+// (a & 0xFFFFFF) * (b & 0xFFFFFF), low 32 bits (v_mul_u32_u24, full rate)
+__device__ __forceinline__ uint32_t umul24(uint32_t a, uint32_t b) { return __umul24(a, b); }
+// sum of the byte products a_i * b_i, + c (v_dot4_u32_u8, one instruction):
+// with b = 0x08040201 and bytes of a in {0, 1}, the four bytes' flags as 4 bits
+__device__ __forceinline__ uint32_t dot4u(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_udot4(a, b, c, false);
+}
 // f * x for a flag f in {0, 1} and x in signed 24 bits, as one v_mul_i32_i24
 // (left to itself the compiler turns some of these selects into a bit test,
 // a compare, an add and a v_cndmask)
@@ -140,6 +147,24 @@ __device__ __forceinline__ int32_t mulsel(int32_t f, int32_t x) {
     int32_t r;
     __asm__("v_mul_i32_i24 %0, %1, %2" : "=v"(r) : "v"(f), "v"(x));
     return r;
+}
+// LDS byte stores at lds + dm + f * x + OFF (f a flag in {0, 1}, x and dm
+// signed 24-bit): the address is ONE v_mad_i32_i24 whatever the flag, shared
+// by stores at offsets 0 and 1, and each store one ds_write_b8 (byte 0 of v)
+// or ds_write_b8_d16_hi (byte 2).  Hand-written: left to itself the compiler
+// merges the two adjacent byte stores into a ds_write_b16 at an odd address
+// (misaligned) and turns some flag multiplies into v_mad_u64_u32.
+struct ldsp { uint32_t a; };
+__device__ __forceinline__ ldsp lds_sel(uint8_t *lds, int32_t f, int32_t x, int32_t dm) {
+    const uint32_t b = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t *)lds + (uint32_t)dm;
+    uint32_t a;
+    __asm__("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(a) : "v"(f), "v"(x), "v"(b));
+    return ldsp{a};
+}
+template <int OFF, bool HI>
+__device__ __forceinline__ void lds_st8(ldsp p, uint32_t v) {
+    if (HI) __asm__ volatile("ds_write_b8_d16_hi %0, %1 offset:%2" ::"v"(p.a), "v"(v), "i"(OFF) : "memory");
+    else __asm__ volatile("ds_write_b8 %0, %1 offset:%2" ::"v"(p.a), "v"(v), "i"(OFF) : "memory");
 }
 // ((hi:lo) >> 8*s)[31:0]
 __device__ __forceinline__ uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t s) {

@@ -38,7 +38,7 @@ EXPORTS = [
     "vcfc_sparsify_shard", "vcfc_ctx_set_ingest_chunk", "vcfc_record_hash_device",
     "vcfc_compress_range", "vcfc_compress_device", "vcfc_compress_range_held", "vcfc_held_place",
     "vcfc_held_sizes", "vcfc_held_free", "vcfc_ctx_set_line_index", "vcfc_ctx_set_trace",
-    "vcfc_ctx_set_deferred_records",
+    "vcfc_ctx_set_deferred_records", "vcfc_encode_deferred_rows",
 ]
 LINE_INDEX_HOP, LINE_INDEX_SCAN = 0, 1                       # include/vcfc.h VCFC_LINE_INDEX_*
 TRACE_INGEST, TRACE_DEVICE, TRACE_SPARSE_QUERY = 1, 2, 4     # include/vcfc.h VCFC_TRACE_*
@@ -70,9 +70,16 @@ def lib():
     L.vcfc_ctx_destroy.argtypes = [vp]
     L.vcfc_ctx_destroy.restype = None
     L.vcfc_ctx_set_ingest_chunk.argtypes = [vp, u64]
-    L.vcfc_ctx_set_line_index.argtypes = [vp, ctypes.c_int]
-    L.vcfc_ctx_set_trace.argtypes = [vp, ctypes.c_uint]
-    L.vcfc_ctx_set_deferred_records.argtypes = [vp, ctypes.c_int]
+    # Exports added since round 3 are bound only when present: A/B runs load
+    # older builds of the library (tools/ab.sh, VCFC_LIB); calling one that
+    # the loaded build lacks raises a clear error (_need).  test_capi checks
+    # that the current build exports every one of them.
+    late = {"vcfc_ctx_set_line_index": [vp, ctypes.c_int], "vcfc_ctx_set_trace": [vp, ctypes.c_uint],
+            "vcfc_ctx_set_deferred_records": [vp, ctypes.c_int],
+            "vcfc_encode_deferred_rows": [vp, u64, u64, vp, ctypes.POINTER(u64)]}
+    for name, args in late.items():
+        if hasattr(L, name):
+            getattr(L, name).argtypes = args
     L.vcfc_record_hash_device.argtypes = [vp, vp, u64, vp, vp]
     L.vcfc_compress_range.argtypes = [vp, ctypes.c_char_p, u64, u64, ctypes.c_int, u64, ctypes.POINTER(u64),
                                       ctypes.POINTER(i64), ctypes.POINTER(u64)]
@@ -260,18 +267,18 @@ class Context:
     def set_line_index(self, mode):
         """compress_device's line index: "hop" (default; guessed line ends,
         checked) or "scan" (every byte).  The output does not depend on it."""
-        raise_for(lib().vcfc_ctx_set_line_index(self._h, {"hop": LINE_INDEX_HOP, "scan": LINE_INDEX_SCAN}[mode]))
+        raise_for(_need("vcfc_ctx_set_line_index")(self._h, {"hop": LINE_INDEX_HOP, "scan": LINE_INDEX_SCAN}[mode]))
 
     def set_deferred_records(self, on):
-        """Deferred records for the file / device compress calls (off by
-        default): rows whose first genotype chunk is all escapes are sized
-        first and written straight into the output (include/vcfc.h).  The
-        output does not depend on it."""
-        raise_for(lib().vcfc_ctx_set_deferred_records(self._h, 1 if on else 0))
+        """Deferred records for the file / device compress calls (on by
+        default since round 5): rows whose first genotype chunk is all
+        escapes are sized first and written straight into the output
+        (include/vcfc.h).  The output does not depend on it."""
+        raise_for(_need("vcfc_ctx_set_deferred_records")(self._h, 1 if on else 0))
 
     def set_trace(self, flags):
         """Stage timings of the host drivers to stderr (TRACE_* flags)."""
-        raise_for(lib().vcfc_ctx_set_trace(self._h, int(flags)))
+        raise_for(_need("vcfc_ctx_set_trace")(self._h, int(flags)))
 
     def __enter__(self):
         return self
@@ -482,6 +489,22 @@ def encode_rows_device(d_buf, d_line_off, d_line_len, n, total_line_bytes, d_out
     st = lib().vcfc_encode_rows_device(d_buf, d_line_off, d_line_len, n, total_line_bytes, d_out, out_cap,
                                        d_rec_off, d_ws, ws_bytes, d_err, stream)
     raise_for(st)
+
+
+def _need(name):
+    """The export `name` of the loaded library (an older build loaded through
+    VCFC_LIB may lack it: a clear error instead of an AttributeError)."""
+    L = lib()
+    if not hasattr(L, name):
+        raise RuntimeError("%s: %s is not exported by this build of libvcfc.so" % (LIB_PATH, name))
+    return getattr(L, name)
+
+
+def encode_deferred_rows(d_ws, n, total_line_bytes, stream=0):
+    """Rows the last encode_rows_device on workspace d_ws deferred (waits for stream)."""
+    v = ctypes.c_uint64(0)
+    raise_for(_need("vcfc_encode_deferred_rows")(d_ws, n, total_line_bytes, stream, ctypes.byref(v)))
+    return int(v.value)
 
 
 class StageTimer:
