@@ -394,12 +394,12 @@ def test_deferred_records(monkeypatch):
         elif kind == 4:   # 3-byte tokens: the fast kernel
             ln = b"\t".join([b"1", b"%d" % i, b"a", b"b", b"c", b"d", b"e", b"f", b"GT"] +
                             [rnd.choice([b"0|0", b"0|1", b"1|1", b"0|2"]) for _ in range(rnd.randint(1, 900))])
-        elif kind == 5:   # every token an unphased / missing escape over > 512 tokens: k_encode_fast hands
-            # the row on after its first chunk, k_encode_var defers it (mixed 0|1 tokens later on)
-            S = rnd.choice([513, 700, 1100])
-            toks = [rnd.choice([b"0/0", b"0/1", b"1/1", b"./."]) for _ in range(S)]
+        elif kind == 5:   # 3-byte escapes beside 1-byte ones over > 1 chunk: k_encode_var's escape chunks
+            # (no plain token), deferred; mixed 0|1 tokens later on in half of them
+            S = rnd.choice([700, 900, 1300])
+            toks = [rnd.choice([b"0/0", b"0/1", b"1/1", b"./.", b"0", b"."]) for _ in range(S)]
             if i % 2:
-                toks[600:] = [rnd.choice([b"0|0", b"0|1"]) for _ in toks[600:]]
+                toks[800:] = [rnd.choice([b"0|0", b"0|1"]) for _ in toks[800:]]
             ln = PFX_V + b"\t".join(toks)
             expect_defer += 1
         else:             # the same within one chunk (<= 512 tokens): staged by the fast kernel

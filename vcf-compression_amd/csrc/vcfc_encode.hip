@@ -130,6 +130,14 @@ __device__ __forceinline__ void ring_stage(Ring &r, uint32_t f, uint4 v) {
     return;
 #endif
     if (DYN && r.mode == RING_SIZE) return;
+    if (DYN && r.mode == RING_DIRECT) {
+        // a deferred record straight into out, at the record's own (any)
+        // alignment: plain stores, so that L2 merges the 16-byte pieces
+        // into whole lines (non-temporal output stores were slower in the
+        // compaction too, §4)
+        vw::gstore16(r.prim, f, v);
+        return;
+    }
     if (r.fpos < r.pb) vw::gstore16_nt(r.prim, f, v);
     else vw::gstore16_nt(r.slot, f - r.pb, v);
 }
@@ -274,8 +282,6 @@ struct FastState {
     uint32_t T, phi;    // token count, gt0's byte phase mod 4
     uint32_t pcls, prs; // class / run start(+1) of the previous token
     uint32_t esc;       // the last genotype chunk held an escape: test the escape shape first
-    uint32_t hand;      // deferred records on and more than one genotype chunk: an all-escape chunk 0 hands the row on
-    uint32_t handoff;   // ... and it did (encode_fast returns false: k_encode_var takes the row and defers it)
 };
 
 // Prefix phase for chunk c: 0 = no sample yet, 1 = first sample starts in
@@ -840,19 +846,10 @@ __device__ __forceinline__ bool gt_step8(const Chunk8 &cur, uint32_t C, FastStat
             return true;
         }
         if (vw::ballot(shape3<false>(d, t0, T)) == 0) {
-            if (f.hand && C == 0) {
-                // every token of chunk 0 an escape (unphased "0/1", "./."):
-                // records ~1.25x the line, so with deferred records on the
-                // row goes to k_encode_var, which sizes it and has it
-                // written straight to out instead of staged and copied
-                bool plain = false;
-#pragma unroll
-                for (int j = 0; j < (int)TPL8; j++) plain |= ((d[j] ^ Z) & 0xFFFEFFFEu) == 0;
-                if (vw::ballot(plain) == 0) {
-                    f.handoff = 1;
-                    return false;
-                }
-            }
+            // (Round 5 handed rows whose chunk 0 is all escapes -- unphased
+            // "0/1", "./." -- to k_encode_var to be deferred: law 2 +4 %,
+            // law 0 +1 % in an A/B, profiles/r05/ab/ab_r5c_law{2,0}.txt;
+            // removed.)
             esc8<false>(d, t0, tf, f, r);
             return true;
         }
@@ -877,7 +874,7 @@ __device__ __forceinline__ bool gt_step8(const Chunk8 &cur, uint32_t C, FastStat
     return false;   // tokens of another length or empty fields: the caller runs gt_general on this chunk
 }
 
-__device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring &r, uint32_t *rec_bytes, bool defer) {
+__device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring &r, uint32_t *rec_bytes) {
     const uint32_t l = vw::lane_id();
     const uint32_t lead = (uint32_t)(reinterpret_cast<uintptr_t>(line) & 15);
     const uint8_t *A = line - lead;
@@ -887,7 +884,6 @@ __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring
     const uint32_t lo16 = BPL * l;
     FastState f;
     f.nf = 0; f.carryT = 1; f.gt0 = -1; f.T = 0; f.phi = 0; f.pcls = CLS_NONE; f.prs = 0; f.esc = 0;
-    f.hand = 0; f.handoff = 0;
     r.wpos = 8;
     r.fpos = 0;
 
@@ -915,7 +911,6 @@ __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring
     const vw::brsrc rsG = vw::make_rsrc(line + f.gt0 - phi, (phi + len - (uint32_t)f.gt0 + 3u) & ~3u);
     const uint32_t ncG = (T + SLOTS8 - 1) / SLOTS8;
     const uint32_t lo32 = BPL8 * l;
-    f.hand = defer && ncG > 1 ? 1u : 0u;
     uint32_t C0 = 0;
     // three chunks in flight per wave (two: 8 waves/SIMD but +3 % on the
     // headline law, ab_depth_occupancy.txt; four: 5 waves/SIMD, slower,
@@ -941,7 +936,6 @@ __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring
             if (!ok || C >= ncG) break;
         }
         if (ok) break;
-        if (f.handoff) return false;   // (an all-escape chunk 0: k_encode_var's row)
         // chunk `gen`: the general step over its two 1 KiB halves
         for (uint32_t h = 0; h < 2; h++) {
             const Chunk hc = look_ahead(load_chunk(rsG, 2 * gen + h, lo16));
@@ -1106,17 +1100,31 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
     // plain 3-byte candidates: bytes "a|b" from the half, a, b in {0,1}; a, b bits
     // (SWAR over the halves' first bytes A and second bytes P, four halves a
     // word: half 4k + i is byte i of A[k] / P[k])
-    uint32_t tb0, tb1;
-    {
-        const uint32_t z8 = zero_bytes4(d[8] ^ 0x09090909u);   // halves 16, 17
-        tb0 = even2(z8) << 16;
-        tb1 = odd2(z8) << 16;
-    }
+    // (round 5: 0x80 in each TAB byte of a dword, then the flags of its
+    // first bytes (0, 2: halves 2j, 2j + 1) and of its second bytes (1, 3)
+    // weighted into the masks by v_dot4_u32_u8 -- byte weights up to 128, so
+    // two accumulators of eight halves each)
+    auto tabz = [](uint32_t x) {
+        const uint32_t w = x ^ 0x09090909u;
+        return ~(((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w | 0x7F7F7F7Fu);
+    };
+    uint32_t a0 = 0, a1 = 0, b0 = 0, b1 = 0;
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        tb0 |= zero_bytes4(vw::perm(d[2 * k + 1], d[2 * k], 0x06040200u) ^ 0x09090909u) << (4 * k);
-        tb1 |= zero_bytes4(vw::perm(d[2 * k + 1], d[2 * k], 0x07050301u) ^ 0x09090909u) << (4 * k);
+    for (int j = 0; j < 8; j++) {
+        const uint32_t z = tabz(d[j]);
+        const uint32_t wf = (1u << (2 * (j & 3))) | (2u << (2 * (j & 3) + 16));   // bytes 0, 2
+        const uint32_t ws = wf << 8;                                              // bytes 1, 3
+        if (j < 4) {
+            a0 = vw::dot4u(z, wf, a0);
+            a1 = vw::dot4u(z, ws, a1);
+        } else {
+            b0 = vw::dot4u(z, wf, b0);
+            b1 = vw::dot4u(z, ws, b1);
+        }
     }
+    const uint32_t z8 = tabz(d[8]);   // halves 16, 17
+    uint32_t tb0 = (a0 >> 7) | ((b0 >> 7) << 8) | ((vw::dot4u(z8, 0x00020001u, 0u) >> 7) << 16);
+    uint32_t tb1 = (a1 >> 7) | ((b1 >> 7) << 8) | ((vw::dot4u(z8, 0x02000100u, 0u) >> 7) << 16);
     if (lastrel >= 0 && lastrel <= 17) tb1 |= 1u << lastrel;   // the row's last half ends its token (line end)
     if (vw::ballot((tb0 & vm) != 0)) return false;           // an empty field, or a token of even length
     // token starts: after a half whose second byte is a TAB (lane 0: the chunk carry)
@@ -1129,8 +1137,7 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
     // token 0: no lead byte) and every token of the chunk is an escape -- no
     // 3-byte token starts here (1-byte tokens, 5 and more: GT:DP:GQ), or,
     // found after the classification below, none of its 3-byte tokens is
-    // plain (unphased "0/1", "./.": the rows k_encode_fast hands on with
-    // deferred records on).  Every half then belongs to an escape: each emits
+    // plain (unphased "0/1", "./." beside haploid or GT:DP:GQ tokens).  Every half then belongs to an escape: each emits
     // its bytes, a start 0xE1 first -- the input with 0xE1 before every token.
     const bool pesc = f.pcls == CLS_ESC || f.pcls == CLS_NONE;
     auto esc_chunk = [&]() {
@@ -1731,7 +1738,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 6))) voi
     Ring r;
     if (!row_setup(a, row, lds + wave * RING_STRIDE, r)) return;
     uint32_t bytes = 0;
-    const bool ok = encode_fast(a.buf + a.line_off[row], a.line_len[row], r, &bytes, a.defer_records != 0);
+    const bool ok = encode_fast(a.buf + a.line_off[row], a.line_len[row], r, &bytes);
     VCFC_DIAG_ROW_END(a, row);
     if (vw::lane_id() == 0) {
         // not the fast shape: k_encode_var's wave for this row takes it
