@@ -61,8 +61,9 @@ def parse():
                          "file -> file compress (row e: every rank its byte range, outputs held and placed at "
                          "the all-gathered offsets), --ingest-rows rows per rank")
     ap.add_argument("--dist-dir", default="/tmp/vcfc_distfile", help="--mode distfile: where the files go")
-    ap.add_argument("--deferred-records", action="store_true",
-                    help="devfile: vcfc_ctx_set_deferred_records (GT:DP:GQ-like rows written straight to the output)")
+    ap.add_argument("--deferred-records", choices=["on", "off"], default="on",
+                    help="devfile: vcfc_ctx_set_deferred_records (on by default since round 5: GT:DP:GQ-like rows "
+                         "written straight to the output)")
     ap.add_argument("--line-index", choices=["hop", "scan"], default="hop",
                     help="--mode devfile: the line index (hop: line ends guessed from the header's sample count "
                          "and checked; scan: every byte)")
@@ -174,6 +175,21 @@ def load_pmc(workload_key, name="pmc_k_encode.json"):
             continue
         if d.get("workload") == workload_key:
             return d.get("hbm_bytes_per_launch")
+    return None
+
+
+def load_pmc_step(workload_key):
+    """HBM bytes of the whole encode step (k_encode kernels + k_compact_out)
+    per call, from the same committed PMC summary as load_pmc, or None."""
+    import glob
+    for p in [os.path.join(REPO, "profiles", "pmc_k_encode.json")] + sorted(
+            glob.glob(os.path.join(REPO, "profiles", "pmc_k_encode_*.json"))):
+        try:
+            d = json.load(open(p))
+        except Exception:
+            continue
+        if d.get("workload") == workload_key and "kernels" in d:
+            return sum(v.get("hbm_bytes", 0) for v in d["kernels"].values())
     return None
 
 
@@ -500,7 +516,7 @@ def bench_devfile(args, torch, vcfc, workload):
     if args.dev_chunk:
         ctx.set_ingest_chunk(args.dev_chunk)
     ctx.set_line_index(args.line_index)
-    ctx.set_deferred_records(args.deferred_records)
+    ctx.set_deferred_records(args.deferred_records == "on")
     for _ in range(args.warmup):
         st, k, _ = ctx.compress_device(d_file.data_ptr(), N, d_out.data_ptr(), cap)
         assert st == 0 and k == want_len, (st, k, want_len)
@@ -521,7 +537,7 @@ def bench_devfile(args, torch, vcfc, workload):
            "config": {"workload": "%s %d samples x %d variants, %.2f GB file in HBM (BASELINE configs[1])"
                                   % (law_name(args.law), S, n, N / 1e9),
                       "file_bytes": N, "output_bytes": want_len,
-                      "deferred_records": args.deferred_records,
+                      "deferred_records": args.deferred_records == "on",
                       "chunk": ("%d bytes of whole lines per line index + encode" % args.dev_chunk) if args.dev_chunk
                                else "the whole file (one line index, one encode)",
                       "line_index": ("hop (line ends guessed from the header's sample count, ~1.2 KiB read per "
@@ -530,7 +546,7 @@ def bench_devfile(args, torch, vcfc, workload):
                         "achieved": round(alg / (ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                         "traffic": load_pmc("%s/%dx%d/%s%s" % (law_name(args.law), S, n, args.line_index,
-                                                                  "/deferred" if args.deferred_records else ""),
+                                                                  "" if args.deferred_records == "on" else "/nodefer"),
                                             "pmc_devfile.json"),
                         "algorithmic_bytes_per_step": alg,
                         "note": "file bytes read once + output written once (the scan index reads the file "
@@ -1121,6 +1137,10 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     stages, calls = timer.read()
+    try:
+        deferred = vcfc.encode_deferred_rows(ws.data_ptr(), n, rows.line_bytes, stream)
+    except RuntimeError:   # (an A/B build of the library without the export)
+        deferred = None
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -1154,6 +1174,7 @@ def main():
     roof = {"kernel": "k_encode", "bound": "hbm", "achieved": round(alg / (k_ms * 1e-3) / 1e9, 1),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(alg / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "traffic": load_pmc(wkey),
+            "step_traffic": load_pmc_step(wkey),
             "algorithmic_bytes_per_launch": alg, "avg_launch_ms": round(k_ms, 4),
             "measured_torch_copy_gbs": copy_gbs,
             "stages_ms": {k: round(v / max(calls, 1), 4) for k, v in stages.items()}}
@@ -1165,6 +1186,7 @@ def main():
                       "samples": S, "rows_per_gpu": n, "gt_bytes_per_gpu": rows.gt_bytes,
                       "line_bytes_per_gpu": rows.line_bytes, "record_bytes_per_gpu": out_bytes,
                       "compression_ratio": round(out_bytes / rows.line_bytes, 4),
+                      "deferred_rows": deferred,
                       "parallelism": "row shards x%d, RCCL all-gather of shard sizes" % world},
            "rccl_world": rccl,
            "roofline": roof}

@@ -262,3 +262,46 @@ def test_encode_captured_in_hip_graph(torch, vcfc):
         assert np.array_equal(r, want_rec)
         k = int(r[n])
         assert torch.equal(out[:k], want_out[:k])
+
+
+@pytest.mark.parametrize("law,kind", [(2, "1"), (1, None), (0, None), (2, None), (2, "3")])
+def test_deferred_records_chosen_per_row(torch, vcfc, monkeypatch, law, kind):
+    """Deferred records are on by default (round 5) and the kernel chooses them
+    per row from the row's bytes: every GT:DP:GQ row (law-2 kind 1: its first
+    genotype chunk all escapes, more than one chunk) is deferred, no row of
+    the chr22 / random_vcf laws nor an unphased row of 3-byte escapes (kind
+    3: the fast kernel's, staged) is, and in the law-2 mix exactly the
+    GT:DP:GQ rows are.  Every record equals the oracle's."""
+    import workload
+    if kind is None:
+        monkeypatch.delenv("VCFC_LAW2_KIND", raising=False)
+    else:
+        monkeypatch.setenv("VCFC_LAW2_KIND", kind)
+    n, S = 3000, 2504
+    rows = workload.DeviceRows(torch, vcfc, n, S, law, seed=91 + law, device="cuda:0")
+    ws_bytes = vcfc.workspace_size(n, rows.line_bytes)
+    cap = vcfc.encode_bound(n, rows.line_bytes)
+    dev = rows.buf.device
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    out = torch.empty(cap, dtype=torch.uint8, device=dev)
+    rec = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    err = torch.empty(1, dtype=torch.int64, device=dev)
+    vcfc.encode_rows_device(rows.buf.data_ptr(), rows.line_off.data_ptr(), rows.line_len.data_ptr(), n,
+                            rows.line_bytes, out.data_ptr(), cap, rec.data_ptr(), ws.data_ptr(), ws_bytes,
+                            err.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    deferred = vcfc.encode_deferred_rows(ws.data_ptr(), n, rows.line_bytes, torch.cuda.current_stream().cuda_stream)
+    assert int(err.cpu().numpy().view(np.uint64)[0]) == vcfc.NO_ERROR
+    lines = rows.host_lines(range(n))
+    gdg = sum(b"GT:DP:GQ" in ln for ln in lines)
+    assert deferred == gdg, (deferred, gdg)
+    if kind == "1":
+        assert gdg == n
+    elif law != 2 or kind == "3":
+        assert gdg == 0
+    else:
+        assert 0 < gdg < n
+    r = rec.cpu().numpy()
+    blob = out[:int(r[n])].cpu().numpy().tobytes()
+    for i, ln in enumerate(lines):
+        st, want = G.oracle_encode_line(ln)
+        assert st == 0 and blob[int(r[i]):int(r[i + 1])] == want, i

@@ -159,6 +159,7 @@ struct ItemState {
 };
 struct ItemLane {
     uint32_t start;    // bit j: byte j of the lane's dword starts an item
+    uint32_t e1;       // bit j: byte j is an escape flag (0xE1)
     uint32_t gb[4];    // tokens before each byte's item
 };
 
@@ -196,6 +197,7 @@ __device__ __forceinline__ ItemLane scan_window(uint32_t v4, uint32_t b0, uint32
     const uint32_t T = ep;                          // terminator bytes (4 after a flag)
     ItemLane r;
     r.start = valid & ~P & ~T;
+    r.e1 = e1M;
     const int32_t lim = (int32_t)(s1 - k0) - 4;     // an escape at byte j needs j <= lim
     const uint32_t overM = lim >= 3 ? 0u : lim < 0 ? 0xFu : (0xFu << (lim + 1)) & 0xFu;
     const uint32_t bad = (P & ~T & (msb4(hb) | tabM | lfM)) | (T & ~tabM) |
@@ -527,14 +529,18 @@ __device__ __forceinline__ void write_one(const VcfcDecodeArgs &a, uint64_t i, u
         // gives its 3 payload bytes, a 0|0 run byte (< 0x80) "0|0", a phased
         // run byte 0x80 / 0xA0 / 0xC0 "1|1" / "0|1" / "1|0"; and the token
         // index of each item start (~0 for bytes that start none: never in a tile)
+        // (round 5: the allele bits of all four bytes at once -- a run byte
+        // 0x80 / 0xA0 / 0xC0 has a = 1 unless bit 5, b = 1 unless bit 6, a
+        // 0|0 run byte (< 0x80) neither -- and each word "a|b\t" by one
+        // v_perm of the two bit words: 11 VALU per byte -> 6)
+        const uint32_t h7 = (v4 >> 7) & 0x01010101u;
+        const uint32_t ab = h7 & ~(v4 >> 5), bb = h7 & ~(v4 >> 6);
         uint32_t w[4], ws[4];
 #pragma unroll
         for (uint32_t j = 0; j < 4; j++) {
-            const uint32_t x = (v4 >> (8 * j)) & 0xFFu;
             const uint32_t pay = (j < 3 ? vw::alignbyte(v4n, v4, j + 1) : v4n) & 0x00FFFFFFu;
-            const uint32_t m = x >> 5;   // 4: 1|1, 5: 0|1, 6: 1|0
-            const uint32_t ph = (m == 5u ? 0x30u : 0x31u) | 0x7C00u | ((m == 6u ? 0x30u : 0x31u) << 16);
-            w[j] = (x == 0xE1u ? pay : x < 0x80u ? 0x307C30u : ph) | 0x09000000u;
+            const uint32_t ph = vw::perm(ab, bb, 0x0C000C04u + j * 0x00010001u) | 0x09307C30u;
+            w[j] = (it.e1 >> j) & 1u ? (pay | 0x09000000u) : ph;
             ws[j] = (it.start >> j) & 1u ? it.gb[j] : ~0u;
         }
         for (;;) {
