@@ -84,6 +84,7 @@ inline uint32_t dot4u(uint32_t a, uint32_t b, uint32_t c) {
 struct ldsp { uint8_t *a; };
 inline ldsp lds_sel(uint8_t *lds, int32_t f, int32_t x, int32_t dm) { return ldsp{lds + mad24(f, x, dm)}; }
 template <int OFF, bool HI> inline void lds_st8(ldsp p, uint32_t v) { p.a[OFF] = (uint8_t)(HI ? (v >> 16) : v); }
+inline void lds_st32(ldsp p, uint32_t v) { memcpy(p.a, &v, 4); }
 inline uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) { return (a & m) | (b & ~m); }
 inline int32_t sbit(uint32_t x, uint32_t bit) { return ((x >> bit) & 1u) ? -1 : 0; }
 inline void wave_sync() { emu::collective(emu::OP_WAVESYNC, 0, 0, 0); }

@@ -736,16 +736,19 @@ __device__ __forceinline__ void esc8(const uint32_t (&d)[TPL8], int32_t t0, int3
     const uint32_t mL = vw::perm(0x08u, 0x80C0A000u, cpL & 0x07070707u) + 0x03020100u;   // mask + slot index
     const uint32_t mH = vw::perm(0x08u, 0x80C0A000u, cpH & 0x07070707u) + 0x07060504u;
     int32_t njp = -(int32_t)j1;   // minus the previous start
+    // (round 5: the addresses as hand-written v_mad_i32_i24, vw::lds_sel --
+    // the compiler had made most of them 64-bit v_mad_u64_u32)
+    int32_t ro = ldm + (int32_t)o;
 #pragma unroll
     for (int j = 0; j < (int)TPL8; j++) {
         const int32_t s = (int32_t)((sbr >> (4 * j)) & 1u);
         const int32_t e = (int32_t)((eb >> (4 * j)) & 1u);
         const uint32_t b = ((((j < 4) ? mL : mH) >> (8 * (j & 3))) & 0xFFu) + (uint32_t)njp;
-        r.lds[(uint32_t)vw::mad24(s, ldm + (int32_t)o, (int32_t)dmi)] = (uint8_t)b;
-        o += (uint32_t)s;
+        vw::lds_st8<0, false>(vw::lds_sel(r.lds, s, ro, (int32_t)dmi), b);
+        ro += s;
         const uint32_t pay = (d[j] << 8) | 0xE1u;   // 0xE1, then the token's three bytes
-        __builtin_memcpy(r.lds + (uint32_t)vw::mad24(e, ldm + (int32_t)o, (int32_t)dmi), &pay, 4);
-        o += 4u * (uint32_t)e;
+        vw::lds_st32(vw::lds_sel(r.lds, e, ro, (int32_t)dmi), pay);
+        ro += 4 * e;
         njp = s ? -j : njp;
     }
     ring_unwrap(r, base + cnt);
@@ -1151,7 +1154,6 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
         // addressed as in the mixed step below
         const int32_t dmi = (int32_t)RING_DUMMY;
         int32_t ro = (int32_t)base - dmi;
-        const uint32_t vm2 = vm & ~(lastin ? (1u << lastrel) : 0u);
         // A row whose first chunk is all escapes (GT:DP:GQ, records about
         // 1.1x the input) is deferred: sized here, its record written
         // straight to out by k_encode_defer once the size scan has placed it,
@@ -1193,16 +1195,24 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
             }
             r.lds[a + 31u] = (uint8_t)(hi8 >> 16);   // half 15's second byte
         } else {
+        // (the row's last half: its second byte, the line end, goes to the
+        // row end's own slot, which lane 0 rewrites; see the mixed step)
 #pragma unroll
         for (int h = 0; h < 16; h++) {
             const int32_t es = (int32_t)((S >> h) & 1u);
-            const int32_t e1 = (int32_t)((vm >> h) & 1u), e2 = (int32_t)((vm2 >> h) & 1u);
-            const uint32_t pay = d[h >> 1] >> (16 * (h & 1));
-            r.lds[(uint32_t)vw::mad24(es, ro, dmi)] = (uint8_t)0xE1u;
+            const int32_t e1 = (int32_t)((vm >> h) & 1u);
+            const uint32_t w = d[h >> 1], wh = w >> 8;
+            vw::lds_st8<0, false>(vw::lds_sel(r.lds, es, ro, dmi), 0xE1u);
             ro += es;
-            r.lds[(uint32_t)vw::mad24(e1, ro, dmi)] = (uint8_t)pay;
-            r.lds[(uint32_t)(dmi + e2 * (ro + 1))] = (uint8_t)(pay >> 8);   // (a plain multiply: mad24 on ro + 1 costs two shifts to sign-extend it)
-            ro += e1 + e2;
+            const vw::ldsp pa = vw::lds_sel(r.lds, e1, ro, dmi);
+            if (h & 1) {
+                vw::lds_st8<0, true>(pa, w);
+                vw::lds_st8<1, true>(pa, wh);
+            } else {
+                vw::lds_st8<0, false>(pa, w);
+                vw::lds_st8<1, false>(pa, wh);
+            }
+            ro += 2 * e1;
         }
         }
 #endif

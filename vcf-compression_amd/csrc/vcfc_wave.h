@@ -161,6 +161,10 @@ __device__ __forceinline__ ldsp lds_sel(uint8_t *lds, int32_t f, int32_t x, int3
     __asm__("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(a) : "v"(f), "v"(x), "v"(b));
     return ldsp{a};
 }
+// one unaligned ds_write_b32 (an escape's 0xE1 and its three bytes, esc8)
+__device__ __forceinline__ void lds_st32(ldsp p, uint32_t v) {
+    __asm__ volatile("ds_write_b32 %0, %1" ::"v"(p.a), "v"(v) : "memory");
+}
 template <int OFF, bool HI>
 __device__ __forceinline__ void lds_st8(ldsp p, uint32_t v) {
     if (HI) __asm__ volatile("ds_write_b8_d16_hi %0, %1 offset:%2" ::"v"(p.a), "v"(v), "i"(OFF) : "memory");
