@@ -34,6 +34,11 @@
 #define VCFCD_NO_ERROR (~0ull)
 // rec_size value of a row the fast kernel leaves to k_encode_var
 #define VCFCD_RETRY 0xFFFFFFFFu
+// ... or, when k_encode_fast parsed a clean prefix inside the line's first
+// 1 KiB and only the genotype tokens were of another shape, VCFCD_RETRY_GT |
+// the first sample's offset (< VCFCD_GT0_NONE): k_encode_var skips the parse
+#define VCFCD_RETRY_GT 0xC0000000u
+#define VCFCD_GT0_NONE 0x3FFFFFFFu
 // rec_size flag of a deferred row: k_encode_var only sized it (every chunk an
 // escape chunk), k_encode_defer writes its record straight to out after the
 // size scan (the size is the low 31 bits)

@@ -284,8 +284,34 @@ struct FastState {
     uint32_t esc;       // the last genotype chunk held an escape: test the escape shape first
 };
 
+// Prefix bytes of 1 KiB chunk c -> ring[8 + x]: realign the lane's bytes to
+// ring dwords (ring position of lane byte i is bo + i + 8 - lead); bytes
+// outside [0, x9) land below 8 (header, rewritten) or at >= wpos (free,
+// overwritten later) -- written before this chunk's tokens.
+__device__ __forceinline__ void prefix_to_ring(const Chunk &cur, uint32_t c, uint32_t lead, Ring &r) {
+    const uint32_t l = vw::lane_id();
+    const uint32_t bo = c * CHUNK + BPL * l;
+    const uint32_t e = (8u - lead) & 3u;
+    const int32_t dq = (int32_t)(8u - lead) - (int32_t)e;
+    const uint32_t pw = vw::shr1(cur.w(TPL - 1), 0u);
+    const uint32_t sh = (4u - e) & 3u;
+    uint32_t *rd = reinterpret_cast<uint32_t *>(r.lds);
+    const uint32_t base = (uint32_t)((int32_t)bo + dq);
+    // dword k holds ring bytes [base + 4k, +4) = lane bytes [4k - e, 4k - e + 4)
+#pragma unroll
+    for (int k = 0; k <= (int)TPL; k++) {
+        const uint32_t lo = k == 0 ? pw : cur.w(k - 1);
+        const uint32_t hi = cur.w(k);   // w(TPL) = y
+        const uint32_t o = e == 0 ? cur.w(k) : vw::alignbyte(hi, lo, sh);
+        const bool wr = e == 0 ? (k < (int)TPL) : (k == (int)TPL ? l == 63 : (k != 0 || l != 0));
+        if (wr) rd[((base + 4u * k) & RMASK) >> 2] = o;   // lane 0's k=0 dword: written by lane 63 before
+    }
+}
+
 // Prefix phase for chunk c: 0 = no sample yet, 1 = first sample starts in
-// this chunk (its tokens still to do), 2 = not the fast shape.  VAR (the
+// this chunk (its tokens still to do), 2 = not the fast shape, 3 (fast
+// kernel) = a clean prefix whose genotype tokens are not all 3 bytes long:
+// f.gt0 is the first sample's offset, handed to k_encode_var.  VAR (the
 // variable-token kernel): the genotype region need only hold odd-length
 // tokens (f.T = its 2-byte half-slots instead of its tokens).
 template <bool VAR>
@@ -345,28 +371,12 @@ __device__ __forceinline__ int fast_prefix_step(const Chunk &cur, uint32_t c, ui
         const uint32_t ge = rel >= 0 ? FULLM : (-rel >= (int32_t)BPL ? 0u : (FULLM & ~((1u << -rel) - 1u)));
         odd = ((m ^ ((0x1111u << ph) & FULLM)) & ge & vm) != 0;
     }
-    if (vw::ballot((et & below) != 0 || (lf & vm) != 0 || odd)) return 2;
-    // prefix bytes -> ring[8 + x]: realign the lane's bytes to ring dwords
-    // (ring position of lane byte i is bo + i + 8 - lead); bytes outside
-    // [0, x9) land below 8 (header, rewritten) or at >= wpos (free,
-    // overwritten later) -- written before this chunk's tokens.
-    {
-        const uint32_t e = (8u - lead) & 3u;
-        const int32_t dq = (int32_t)(8u - lead) - (int32_t)e;
-        const uint32_t pw = vw::shr1(cur.w(TPL - 1), 0u);
-        const uint32_t sh = (4u - e) & 3u;
-        uint32_t *rd = reinterpret_cast<uint32_t *>(r.lds);
-        const uint32_t base = (uint32_t)((int32_t)bo + dq);
-        // dword k holds ring bytes [base + 4k, +4) = lane bytes [4k - e, 4k - e + 4)
-#pragma unroll
-        for (int k = 0; k <= (int)TPL; k++) {
-            const uint32_t lo = k == 0 ? pw : cur.w(k - 1);
-            const uint32_t hi = cur.w(k);   // w(TPL) = y
-            const uint32_t o = e == 0 ? cur.w(k) : vw::alignbyte(hi, lo, sh);
-            const bool wr = e == 0 ? (k < (int)TPL) : (k == (int)TPL ? l == 63 : (k != 0 || l != 0));
-            if (wr) rd[((base + 4u * k) & RMASK) >> 2] = o;   // lane 0's k=0 dword: written by lane 63 before
-        }
+    if (vw::ballot((et & below) != 0 || (lf & vm) != 0)) return 2;
+    if (!VAR && vw::ballot(odd)) {   // a clean prefix, tokens of another length: k_encode_var's row, gt0 known
+        f.gt0 = (int32_t)x9;
+        return 3;
     }
+    prefix_to_ring(cur, c, lead, r);
     f.nf += vw::readlane(inc, 63);
     if (!hb) {
         const int32_t upto = (int32_t)((c + 1) * CHUNK) - (int32_t)lead;
@@ -877,11 +887,16 @@ __device__ __forceinline__ bool gt_step8(const Chunk8 &cur, uint32_t C, FastStat
     return false;   // tokens of another length or empty fields: the caller runs gt_general on this chunk
 }
 
-__device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring &r, uint32_t *rec_bytes) {
+// false: not the fast shape; *gt0_hint = the first sample's offset when the
+// prefix (in the first 1 KiB) was clean and only the tokens were of another
+// shape (k_encode_var then skips the prefix parse), else ~0
+__device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring &r, uint32_t *rec_bytes,
+                            uint32_t *gt0_hint) {
     const uint32_t l = vw::lane_id();
     const uint32_t lead = (uint32_t)(reinterpret_cast<uintptr_t>(line) & 15);
     const uint8_t *A = line - lead;
     const uint32_t span = lead + len;
+    *gt0_hint = ~0u;
     if (len == 0) return false;
     const uint32_t nch = (span + CHUNK - 1) / CHUNK;
     const uint32_t lo16 = BPL * l;
@@ -903,7 +918,8 @@ __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring
         if (c >= nch) return false;   // < 10 fields
         b = load_chunk(rsA, c, lo16);
     }
-    if (st == 2) return false;
+    if (st == 3 && c == 0) *gt0_hint = (uint32_t)f.gt0;
+    if (st >= 2) return false;
 
     // genotype phase: runs of clean chunks, three chunks in flight, broken
     // by the (rare) chunks that need the general step.  The inner loop has a
@@ -1404,9 +1420,13 @@ __device__ __forceinline__ bool var_chunks(Chunk8v &x, Chunk8v &y, Chunk8v &z, u
 // follow).  (A copy of the chunk loop per fate, so that staged rows would
 // run the default kernel's code, spilled 156 bytes per lane.)  *deferred:
 // the row was only sized (RING_SIZE), the ring's bytes never left it.
+// gt0_hint (< VCFCD_GT0_NONE): the first sample's offset, found by
+// k_encode_fast in a clean prefix inside the line's first 1 KiB -- the
+// prefix is then copied without its parse, and the genotype chunks load
+// beside it instead of after it (one memory latency fewer per row).
 template <int VM>
 __device__ bool encode_var(const uint8_t *__restrict__ line, uint32_t len, Ring &r, uint32_t *rec_bytes, bool nlc,
-                           bool *nlhit, bool *deferred) {
+                           bool *nlhit, bool *deferred, uint32_t gt0_hint) {
     const uint32_t l = vw::lane_id();
     const uint32_t lead = (uint32_t)(reinterpret_cast<uintptr_t>(line) & 15);
     const uint8_t *A = line - lead;
@@ -1421,21 +1441,32 @@ __device__ bool encode_var(const uint8_t *__restrict__ line, uint32_t len, Ring 
     *deferred = false;
     r.wpos = 8;
     r.fpos = 0;
-    // prefix phase: as encode_fast
     const vw::brsrc rsA = vw::make_rsrc(A, (span + 3u) & ~3u);
     uint32_t c = 0;
     Chunk b = load_chunk(rsA, 0, lo16);
-    int st;
-    for (;;) {
-        st = (int)vw::readfirst((uint32_t)fast_prefix_step<true>(look_ahead(b), c, lead, len, f, r));
-        if (st != 0) break;
-        c = vw::readfirst(c + 1);
-        if (c >= nch) return false;
-        b = load_chunk(rsA, c, lo16);
+    const bool known = gt0_hint < VCFCD_GT0_NONE && gt0_hint < len;
+    if (!known) {
+        // prefix phase: as encode_fast
+        int st;
+        for (;;) {
+            st = (int)vw::readfirst((uint32_t)fast_prefix_step<true>(look_ahead(b), c, lead, len, f, r));
+            if (st != 0) break;
+            c = vw::readfirst(c + 1);
+            if (c >= nch) return false;
+            b = load_chunk(rsA, c, lo16);
+        }
+        if (st == 2) return false;
+        ring_flush_var<VM != VAR_PLAIN>(r);   // < 512 bytes pending before the first chunk
+    } else {
+        // (fast_prefix_step<true>'s genotype-region checks on the known gt0)
+        f.gt0 = (int32_t)gt0_hint;
+        f.phi = (lead + gt0_hint) & 3u;
+        const uint32_t glen = len - gt0_hint;
+        if (((glen + 1) & 1u) != 0) return false;
+        f.T = (glen + 1) >> 1;
+        if (f.T >= (1u << 23) - 2 * MOD_BIAS) return false;
     }
-    if (st == 2) return false;
     f.carryT = 1;   // token 0 starts the genotype region
-    ring_flush_var<VM != VAR_PLAIN>(r);   // < 512 bytes pending before the first chunk
     const uint32_t phi = f.phi, NH = f.T;
     const vw::brsrc rsG = vw::make_rsrc(line + f.gt0 - phi, (phi + len - (uint32_t)f.gt0 + 3u) & ~3u);
     const uint32_t ncG = (NH + HPC - 1) / HPC;
@@ -1445,6 +1476,11 @@ __device__ bool encode_var(const uint8_t *__restrict__ line, uint32_t len, Ring 
     Chunk8v b1 = load_chunk8v(rsG, 1, lo32);
     Chunk8v b2 = load_chunk8v(rsG, 2, lo32);
     vw::pin_loads();
+    if (known) {   // the prefix bytes (chunk 0, loaded first) while the genotype chunks are in flight
+        prefix_to_ring(look_ahead(b), 0, lead, r);
+        r.wpos = 8u + gt0_hint;
+        ring_flush_var<VM != VAR_PLAIN>(r);
+    }
     const bool ok = var_chunks<VM>(b0, b1, b2, 0, ncG, rsG, lo32, f, r);
     if (!ok) {
         *nlhit = f.nlhit != 0;
@@ -1747,14 +1783,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 6))) voi
     VCFC_DIAG_ROW_BEGIN();
     Ring r;
     if (!row_setup(a, row, lds + wave * RING_STRIDE, r)) return;
-    uint32_t bytes = 0;
-    const bool ok = encode_fast(a.buf + a.line_off[row], a.line_len[row], r, &bytes);
+    uint32_t bytes = 0, gt0 = ~0u;
+    const bool ok = encode_fast(a.buf + a.line_off[row], a.line_len[row], r, &bytes, &gt0);
     VCFC_DIAG_ROW_END(a, row);
     if (vw::lane_id() == 0) {
         // not the fast shape: k_encode_var's wave for this row takes it
         // (a flag per row, no shared queue: 750k rows appending to one
-        // counter serialise at the memory side, ~8 ms on the law-2 rows)
-        a.rec_size[row] = ok ? bytes : VCFCD_RETRY;
+        // counter serialise at the memory side, ~8 ms on the law-2 rows),
+        // with the first sample's offset when the prefix was parsed clean
+        a.rec_size[row] = ok ? bytes : (gt0 < VCFCD_GT0_NONE ? (VCFCD_RETRY_GT | gt0) : VCFCD_RETRY);
     }
 }
 
@@ -1796,7 +1833,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
     const uint32_t wave = vw::readfirst(threadIdx.x >> 6);
     const uint32_t l = vw::lane_id();
     const uint64_t row0 = row_lo + ((uint64_t)blockIdx.x * K1_WAVES + wave) * VAR_ROWS;
-    const bool flagged = l < VAR_ROWS && row0 + l < row_hi && a.rec_size[row0 + l] == VCFCD_RETRY;
+    // a flagged row: VCFCD_RETRY, or VCFCD_RETRY_GT | the first sample's offset
+    const uint32_t rs = l < VAR_ROWS && row0 + l < row_hi ? a.rec_size[row0 + l] : 0u;
+    const bool flagged = (rs & VCFCD_RETRY_GT) == VCFCD_RETRY_GT;
     uint64_t todo = vw::ballot(flagged);
     uint32_t dmask = 0;   // rows deferred (bit: row - row0)
     while (todo) {
@@ -1811,8 +1850,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
         // the device file), the general path scans the row first.
         uint32_t bytes = 0;
         bool nlhit = false, deferred = false;
-        const bool var_ok =
-            encode_var<VM>(a.buf + a.line_off[row], a.line_len[row], r, &bytes, a.nl_check, &nlhit, &deferred);
+        const uint32_t gt0 = vw::readlane(rs, (uint32_t)(row - row0)) & VCFCD_GT0_NONE;
+        const bool var_ok = encode_var<VM>(a.buf + a.line_off[row], a.line_len[row], r, &bytes, a.nl_check, &nlhit,
+                                           &deferred, gt0);
         if (!var_ok && !nlhit && a.nl_check) nlhit = row_has_nl(a.buf + a.line_off[row], a.line_len[row]);
         if (nlhit) {
             if (l == 0) {
@@ -1871,7 +1911,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
         uint32_t bytes = 0;
         bool nlhit = false, deferred = false;
         const bool ok =
-            encode_var<VAR_DIRECT>(a.buf + a.line_off[row], a.line_len[row], r, &bytes, false, &nlhit, &deferred);
+            encode_var<VAR_DIRECT>(a.buf + a.line_off[row], a.line_len[row], r, &bytes, false, &nlhit, &deferred,
+                                   VCFCD_GT0_NONE);
         if (l == 0 && (!ok || bytes != size))   // (cannot happen: the same code sized it)
             atomicMin((unsigned long long *)a.err, (unsigned long long)((row << 8) | VCFCD_E_INTERNAL));
     }
