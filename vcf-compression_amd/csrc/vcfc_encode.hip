@@ -1456,7 +1456,6 @@ __device__ bool encode_var(const uint8_t *__restrict__ line, uint32_t len, Ring 
             b = load_chunk(rsA, c, lo16);
         }
         if (st == 2) return false;
-        ring_flush_var<VM != VAR_PLAIN>(r);   // < 512 bytes pending before the first chunk
     } else {
         // (fast_prefix_step<true>'s genotype-region checks on the known gt0)
         f.gt0 = (int32_t)gt0_hint;
@@ -1476,11 +1475,15 @@ __device__ bool encode_var(const uint8_t *__restrict__ line, uint32_t len, Ring 
     Chunk8v b1 = load_chunk8v(rsG, 1, lo32);
     Chunk8v b2 = load_chunk8v(rsG, 2, lo32);
     vw::pin_loads();
-    if (known) {   // the prefix bytes (chunk 0, loaded first) while the genotype chunks are in flight
-        prefix_to_ring(look_ahead(b), 0, lead, r);
-        r.wpos = 8u + gt0_hint;
-        ring_flush_var<VM != VAR_PLAIN>(r);
-    }
+    // The prefix bytes while the genotype chunks are in flight: with gt0
+    // known, chunk 0 (loaded first) is copied here; without, the prefix
+    // step wrote them and this rewrites chunk c's the same (unconditional,
+    // so the loop is entered from one path: a branch here made hipcc's
+    // counted vmcnt waits in the chunk loop fall back to vmcnt(0) and the
+    // variable-token rows 9-12 % slower)
+    prefix_to_ring(look_ahead(b), c, lead, r);
+    r.wpos = 8u + (uint32_t)f.gt0;
+    ring_flush_var<VM != VAR_PLAIN>(r);   // < 512 bytes pending before the first chunk
     const bool ok = var_chunks<VM>(b0, b1, b2, 0, ncG, rsG, lo32, f, r);
     if (!ok) {
         *nlhit = f.nlhit != 0;
