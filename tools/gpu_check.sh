@@ -66,6 +66,10 @@ for s in $STEPS; do
          python3 tools/pmc_encode_json.py "$O/pmcenc_l1_FETCH_SIZE" "$O/pmcenc_l1_WRITE_SIZE" "chr22-shaped/2504x1000000" "$O/pmc_k_encode.json" "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes (tools/gpu_check.sh pmcenc, run $TAG)" > /dev/null &&
          python3 tools/pmc_encode_json.py "$O/pmcenc_l0_FETCH_SIZE" "$O/pmcenc_l0_WRITE_SIZE" "random_vcf-law/2504x1000000" "$O/pmc_k_encode_law0.json" "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes (tools/gpu_check.sh pmcenc, run $TAG)" > /dev/null &&
          python3 tools/pmc_encode_json.py "$O/pmcenc_l2_FETCH_SIZE" "$O/pmcenc_l2_WRITE_SIZE" "general-shapes (chrX haploid/GT:DP:GQ/missing)/2504x1000000" "$O/pmc_k_encode_law2.json" "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes (tools/gpu_check.sh pmcenc, run $TAG)" > /dev/null || { echo "pmc json failed"; exit 1; } ;;
+    pmcinstall) # the PMC summaries this run just made become the ones bench.py reads (same-box lines)
+         for f in "$O"/pmc_k_encode*.json "$O"/pmc_k_query.json "$O"/pmc_devfile_l*.json; do [ -f "$f" ] && cp "$f" profiles/; done; ls -l profiles/pmc_*.json ;;
+    profbench) # the default bench command itself under rocprofv3: the JSON line and the kernel stats of one process
+         (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/profbench" -o run -- python3 "$R/bench.py" > "$O/bench_under_prof.json" 2> "$O/profbench.log") || { echo "profbench failed rc=$?"; tail -30 "$O/profbench.log"; exit 1; } ; cat "$O/bench_under_prof.json" ;;
     benchdev) timeout -k 10 300 python bench.py --mode devfile > "$O/bench_devfile.json" 2> "$O/bench_devfile.err" || { echo "benchdev failed"; tail -30 "$O/bench_devfile.err"; exit 1; } ; cat "$O/bench_devfile.json" ;;
     pmcdev) # HBM bytes per devfile step (every kernel of one call), law ${LAW:-1} -> pmc_devfile_l<law>.json
          for P in FETCH_SIZE WRITE_SIZE; do
