@@ -79,8 +79,11 @@ int vcfc_ctx_set_trace(vcfc_ctx *ctx, unsigned flags);
  * ~1.1x their lines) and that spans more than one 2 KiB chunk is only sized
  * by the first pass and encoded straight into the output once the record
  * offsets are known, instead of staged and copied.  The choice is made per
- * row by the kernel from the row's bytes; a batch without such rows pays
- * one empty launch.  Output identical either way. */
+ * row by the kernel from the row's bytes; once two rows agree on their token
+ * count, a deferred row's size is predicted from its first chunk and checked
+ * when it is written (a wrong guess lays the batch out again: three gated
+ * launches that return at once otherwise).  Output identical either way
+ * (DESIGN.md section 3). */
 int vcfc_ctx_set_deferred_records(vcfc_ctx *ctx, int on);
 
 /* ---- one line: replaces compress_data_line (src/compress.hpp:20-23) --------
@@ -123,8 +126,10 @@ int vcfc_encode_rows_device(const uint8_t *d_buf, const uint64_t *d_line_off,
                             void *d_ws, uint64_t ws_bytes, uint64_t *d_err, void *stream);
 
 /* Rows the last vcfc_encode_rows_device call on workspace d_ws (sized for
- * n, total_line_bytes) deferred (see vcfc_ctx_set_deferred_records); waits
- * for `stream`. */
+ * n, total_line_bytes) deferred and wrote straight into the output (see
+ * vcfc_ctx_set_deferred_records; a row whose predicted size led there but
+ * whose later bytes sent it to the general path is not counted); waits for
+ * `stream`. */
 int vcfc_encode_deferred_rows(const void *d_ws, uint64_t n_rows, uint64_t total_line_bytes, void *stream,
                               uint64_t *rows);
 

@@ -25,6 +25,7 @@ def lib():
                                       ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
                                       ctypes.POINTER(ctypes.c_uint32)]
         L.emu_last_deferred.restype = ctypes.c_uint32
+        L.emu_last_mispredict.restype = ctypes.c_uint32
         L.emu_sparse_plan.argtypes = [vp, vp, ctypes.c_uint64, ctypes.c_uint64, vp, vp, vp]
         L.emu_decompress.argtypes = [ctypes.c_char_p, ctypes.c_uint64, vp, ctypes.c_uint64,
                                      ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint64]
@@ -78,6 +79,13 @@ def last_deferred():
     """Rows the last emu_encode call deferred (sized by k_encode_var, written
     to out by k_encode_defer)."""
     return int(lib().emu_last_deferred())
+
+
+def last_mispredict():
+    """Whether the last emu_encode call's first deferred pass found a
+    predicted record size wrong (the size scan, compaction and deferred
+    writes then ran again on exact sizes)."""
+    return int(lib().emu_last_mispredict())
 
 
 def emu_encode(buf, line_off, line_len, cap=None):

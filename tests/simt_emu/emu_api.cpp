@@ -26,8 +26,12 @@ static uint32_t emu_defer() {
     const char *e = getenv("EMU_DEFER");
     return e ? (atoi(e) != 0 ? 1u : 0u) : (uint32_t)VCFC_DEFER_DEFAULT;
 }
-// rows the last emu_encode_rows call deferred (VCFCD_DEFER: written by k_encode_defer)
+static uint32_t g_last_mispredict = 0;
+// rows the last emu_encode_rows call deferred (VCFCD_DEFER: written by
+// k_encode_defer; predicted rows taken by the general path after all not counted)
 extern "C" uint32_t emu_last_deferred() { return g_last_deferred; }
+// whether its first deferred pass found a predicted size wrong (the layout ran again)
+extern "C" uint32_t emu_last_mispredict() { return g_last_mispredict; }
 
 extern "C" int emu_encode_rows(const uint8_t *buf, const uint64_t *line_off, const uint32_t *line_len,
                                uint64_t n, uint8_t *out, uint64_t out_cap, uint64_t *rec_off,
@@ -44,11 +48,13 @@ extern "C" int emu_encode_rows(const uint8_t *buf, const uint64_t *line_off, con
     a.line_bytes_hint = getenv("EMU_WIDE_COMPACT") ? (~0ull >> 1) : total;   // (tests force the 64-lane compaction)
     a.err = (uint64_t *)(ws + L.err);
     a.defer_records = emu_defer();   // (tests: deferred records; the product default unless EMU_DEFER is set)
+    a.nl_check = getenv("EMU_NL_CHECK") ? 1u : 0u;   // (tests: rows from a guessed line index)
     emu::g.switches = 0;
     int st = (int)vcfc_encode_device(a, nullptr);
     *err_word = *a.err;
     if (retries) *retries = *a.retry_count;   // rows that took the general path
-    g_last_deferred = *a.defer_count;
+    g_last_deferred = *a.defer_count - *a.defer_fallback;
+    g_last_mispredict = *a.mispredict;
     if (switches) *switches = emu::g.switches;
     free(ws);
     return st;

@@ -64,6 +64,7 @@ inline void __builtin_amdgcn_s_sleep(int) {}
 template <class T> inline T atomicMin(T *p, T v) { T o = *p; if (v < o) *p = v; return o; }
 template <class T> inline T atomicMax(T *p, T v) { T o = *p; if (v > o) *p = v; return o; }
 template <class T> inline T atomicOr(T *p, T v) { T o = *p; *p = o | v; return o; }
+template <class T> inline T atomicExch(T *p, T v) { T o = *p; *p = v; return o; }
 
 inline emu::dim3v emu_dim(dim3 d) { emu::dim3v r; r.x = d.x; r.y = d.y; r.z = d.z; return r; }
 #define hipLaunchKernelGGL(K, G, B, SHM, STREAM, ...) \

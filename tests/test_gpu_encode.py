@@ -231,6 +231,36 @@ def test_variable_token_rows(ctx, seed):
     assert ctx.compress_buffer(data) == want
 
 
+@pytest.mark.parametrize("odd", ["none", "ntok", "mixed_later", "general_later"])
+def test_predicted_deferred_records(ctx, odd):
+    """GT:DP:GQ rows of one sample count: after two rows agree on their token
+    count, k_encode_var sizes the later deferred rows from their first chunk
+    (all escapes predicted) and k_encode_defer's first pass checks each.
+    With one odd row among them -- a sample more, plain tokens after a
+    first chunk of 1-byte escapes, two even-length tokens after the first
+    chunk (the general path) -- the check fails and the gated size scan,
+    compaction and deferred pass lay the batch out again: byte-exact
+    against the oracle through compress_buffer either way."""
+    import random
+    import test_kernel_emu as T
+    rnd = random.Random(hash(odd) & 0xFFFF)
+    lines = [T._gdg(rnd, 700) for _ in range(300)]
+    for i in range(17, 300, 61):
+        if odd == "ntok":
+            lines[i] = T._gdg(rnd, 701)
+        elif odd == "mixed_later":
+            lines[i] = T.PFX_V + b"\t".join([rnd.choice([b"0", b"1", b"."]) for _ in range(1100)] +
+                                            [rnd.choice([b"0|0", b"0|1"]) for _ in range(400)])
+        elif odd == "general_later":
+            lines[i] = T.PFX_V + b"\t".join([b"0|1:33:99"] * 300 + [b"0|1:3:99"] * 2 + [b"0|1:33:99"] * 398)
+    hdr = (b"##fileformat=VCFv4.2\n#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\t" +
+           b"\t".join(b"S%d" % j for j in range(700)) + b"\n")
+    data = hdr + b"\n".join(lines) + b"\n"
+    st, want, _ = G.oracle_compress(data)
+    assert st == 0
+    assert ctx.compress_buffer(data) == want
+
+
 def test_encode_captured_in_hip_graph(torch, vcfc):
     """vcfc_encode_rows_device enqueues its whole pipeline (memsets, the two
     look-back scans, k_encode_fast, k_encode_var, k_compact_out) with no host

@@ -432,6 +432,117 @@ def test_deferred_records(monkeypatch):
     assert out2[:int(ro[cut])] == out[:int(ro[cut])]
 
 
+def test_deferred_runs_share_tiles(monkeypatch):
+    """Output tiles (4 KiB) whose bytes all belong to deferred records are
+    skipped by the compaction, including a tile a deferred record ends in
+    when the next records up to the tile end are deferred too, or the batch
+    ends there; a tile that reaches a staged record is compacted.  Runs of
+    GT:DP:GQ rows (records of 2.5-11 KiB, so a tile meets up to three of
+    them) beside short staged rows and at the batch end, byte-exact."""
+    monkeypatch.setenv("EMU_DEFER", "1")
+    rnd = random.Random(77)
+
+    def gdg(S):
+        return PFX_V + b"\t".join(b"%d|%d:%d:%d" % (rnd.randint(0, 1), rnd.randint(0, 1), rnd.randint(10, 99),
+                                                 rnd.randint(10, 99)) for _ in range(S))
+    lines, expect_defer = [], 0
+    for run_len in (5, 1, 3, 7):
+        for _ in range(run_len):
+            lines.append(gdg(rnd.choice([260, 300, 333, 410, 700, 1100])))
+            expect_defer += 1
+        lines.append(PFX_V + b"\t".join(rnd.choice([b"0|0", b"0|1"]) for _ in range(rnd.randint(1, 40))))
+    for _ in range(4):   # the batch ends inside a deferred run
+        lines.append(gdg(rnd.choice([260, 500, 900])))
+        expect_defer += 1
+    want = [G.oracle_encode_line(x)[1] for x in lines]
+    for lead in (0, 7):
+        st, out, ro, err = run(lines, lead)
+        assert err == (1 << 64) - 1 and E.last_deferred() == expect_defer
+        assert out == b"".join(want), lead
+
+
+def _gdg(rnd, S):
+    return PFX_V + b"\t".join(b"%d|%d:%d:%d" % (rnd.randint(0, 1), rnd.randint(0, 1), rnd.randint(10, 99),
+                                             rnd.randint(10, 99)) for _ in range(S))
+
+
+def _encode_both(lines, monkeypatch, cap=None):
+    """(deferral off, deferral on) results of the emulated encode."""
+    buf = bytearray()
+    offs, lens = [], []
+    for ln in lines:
+        offs.append(len(buf))
+        lens.append(len(ln))
+        buf += ln + b"\n"
+    args = (bytes(buf), np.array(offs, np.uint64), np.array(lens, np.uint32))
+    monkeypatch.setenv("EMU_DEFER", "0")
+    off = E.emu_encode(*args, cap=cap)
+    monkeypatch.setenv("EMU_DEFER", "1")
+    on = E.emu_encode(*args, cap=cap)
+    return off, on
+
+
+def test_predicted_deferred_records(monkeypatch):
+    """Once two rows of a wave agree on their token count, k_encode_var
+    sizes a later row deferred on its first chunk without reading the rest
+    (all escapes predicted: len + 9 + tokens); k_encode_defer's first pass
+    encodes it in full and checks.  Correct predictions: no second layout
+    pass.  Byte-exact either way against the oracle and against the encode
+    without deferral."""
+    rnd = random.Random(5)
+    lines = [_gdg(rnd, 700) for _ in range(40)]
+    want = b"".join(G.oracle_encode_line(x)[1] for x in lines)
+    (st0, out0, ro0, err0), (st1, out1, ro1, err1) = _encode_both(lines, monkeypatch)
+    assert err0 == err1 == (1 << 64) - 1
+    assert out0 == out1 == want and list(ro0) == list(ro1)
+    assert E.last_deferred() == 40 and E.last_mispredict() == 0
+
+
+@pytest.mark.parametrize("case", ["ntok", "mixed_later", "general_later", "cap", "newline"])
+def test_mispredicted_deferred_records(case, monkeypatch):
+    """Predictions that are wrong: another token count (a row with one
+    sample more), plain tokens after a first chunk of 1-byte escapes (the
+    record is not all escapes),
+    an even-length token after the first chunk (the row leaves the
+    variable-token path: general path, staged, not counted as deferred),
+    out_cap cutting the batch (the held-back out_cap report against the
+    exact one), a '\\n' inside a predicted row of a guessed line index.  The
+    first deferred pass flags it and the layout runs again on exact sizes:
+    the same bytes and offsets as without deferral, the same error word."""
+    rnd = random.Random(hash(case) & 0xFFFF)
+    lines = [_gdg(rnd, 700) for _ in range(12)]
+    cap = None
+    if case == "ntok":
+        lines[6] = _gdg(rnd, 701)
+    elif case == "mixed_later":
+        # (1-byte escapes in chunk 0: the mixed step takes 1- and 3-byte tokens)
+        lines[6] = PFX_V + b"\t".join([rnd.choice([b"0", b"1", b"."]) for _ in range(1100)] +
+                                      [rnd.choice([b"0|0", b"0|1"]) for _ in range(400)])
+    elif case == "general_later":
+        # (two: an odd count of even-length tokens fails the region's parity check up front)
+        lines[6] = PFX_V + b"\t".join([b"0|1:33:99"] * 300 + [b"0|1:3:99"] * 2 + [b"0|1:33:99"] * 398)
+    elif case == "newline":
+        monkeypatch.setenv("EMU_NL_CHECK", "1")
+        lines[6] = PFX_V + b"\t".join([b"0|1:33:99"] * 300 + [b"0|1:33\n99"] + [b"0|1:33:99"] * 399)
+    (st0, out0, ro0, err0), _ = _encode_both(lines, monkeypatch)
+    if case == "cap":
+        cap = int(ro0[9]) + 50
+        (st0, out0, ro0, err0), (st1, out1, ro1, err1) = _encode_both(lines, monkeypatch, cap)
+        assert err0 == err1 == (9 << 8) | 4
+        assert out1[:int(ro0[9])] == out0[:int(ro0[9])]
+        return
+    (st0, out0, ro0, err0), (st1, out1, ro1, err1) = _encode_both(lines, monkeypatch)
+    assert E.last_mispredict() == 1
+    assert err1 == err0
+    if case == "newline":
+        assert err0 == (6 << 8) | 9
+        return
+    assert err0 == (1 << 64) - 1
+    assert out1 == out0 == b"".join(G.oracle_encode_line(x)[1] for x in lines)
+    assert list(ro1) == list(ro0)
+    assert E.last_deferred() == (11 if case == "general_later" else 12)
+
+
 @pytest.mark.parametrize("defer", ["0", "1"])
 def test_escape_rows_ending_on_a_chunk_end(defer, monkeypatch):
     """rows whose genotype region is a whole number of 2 KiB

@@ -9,6 +9,6 @@ for round in 1 2 3; do
   for lib in "$@"; do
     n=$(basename $(dirname "$lib"))
     VCFC_LIB="$R/$lib" timeout -k 10 300 python bench.py --no-cpu-baseline --steps 30 ${AB_ARGS} > "$O/$n.$round.json" 2> "$O/$n.$round.err" || { echo "bench $lib failed"; tail -20 "$O/$n.$round.err"; exit 1; }
-    python -c "import json,sys; d=json.load(open(sys.argv[1])); r=d['roofline']; print(sys.argv[2], sys.argv[3], r['avg_launch_ms'], r.get('stages_ms', {}).get('k_compact', -1), d['ms_per_step'])" "$O/$n.$round.json" "$n" "$round" | tee -a "$O/ab.txt"
+    python -c "import json,sys; d=json.load(open(sys.argv[1])); r=d.get('roofline') or {}; print(sys.argv[2], sys.argv[3], r.get('avg_launch_ms', -1), (r.get('stages_ms') or {}).get('k_compact', -1), d['ms_per_step'])" "$O/$n.$round.json" "$n" "$round" | tee -a "$O/ab.txt"
   done
 done

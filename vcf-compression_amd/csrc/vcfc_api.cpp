@@ -342,13 +342,14 @@ int vcfc_encode_deferred_rows(const void *d_ws, uint64_t n, uint64_t total_line_
     *rows = 0;
     if (n == 0) return VCFC_OK;
     const VcfcWorkspaceLayout L = vcfc_encode_workspace_layout(n, total_line_bytes);
-    uint32_t v = 0;
+    uint32_t v = 0, fb = 0;   // deferred by k_encode_var, of which taken by the general path after all
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (hipMemcpyAsync(&v, static_cast<const uint8_t *>(d_ws) + vcfc_defer_count_offset(L), 4, hipMemcpyDeviceToHost,
-                       s) != hipSuccess ||
+    const uint8_t *ws = static_cast<const uint8_t *>(d_ws);
+    if (hipMemcpyAsync(&v, ws + vcfc_defer_count_offset(L), 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(&fb, ws + vcfc_defer_fallback_offset(L), 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         return VCFC_E_HIP;
-    *rows = v;
+    *rows = v - fb;
     return VCFC_OK;
 }
 

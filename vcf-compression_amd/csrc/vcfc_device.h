@@ -72,6 +72,14 @@ struct VcfcEncodeArgs {
     uint32_t *retry_count;     // rows that took the general path (emulator builds only, diag hooks)
     uint32_t *defer_count;     // deferred rows (VCFCD_DEFER), zeroed per encode with lb
     uint32_t *defer_list;      // their row indices (any order), n entries
+    // predicted deferred records (k_encode_var sizes an all-escape row from
+    // its first chunk and the token count two earlier rows agreed on;
+    // k_encode_defer's first pass checks every record against its size):
+    uint32_t *mispredict;      // nonzero: some record's size was wrong -- the size scan, compaction and
+                               // deferred writes run again on the exact sizes (gated launches)
+    uint32_t *defer_fallback;  // deferred rows that turned out not to be variable-token rows (general path)
+    uint64_t *nospace;         // the first size scan's out_cap report (row << 8 | VCFCD_E_NOSPACE),
+                               // merged into err unless the scan runs again
     uint8_t *lb;               // look-back scan state (tickets, tile flags; zeroed per encode)
     uint32_t *tile_first;      // per 4 KiB output tile: the row holding its first byte (compaction)
     uint8_t *prim;             // per-row primary staging: record bytes [0, prim_bytes) at prim + prim_bytes * row
@@ -106,8 +114,8 @@ __host__ __device__ inline uint32_t vcfc_prim_bytes(uint64_t n, uint64_t total_l
 }
 
 struct VcfcWorkspaceLayout {
-    uint64_t slot_off, rec_size, partials, err, lb, lb_bytes, retry_count, defer_count, defer_list, tile_first, prim,
-        slots, dbg, total;
+    uint64_t slot_off, rec_size, partials, err, lb, lb_bytes, retry_count, defer_count, mispredict, defer_fallback,
+        nospace, defer_list, tile_first, prim, slots, dbg, total;
     uint32_t prim_bytes;
 };
 
@@ -134,6 +142,9 @@ inline void vcfc_encode_args_workspace(VcfcEncodeArgs &a, uint8_t *ws, const Vcf
     a.retry_count = reinterpret_cast<uint32_t *>(ws + L.retry_count);
     a.defer_count = reinterpret_cast<uint32_t *>(ws + L.defer_count);
     a.defer_list = reinterpret_cast<uint32_t *>(ws + L.defer_list);
+    a.mispredict = reinterpret_cast<uint32_t *>(ws + L.mispredict);
+    a.defer_fallback = reinterpret_cast<uint32_t *>(ws + L.defer_fallback);
+    a.nospace = reinterpret_cast<uint64_t *>(ws + L.nospace);
     a.lb = ws + L.lb;
     a.tile_first = reinterpret_cast<uint32_t *>(ws + L.tile_first);
     a.prim = ws + L.prim;
@@ -146,6 +157,9 @@ inline void vcfc_encode_args_workspace(VcfcEncodeArgs &a, uint8_t *ws, const Vcf
 // Rows the last encode on this workspace deferred (the device word behind
 // VcfcEncodeArgs::defer_count; read by the caller after the stream is done).
 inline uint64_t vcfc_defer_count_offset(const VcfcWorkspaceLayout &L) { return L.defer_count; }
+// ... of which this many were written by the general path after all (a
+// predicted all-escape row whose later chunks had another shape)
+inline uint64_t vcfc_defer_fallback_offset(const VcfcWorkspaceLayout &L) { return L.defer_fallback; }
 
 // Enqueue the whole encode on `stream` (no host synchronisation, capturable).
 // If `ev` is non-null, ev[0..5] are recorded before the slot scan, after it,

@@ -1397,10 +1397,12 @@ __device__ __forceinline__ bool gt_var8(const Chunk8v &cur, uint32_t C, VarState
 // encode_fast).  false: not this shape.
 template <int VM>
 __device__ __forceinline__ bool var_chunks(Chunk8v &x, Chunk8v &y, Chunk8v &z, uint32_t C, uint32_t ncG,
-                                           vw::brsrc rsG, uint32_t lo32, VarState &f, Ring &r) {
+                                           vw::brsrc rsG, uint32_t lo32, VarState &f, Ring &r, bool may_predict) {
     bool ok = true;
     for (;;) {
         ok = vw::readfirst(gt_var8<VM>(x, C, f, r));
+        // a deferred row sized by prediction (VAR_DEFER): nothing after chunk 0
+        if (VM == VAR_DEFER && may_predict && f.sizeonly) break;
         x = load_chunk8v(rsG, C + 3, lo32);
         vw::pin_loads();
         if (ok && C + 1 < ncG) ok = vw::readfirst(gt_var8<VM>(y, C + 1, f, r));
@@ -1424,9 +1426,16 @@ __device__ __forceinline__ bool var_chunks(Chunk8v &x, Chunk8v &y, Chunk8v &z, u
 // k_encode_fast in a clean prefix inside the line's first 1 KiB -- the
 // prefix is then copied without its parse, and the genotype chunks load
 // beside it instead of after it (one memory latency fewer per row).
+// ntok_ref (VAR_DEFER; 0: none): the token count of the wave's earlier rows.
+// A row deferred on its first chunk is then not read further: its record is
+// predicted as all escapes -- 8 + len + 1 + ntok_ref bytes (each token gains
+// 0xE1, the line its '\n') -- and k_encode_defer's first pass, which encodes
+// it in full, checks the prediction (*predicted).  *ntok: the row's token
+// count (rows encoded in full).
 template <int VM>
-__device__ bool encode_var(const uint8_t *__restrict__ line, uint32_t len, Ring &r, uint32_t *rec_bytes, bool nlc,
-                           bool *nlhit, bool *deferred, uint32_t gt0_hint) {
+__device__ __forceinline__ bool encode_var(const uint8_t *__restrict__ line, uint32_t len, Ring &r, uint32_t *rec_bytes, bool nlc,
+                           bool *nlhit, bool *deferred, uint32_t gt0_hint, uint32_t ntok_ref = 0,
+                           bool *predicted = nullptr, uint32_t *ntok = nullptr) {
     const uint32_t l = vw::lane_id();
     const uint32_t lead = (uint32_t)(reinterpret_cast<uintptr_t>(line) & 15);
     const uint8_t *A = line - lead;
@@ -1439,6 +1448,7 @@ __device__ bool encode_var(const uint8_t *__restrict__ line, uint32_t len, Ring 
     f.nlc = nlc ? 1u : 0u; f.nlhit = 0; f.defer = 0; f.sizeonly = 0;
     *nlhit = false;
     *deferred = false;
+    if (predicted) *predicted = false;
     r.wpos = 8;
     r.fpos = 0;
     const vw::brsrc rsA = vw::make_rsrc(A, (span + 3u) & ~3u);
@@ -1484,10 +1494,20 @@ __device__ bool encode_var(const uint8_t *__restrict__ line, uint32_t len, Ring 
     prefix_to_ring(look_ahead(b), c, lead, r);
     r.wpos = 8u + (uint32_t)f.gt0;
     ring_flush_var<VM != VAR_PLAIN>(r);   // < 512 bytes pending before the first chunk
-    const bool ok = var_chunks<VM>(b0, b1, b2, 0, ncG, rsG, lo32, f, r);
+    // (an all-escape row of ntok tokens has len >= 2 ntok - 1: a larger
+    // count cannot be its own, and the predicted record stays within the
+    // per-row bound len + len / 2 + 16 that out_cap is sized by)
+    const bool may_predict = VM == VAR_DEFER && ntok_ref != 0 && ntok_ref <= (len + 1) / 2;
+    const bool ok = var_chunks<VM>(b0, b1, b2, 0, ncG, rsG, lo32, f, r, may_predict);
     if (!ok) {
         *nlhit = f.nlhit != 0;
         return false;
+    }
+    if (VM == VAR_DEFER && may_predict && f.sizeonly) {
+        *rec_bytes = len + 9u + ntok_ref;
+        *deferred = true;
+        *predicted = true;
+        return true;
     }
     // row end: pending chunk of the last run, then '\n'
     const uint32_t T = f.ntok, pcls = f.pcls, prs = f.prs;
@@ -1505,6 +1525,7 @@ __device__ bool encode_var(const uint8_t *__restrict__ line, uint32_t len, Ring 
     ring_finish<VM != VAR_PLAIN>(r, (uint32_t)f.gt0);
     *rec_bytes = r.wpos;
     *deferred = VM == VAR_DEFER && f.sizeonly != 0;
+    if (ntok) *ntok = f.ntok;
     return true;
 }
 
@@ -1532,7 +1553,7 @@ __device__ __forceinline__ uint32_t mask_range16(int32_t lo, int32_t hi) {   // 
     return hi > lo ? ((1u << hi) - 1u) ^ ((1u << lo) - 1u) : 0u;
 }
 
-__device__ uint32_t encode_general(const uint8_t *__restrict__ line, uint32_t len, Ring &r,
+__device__ __forceinline__ uint32_t encode_general(const uint8_t *__restrict__ line, uint32_t len, Ring &r,
                                    uint32_t *rec_bytes) {
     const uint32_t l = vw::lane_id();
     const uint32_t lead = (uint32_t)(reinterpret_cast<uintptr_t>(line) & 15);
@@ -1841,6 +1862,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
     const bool flagged = (rs & VCFCD_RETRY_GT) == VCFCD_RETRY_GT;
     uint64_t todo = vw::ballot(flagged);
     uint32_t dmask = 0;   // rows deferred (bit: row - row0)
+    // (VAR_DEFER) token counts of the wave's rows encoded in full: once two
+    // in a row agree, later deferred rows are predicted from it (a VCF's
+    // rows all hold one token per sample; a wrong guess costs the batch a
+    // second size scan, compaction and deferred pass, never wrong output)
+    uint32_t ntok_ref = 0, ntok_last = ~0u;
     while (todo) {
         const uint64_t row = row0 + (uint64_t)__builtin_ctzll(todo);
         todo &= todo - 1;
@@ -1851,11 +1877,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
         // variable-token path checks its genotype chunks as it reads them
         // (round 4; a separate scan of every flagged row cost law 2 ~1 ms on
         // the device file), the general path scans the row first.
-        uint32_t bytes = 0;
-        bool nlhit = false, deferred = false;
+        uint32_t bytes = 0, ntok = 0;
+        bool nlhit = false, deferred = false, predicted = false;
         const uint32_t gt0 = vw::readlane(rs, (uint32_t)(row - row0)) & VCFCD_GT0_NONE;
         const bool var_ok = encode_var<VM>(a.buf + a.line_off[row], a.line_len[row], r, &bytes, a.nl_check, &nlhit,
-                                           &deferred, gt0);
+                                           &deferred, gt0, ntok_ref, &predicted, &ntok);
+        if (VM == VAR_DEFER && var_ok && !predicted) {
+            ntok_ref = ntok == ntok_last ? ntok : 0u;
+            ntok_last = ntok;
+        }
         if (!var_ok && !nlhit && a.nl_check) nlhit = row_has_nl(a.buf + a.line_off[row], a.line_len[row]);
         if (nlhit) {
             if (l == 0) {
@@ -1887,22 +1917,53 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
     }
 }
 
+// scan shape (k_scan_lb / launch_scan below): items per thread, threads and items per block
+constexpr int SCAN_ITEMS = 16, SCAN_THREADS = 256, SCAN_TILE = SCAN_ITEMS * SCAN_THREADS;
+
 // Deferred rows (VCFCD_DEFER): after the size scan and the compaction, each
 // record is encoded again from its line straight into out at rec_off[row]
 // (RING_DIRECT; whole 16-byte blocks, the last few bytes one by one, so a
 // neighbour's bytes -- the compaction's -- are never touched).  A resident
 // grid strides over the deferred-row list; an empty list costs the launch.
+// PASS 1 also checks the sizes k_encode_var predicted (it reads each line in
+// full anyway): a record of another size, a line of another shape (then
+// encoded by the general path into its staging, no longer deferred), a line
+// holding '\n' (a.nl_check) or a record not certainly inside out_cap (its
+// offset may rest on predictions) sets a.mispredict.  The first wave to set
+// it rearms the size scan's look-back state, and the gated size scan,
+// compaction and PASS 2 then redo the layout on exact sizes; without a
+// misprediction they return at once (the scan merging the first scan's
+// out_cap report into err).
+template <int PASS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) void k_encode_defer(VcfcEncodeArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[K1_WAVES * RING_STRIDE];
+    if (PASS == 2 && *a.mispredict == 0) return;
     const uint32_t wave = vw::readfirst(threadIdx.x >> 6);
     const uint32_t l = vw::lane_id();
     const uint32_t cnt = vw::readfirst(*a.defer_count);
     const uint32_t G = gridDim.x * K1_WAVES;
+    auto miss = [&]() {
+        if (l == 0 && atomicExch(a.mispredict, 1u) == 0u) {
+            // the size scan's ticket and tile flags, for its second launch
+            const uint64_t nt = (a.n + SCAN_TILE - 1) / SCAN_TILE;
+            uint32_t *tickets = reinterpret_cast<uint32_t *>(a.lb);
+            uint64_t *flags_b = reinterpret_cast<uint64_t *>(a.lb + 16) + nt + 1;
+            tickets[1] = 0;
+            for (uint64_t i = 0; i <= nt; i++) flags_b[i] = 0;
+        }
+    };
     for (uint32_t q = blockIdx.x * K1_WAVES + wave; q < cnt; q += G) {
         const uint64_t row = vw::readfirst(a.defer_list[q]);
-        const uint32_t size = a.rec_size[row] & ~VCFCD_DEFER;
+        const uint32_t rsz = a.rec_size[row];
+        if (PASS == 2 && !(rsz & VCFCD_DEFER)) continue;   // (taken by the general path in pass 1)
+        const uint32_t size = rsz & ~VCFCD_DEFER;
+        const uint32_t len = a.line_len[row];
         const uint64_t o = a.rec_off[row];
-        if (o + size > a.out_cap) continue;   // (the size scan reported it)
+        if (PASS == 1 && o + (uint64_t)len + (len >> 1) + 16u > a.out_cap) {
+            miss();   // (pass 2, on exact offsets, or the exact size scan's out_cap report)
+            continue;
+        }
+        if (o + size > a.out_cap) continue;   // (pass 2: the size scan reported it)
         Ring r;
         r.lds = lds + wave * RING_STRIDE;
         r.prim = a.out + o;
@@ -1913,11 +1974,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
         r.mode = RING_DIRECT;
         uint32_t bytes = 0;
         bool nlhit = false, deferred = false;
-        const bool ok =
-            encode_var<VAR_DIRECT>(a.buf + a.line_off[row], a.line_len[row], r, &bytes, false, &nlhit, &deferred,
-                                   VCFCD_GT0_NONE);
-        if (l == 0 && (!ok || bytes != size))   // (cannot happen: the same code sized it)
-            atomicMin((unsigned long long *)a.err, (unsigned long long)((row << 8) | VCFCD_E_INTERNAL));
+        const bool ok = encode_var<VAR_DIRECT>(a.buf + a.line_off[row], len, r, &bytes, PASS == 1 && a.nl_check,
+                                               &nlhit, &deferred, VCFCD_GT0_NONE);
+        if (PASS == 2) {
+            if (l == 0 && (!ok || bytes != size))   // (cannot happen: the sizes are exact)
+                atomicMin((unsigned long long *)a.err, (unsigned long long)((row << 8) | VCFCD_E_INTERNAL));
+            continue;
+        }
+        if (ok && bytes == size) continue;
+        miss();
+        if (ok) {   // a predicted size was wrong
+            if (l == 0) a.rec_size[row] = bytes | VCFCD_DEFER;
+            continue;
+        }
+        bool nl = nlhit;
+        if (!nl && a.nl_check) nl = row_has_nl(a.buf + a.line_off[row], len);
+        if (nl) {   // (as k_encode_var: the caller indexes the lines again)
+            if (l == 0) {
+                a.rec_size[row] = 0;
+                atomicMin((unsigned long long *)a.err, (unsigned long long)((row << 8) | VCFCD_E_NEWLINE));
+            }
+            continue;
+        }
+        // another shape after its first chunk: the general path, staged (as k_encode_var)
+        if (l == 0) atomicAdd(a.defer_fallback, 1u);
+        if (!row_setup(a, row, lds + wave * RING_STRIDE, r)) continue;
+        const uint32_t st = encode_general(a.buf + a.line_off[row], len, r, &bytes);
+        if (l == 0) {
+            a.rec_size[row] = st == VCFCD_OK ? bytes : 0u;
+            if (st != VCFCD_OK) atomicMin((unsigned long long *)a.err, (unsigned long long)((row << 8) | st));
+        }
     }
 }
 
@@ -1986,7 +2072,9 @@ __global__ __launch_bounds__(256) void k_compact_out(const uint8_t *__restrict__
                                                      const uint64_t *__restrict__ slot_off,
                                                      const uint64_t *__restrict__ rec_off, uint64_t n,
                                                      const uint32_t *__restrict__ tile_first,
-                                                     uint8_t *__restrict__ out, uint64_t out_cap, uint32_t pb) {
+                                                     uint8_t *__restrict__ out, uint64_t out_cap, uint32_t pb,
+                                                     const uint32_t *gate) {
+    if (gate && *gate == 0) return;   // (the second compaction: only after a misprediction)
     const uint32_t l = vw::lane_id();
     const uint64_t g = (uint64_t)blockIdx.x * 4 + vw::readfirst(threadIdx.x >> 6);
     const uint64_t G = (uint64_t)gridDim.x * 4;
@@ -2066,7 +2154,6 @@ __global__ __launch_bounds__(256) void k_compact_out(const uint8_t *__restrict__
 // ---------------------------------------------------------------------------
 // Exclusive scan u32 -> u64 (n + 1 outputs).  MODE 0: identity, MODE 1:
 // vcfc_slot_bytes(len), MODE 2: record sizes (VCFCD_DEFER masked).  4096 items per 256-thread block.
-constexpr int SCAN_ITEMS = 16, SCAN_THREADS = 256, SCAN_TILE = SCAN_ITEMS * SCAN_THREADS;
 
 template <int MODE> __device__ __forceinline__ uint64_t scan_xf(uint32_t v) {
     return MODE == 1 ? vcfc_slot_bytes(v) : MODE == 2 ? (uint64_t)(v & ~VCFCD_DEFER) : (uint64_t)v;
@@ -2167,13 +2254,22 @@ __device__ __forceinline__ void lb_store(uint64_t *p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// gate (the size scan's second launch, after k_encode_defer<1>): nothing
+// to redo unless *gate -- then block 0 merges the first scan's out_cap
+// report (*merge) into err and every block returns.
 template <int MODE, bool TILES>
 __global__ __launch_bounds__(256) void k_scan_lb(const uint32_t *__restrict__ in, uint64_t n, uint32_t *ticket,
                                                  uint64_t *flags, uint64_t *__restrict__ out,
-                                                 uint32_t *__restrict__ tile_first, uint64_t out_cap, uint64_t *err) {
+                                                 uint32_t *__restrict__ tile_first, uint64_t out_cap, uint64_t *err,
+                                                 const uint32_t *gate, const uint64_t *merge) {
     __shared__ uint64_t sh[SCAN_THREADS];
     __shared__ uint32_t s_tile;
     __shared__ uint64_t s_excl;
+    if (gate && *gate == 0) {
+        if (blockIdx.x == 0 && threadIdx.x == 0 && merge && *merge != ~0ull)
+            atomicMin((unsigned long long *)err, (unsigned long long)*merge);
+        return;
+    }
     if (threadIdx.x == 0) s_tile = atomicAdd(ticket, 1u);
     __syncthreads();
     const uint64_t tile = s_tile;
@@ -2229,11 +2325,28 @@ __global__ __launch_bounds__(256) void k_scan_lb(const uint32_t *__restrict__ in
             if (TILES) {
                 const uint64_t b = run + vals[i];
                 if (b > out_cap) atomicMin((unsigned long long *)err, (unsigned long long)((r << 8) | VCFCD_E_NOSPACE));
-                // (a tile wholly inside a deferred record: flagged, the
-                // compaction skips it -- k_encode_defer writes those bytes)
-                const uint32_t dfl = MODE == 2 && (in[r] & VCFCD_DEFER) ? TILE_DEFERRED : 0u;
-                for (uint64_t t = (run + CT - 1) / CT; t * CT < b; t++)
-                    tile_first[t] = (uint32_t)r | ((t + 1) * CT <= b ? dfl : 0u);
+                // (a tile whose bytes all belong to deferred records: flagged,
+                // the compaction skips it -- k_encode_defer writes those
+                // bytes.  The tile a deferred record ends in is followed
+                // into the next records while they are deferred or empty;
+                // records end past the batch's last byte count as covered.
+                // Round 5: kind-1 law 2, every record deferred, k_compact
+                // copied one 4 KiB tile of staging garbage per record)
+                const bool dr = MODE == 2 && (in[r] & VCFCD_DEFER);
+                for (uint64_t t = (run + CT - 1) / CT; t * CT < b; t++) {
+                    const uint64_t te = (t + 1) * CT;
+                    bool skip = dr && te <= b;
+                    if (dr && te > b) {
+                        uint64_t e = b, q = r + 1;
+                        for (int k = 0; k < 4 && q < n && e < te; k++, q++) {
+                            const uint32_t v = in[q];
+                            if (v != 0 && !(v & VCFCD_DEFER)) break;
+                            e += v & ~VCFCD_DEFER;
+                        }
+                        skip = e >= te || q >= n;
+                    }
+                    tile_first[t] = (uint32_t)r | (skip ? TILE_DEFERRED : 0u);
+                }
             }
             if (r + 1 == n) out[n] = run + vals[i];
         }
@@ -2251,9 +2364,12 @@ __global__ __launch_bounds__(256) void k_scan_lb(const uint32_t *__restrict__ in
 // garbage into its first 16 bytes from the second replay on, consistent
 // with the hang (the ticket array's memset, far more than 8 bytes, did not
 // leave zeros).  A kernel node is replayed like every other launch.
-__global__ __launch_bounds__(256) void k_encode_reset(uint64_t *lb, uint64_t words, uint64_t *err) {
+__global__ __launch_bounds__(256) void k_encode_reset(uint64_t *lb, uint64_t words, uint64_t *err, uint64_t *nospace) {
     for (uint64_t i = threadIdx.x; i < words; i += 256) lb[i] = 0;
-    if (threadIdx.x == 0) *err = ~0ull;
+    if (threadIdx.x == 0) {
+        *err = ~0ull;
+        *nospace = ~0ull;
+    }
 }
 
 }  // namespace
@@ -2272,7 +2388,11 @@ VcfcWorkspaceLayout vcfc_encode_workspace_layout(uint64_t n, uint64_t total_line
     L.lb = o;
     L.retry_count = o + 8;
     L.defer_count = o + 12;
-    L.lb_bytes = 16 + 16 * nt;
+    // after both scans' flags: the misprediction word, the fallback count, the first scan's out_cap report
+    L.mispredict = o + 16 + 16 * nt;
+    L.defer_fallback = L.mispredict + 4;
+    L.nospace = L.mispredict + 8;
+    L.lb_bytes = 32 + 16 * nt;
     o = al(o + L.lb_bytes);
     L.defer_list = o; o = al(o + 4 * n);
     L.tile_first = o; o = al(o + 4 * (vcfc_record_bound(n, total_line_bytes) / CT + 2));
@@ -2303,12 +2423,13 @@ hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t s, hipEvent_t
     // (nt + 1), size-scan flags (nt + 1)
     uint32_t *tickets = reinterpret_cast<uint32_t *>(a.lb);
     uint64_t *flags_a = reinterpret_cast<uint64_t *>(a.lb + 16), *flags_b = flags_a + nt + 1;
+    // (the tickets and counters, both scans' flags, the misprediction word and the fallback count)
     hipLaunchKernelGGL(k_encode_reset, dim3(1), dim3(256), 0, s, reinterpret_cast<uint64_t *>(a.lb),
-                       (uint64_t)(2 + 2 * (nt + 1)), a.err);
+                       (uint64_t)(2 + 2 * (nt + 1) + 1), a.err, a.nospace);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[0], s);
     hipLaunchKernelGGL((k_scan_lb<1, false>), dim3((unsigned)nt), dim3(SCAN_THREADS), 0, s, a.line_len, a.n, tickets,
-                       flags_a, a.slot_off, nullptr, 0, nullptr);
+                       flags_a, a.slot_off, nullptr, 0, nullptr, nullptr, nullptr);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[1], s);
     hipLaunchKernelGGL(k_encode_fast, dim3((unsigned)((a.n + K1_WAVES - 1) / K1_WAVES)), dim3(64 * K1_WAVES), 0, s, a,
@@ -2322,27 +2443,38 @@ hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t s, hipEvent_t
                            (uint64_t)0, a.n);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[2], s);
-    if (a.defer_records)   // (sizes flagged VCFCD_DEFER: masked, and their tiles flagged for the compaction)
+    // (deferred records: sizes flagged VCFCD_DEFER masked, their tiles
+    // flagged for the compaction, and the out_cap report held back -- some
+    // sizes may be predictions)
+    if (a.defer_records)
         hipLaunchKernelGGL((k_scan_lb<2, true>), dim3((unsigned)nt), dim3(SCAN_THREADS), 0, s, a.rec_size, a.n,
-                           tickets + 1, flags_b, a.rec_off, a.tile_first, a.out_cap, a.err);
+                           tickets + 1, flags_b, a.rec_off, a.tile_first, a.out_cap, a.nospace, nullptr, nullptr);
     else
         hipLaunchKernelGGL((k_scan_lb<0, true>), dim3((unsigned)nt), dim3(SCAN_THREADS), 0, s, a.rec_size, a.n,
-                           tickets + 1, flags_b, a.rec_off, a.tile_first, a.out_cap, a.err);
+                           tickets + 1, flags_b, a.rec_off, a.tile_first, a.out_cap, a.err, nullptr, nullptr);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[3], s);
     // a grid of 8 waves per SIMD striding over the output tiles (uniform work)
     const uint64_t tiles = vcfc_record_bound(a.n, a.line_bytes_hint) / CT + 1;
     const uint64_t cblocks = tiles < 8192 ? (tiles + 3) / 4 : 2048;
     hipLaunchKernelGGL(k_compact_out, dim3((unsigned)cblocks), dim3(256), 0, s, a.prim, a.slots, a.slot_off,
-                       a.rec_off, a.n, a.tile_first, a.out, a.out_cap, a.prim_bytes);
+                       a.rec_off, a.n, a.tile_first, a.out, a.out_cap, a.prim_bytes, nullptr);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[4], s);
     // the deferred rows' records, straight into out (a resident grid; exits
     // at once when k_encode_var deferred none)
     if (a.defer_records) {
         const uint64_t dblocks = (a.n + K1_WAVES - 1) / K1_WAVES;
-        hipLaunchKernelGGL(k_encode_defer, dim3((unsigned)(dblocks < DEFER_BLOCKS ? dblocks : DEFER_BLOCKS)),
-                           dim3(64 * K1_WAVES), 0, s, a);
+        const dim3 dgrid((unsigned)(dblocks < DEFER_BLOCKS ? dblocks : DEFER_BLOCKS));
+        hipLaunchKernelGGL(k_encode_defer<1>, dgrid, dim3(64 * K1_WAVES), 0, s, a);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        // after a misprediction: the layout again on exact sizes (three
+        // launches that return at once otherwise)
+        hipLaunchKernelGGL((k_scan_lb<2, true>), dim3((unsigned)nt), dim3(SCAN_THREADS), 0, s, a.rec_size, a.n,
+                           tickets + 1, flags_b, a.rec_off, a.tile_first, a.out_cap, a.err, a.mispredict, a.nospace);
+        hipLaunchKernelGGL(k_compact_out, dim3((unsigned)cblocks), dim3(256), 0, s, a.prim, a.slots, a.slot_off,
+                           a.rec_off, a.n, a.tile_first, a.out, a.out_cap, a.prim_bytes, a.mispredict);
+        hipLaunchKernelGGL(k_encode_defer<2>, dgrid, dim3(64 * K1_WAVES), 0, s, a);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (ev) (void)hipEventRecord(ev[5], s);
