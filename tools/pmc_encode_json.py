@@ -12,12 +12,16 @@ KERNELS = ("k_encode_fast", "k_encode_var", "k_encode_general", "k_encode_defer"
 
 
 def per_kernel(d, counter):
-    vals = defaultdict(list)
+    """Counter total of each kernel per encode call: summed over all its
+    dispatches (k_encode_defer<1> and <2>, the compaction and its gated
+    second launch) and divided by the calls (one k_encode_fast dispatch each)."""
+    tot, calls = defaultdict(float), 0
     for r in csv.DictReader(open(d + "/run_counter_collection.csv")):
         name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].split("<")[0].split()[-1]
         if r["Counter_Name"] == counter and name in KERNELS:
-            vals[name].append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in vals.items()}
+            tot[name] += float(r["Counter_Value"])
+            calls += name == "k_encode_fast"
+    return {k: v / max(calls, 1) for k, v in tot.items()}
 
 
 def main():
