@@ -49,7 +49,7 @@ for s in $STEPS; do
            (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --pmc $P --kernel-trace --output-format csv -d "$O/pmcx_$n" -o run -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS} > "$O/pmcx_$n.log" 2>&1) || { echo "pmcx $n failed rc=$?"; tail -30 "$O/pmcx_$n.log"; exit 1; }
          done ;;
     distfile) timeout -k 10 600 python bench.py --mode distfile --steps 3 --warmup 1 > "$O/bench_distfile.json" 2> "$O/bench_distfile.err" || { echo "distfile failed"; tail -30 "$O/bench_distfile.err"; exit 1; } ; cat "$O/bench_distfile.json" ;;
-    distfile2) VCFC_BENCH_REHEARSAL=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29621 bench.py --mode distfile --steps 3 --warmup 1 --dist-dir /tmp/vcfc_distfile2 > "$O/bench_distfile2.json" 2> "$O/bench_distfile2.err" || { echo "distfile2 failed"; tail -30 "$O/bench_distfile2.err"; exit 1; } ; cat "$O/bench_distfile2.json" ;;
+    distfile2) VCFC_BENCH_REHEARSAL=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29621 bench.py --gpus 2 --mode distfile --steps 3 --warmup 1 --dist-dir /tmp/vcfc_distfile2 > "$O/bench_distfile2.json" 2> "$O/bench_distfile2.err" || { echo "distfile2 failed"; tail -30 "$O/bench_distfile2.err"; exit 1; } ; cat "$O/bench_distfile2.json" ;;
     bench2) timeout -k 10 600 python bench.py --law 2 --no-cpu-baseline > "$O/bench_law2.json" 2> "$O/bench_law2.err" || { echo "bench2 failed"; tail -30 "$O/bench_law2.err"; exit 1; } ; cat "$O/bench_law2.json" ;;
     prof2) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof2" -o run -- python3 "$R/bench.py" --law 2 --steps 10 --warmup 2 --no-cpu-baseline > "$O/prof2.log" 2>&1) || { echo "prof2 failed rc=$?"; tail -30 "$O/prof2.log"; exit 1; } ;;
     pmc2) for P in FETCH_SIZE WRITE_SIZE; do
