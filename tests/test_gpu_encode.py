@@ -231,14 +231,16 @@ def test_variable_token_rows(ctx, seed):
     assert ctx.compress_buffer(data) == want
 
 
-@pytest.mark.parametrize("odd", ["none", "ntok", "mixed_later", "general_later"])
+@pytest.mark.parametrize("odd", ["none", "ntok", "mixed_later", "general_later", "long_then_plain"])
 def test_predicted_deferred_records(ctx, odd):
     """GT:DP:GQ rows of one sample count: after two rows agree on their token
-    count, k_encode_var sizes the later deferred rows from their first chunk
-    (all escapes predicted) and k_encode_defer's first pass checks each.
-    With one odd row among them -- a sample more, plain tokens after a
-    first chunk of 1-byte escapes, two even-length tokens after the first
-    chunk (the general path) -- the check fails and the gated size scan,
+    count, k_encode_var sizes the later deferred rows without reading them
+    (a long first token: all escapes predicted; 1-byte tokens: from their
+    first chunk) and k_encode_defer's first pass checks each.  With one odd
+    row among them -- a sample more, plain tokens after a first chunk of
+    1-byte escapes, two even-length tokens after the first chunk (the
+    general path), plain tokens right after a long first token -- the
+    check fails and the gated size scan,
     compaction and deferred pass lay the batch out again: byte-exact
     against the oracle through compress_buffer either way."""
     import random
@@ -253,6 +255,8 @@ def test_predicted_deferred_records(ctx, odd):
                                             [rnd.choice([b"0|0", b"0|1"]) for _ in range(400)])
         elif odd == "general_later":
             lines[i] = T.PFX_V + b"\t".join([b"0|1:33:99"] * 300 + [b"0|1:3:99"] * 2 + [b"0|1:33:99"] * 398)
+        elif odd == "long_then_plain":
+            lines[i] = T.PFX_V + b"\t".join([b"0|1:33:99"] + [rnd.choice([b"0|0", b"0|1"]) for _ in range(699)])
     hdr = (b"##fileformat=VCFv4.2\n#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\t" +
            b"\t".join(b"S%d" % j for j in range(700)) + b"\n")
     data = hdr + b"\n".join(lines) + b"\n"

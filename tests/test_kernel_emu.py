@@ -498,11 +498,12 @@ def test_predicted_deferred_records(monkeypatch):
     assert E.last_deferred() == 40 and E.last_mispredict() == 0
 
 
-@pytest.mark.parametrize("case", ["ntok", "mixed_later", "general_later", "cap", "newline"])
+@pytest.mark.parametrize("case", ["ntok", "mixed_later", "general_later", "long_then_plain", "cap", "newline"])
 def test_mispredicted_deferred_records(case, monkeypatch):
     """Predictions that are wrong: another token count (a row with one
     sample more), plain tokens after a first chunk of 1-byte escapes (the
-    record is not all escapes),
+    record is not all escapes), plain tokens right after a long first token
+    (predicted from that token alone, before any genotype chunk is read),
     an even-length token after the first chunk (the row leaves the
     variable-token path: general path, staged, not counted as deferred),
     out_cap cutting the batch (the held-back out_cap report against the
@@ -521,6 +522,8 @@ def test_mispredicted_deferred_records(case, monkeypatch):
     elif case == "general_later":
         # (two: an odd count of even-length tokens fails the region's parity check up front)
         lines[6] = PFX_V + b"\t".join([b"0|1:33:99"] * 300 + [b"0|1:3:99"] * 2 + [b"0|1:33:99"] * 398)
+    elif case == "long_then_plain":   # predicted from its long first token alone; plain tokens follow at once
+        lines[6] = PFX_V + b"\t".join([b"0|1:33:99"] + [rnd.choice([b"0|0", b"0|1"]) for _ in range(900)])
     elif case == "newline":
         monkeypatch.setenv("EMU_NL_CHECK", "1")
         lines[6] = PFX_V + b"\t".join([b"0|1:33:99"] * 300 + [b"0|1:33\n99"] + [b"0|1:33:99"] * 399)
@@ -540,7 +543,8 @@ def test_mispredicted_deferred_records(case, monkeypatch):
     assert err0 == (1 << 64) - 1
     assert out1 == out0 == b"".join(G.oracle_encode_line(x)[1] for x in lines)
     assert list(ro1) == list(ro0)
-    assert E.last_deferred() == (11 if case == "general_later" else 12)
+    # (a row that leaves the variable-token path is staged by the general path, not deferred)
+    assert E.last_deferred() == (11 if case in ("general_later", "long_then_plain") else 12)
 
 
 @pytest.mark.parametrize("defer", ["0", "1"])

@@ -39,6 +39,9 @@
 // the first sample's offset (< VCFCD_GT0_NONE): k_encode_var skips the parse
 #define VCFCD_RETRY_GT 0xC0000000u
 #define VCFCD_GT0_NONE 0x3FFFFFFFu
+// ... with this bit when the first sample's token is 5 bytes or longer (an
+// escape: GT:DP:GQ and the like; the offset itself is < 1 KiB)
+#define VCFCD_GT0_LONG 0x20000000u
 // rec_size flag of a deferred row: k_encode_var only sized it (every chunk an
 // escape chunk), k_encode_defer writes its record straight to out after the
 // size scan (the size is the low 31 bits)

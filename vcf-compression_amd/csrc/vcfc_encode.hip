@@ -373,7 +373,15 @@ __device__ __forceinline__ int fast_prefix_step(const Chunk &cur, uint32_t c, ui
     }
     if (vw::ballot((et & below) != 0 || (lf & vm) != 0)) return 2;
     if (!VAR && vw::ballot(odd)) {   // a clean prefix, tokens of another length: k_encode_var's row, gt0 known
-        f.gt0 = (int32_t)x9;
+        // the first token 5 bytes or longer (no TAB in line bytes x9 + 1 ..
+        // x9 + 4, all inside this chunk and the line): VCFCD_GT0_LONG
+        const int32_t w0 = (int32_t)x9 + 1 - x0;   // the window's first byte, lane-relative
+        const uint32_t win = w0 >= (int32_t)BPL || w0 + 4 <= 0
+                                 ? 0u
+                                 : ((w0 < 0 ? 0xFu >> -w0 : 0xFu << w0) & FULLM);
+        const bool inside = x9 + 5u <= len && (int32_t)x9 + 5 <= (int32_t)((c + 1) * CHUNK) - (int32_t)lead;
+        const bool long1 = inside && vw::ballot((m & win) != 0) == 0;
+        f.gt0 = (int32_t)(x9 | (long1 ? VCFCD_GT0_LONG : 0u));
         return 3;
     }
     prefix_to_ring(cur, c, lead, r);
@@ -1453,8 +1461,24 @@ __device__ __forceinline__ bool encode_var(const uint8_t *__restrict__ line, uin
     r.fpos = 0;
     const vw::brsrc rsA = vw::make_rsrc(A, (span + 3u) & ~3u);
     uint32_t c = 0;
-    Chunk b = load_chunk(rsA, 0, lo16);
+    const bool long1 = gt0_hint < VCFCD_GT0_NONE && (gt0_hint & VCFCD_GT0_LONG) != 0;
+    if (gt0_hint < VCFCD_GT0_NONE) gt0_hint &= ~VCFCD_GT0_LONG;
     const bool known = gt0_hint < VCFCD_GT0_NONE && gt0_hint < len;
+    // A deferred row's size predicted before any load: the first token is an
+    // escape of 5+ bytes (k_encode_fast's VCFCD_GT0_LONG), the genotype
+    // region spans more than one chunk and has odd-length tokens' parity.
+    // (k_encode_defer<1> checks it as it writes the record.)
+    if (VM == VAR_DEFER && known && long1 && ntok_ref != 0 && ntok_ref <= (len + 1) / 2) {
+        const uint32_t glen = len - gt0_hint;
+        const uint32_t nh = (glen + 1) >> 1;
+        if (((glen + 1) & 1u) == 0 && nh < (1u << 23) - 2 * MOD_BIAS && (nh + HPC - 1) / HPC > 1) {
+            *rec_bytes = len + 9u + ntok_ref;
+            *deferred = true;
+            *predicted = true;
+            return true;
+        }
+    }
+    Chunk b = load_chunk(rsA, 0, lo16);
     if (!known) {
         // prefix phase: as encode_fast
         int st;
