@@ -265,14 +265,17 @@ def test_predicted_deferred_records(ctx, odd):
     assert ctx.compress_buffer(data) == want
 
 
-def test_encode_captured_in_hip_graph(torch, vcfc):
-    """vcfc_encode_rows_device enqueues its whole pipeline (memsets, the two
-    look-back scans, k_encode_fast, k_encode_var, k_compact_out) with no host
-    synchronisation, so it can be captured in a HIP graph: the replayed graph
-    writes the same records, offsets and status as an eager call, replay after
-    replay (the workspace state is re-zeroed by the captured memsets)."""
+@pytest.mark.parametrize("law", [0, 2])
+def test_encode_captured_in_hip_graph(torch, vcfc, law):
+    """vcfc_encode_rows_device enqueues its whole pipeline (the reset kernel,
+    the two look-back scans, k_encode_fast, k_encode_var, k_compact_out, the
+    deferred passes and the gated relayout) with no host synchronisation, so
+    it can be captured in a HIP graph: the replayed graph writes the same
+    records, offsets and status as an eager call, replay after replay (the
+    workspace state is re-zeroed by the captured reset kernel).  Law 2 takes
+    the deferred and predicted records (GT:DP:GQ rows)."""
     import workload
-    rows = workload.DeviceRows(torch, vcfc, 2000, 2504, 0, seed=41, device="cuda:0")
+    rows = workload.DeviceRows(torch, vcfc, 2000, 2504, law, seed=41, device="cuda:0")
     n = rows.n
     want_out, want_rec, want_err = _device_encode(torch, vcfc, rows)
     ws_bytes = vcfc.workspace_size(n, rows.line_bytes)
@@ -296,6 +299,48 @@ def test_encode_captured_in_hip_graph(torch, vcfc):
         assert np.array_equal(r, want_rec)
         k = int(r[n])
         assert torch.equal(out[:k], want_out[:k])
+
+
+def test_mispredicted_batch_replayed_in_hip_graph(torch, vcfc):
+    """A batch whose predicted deferred records are wrong (one GT:DP:GQ row
+    with a sample more among rows that agree), captured in a HIP graph: every
+    replay resets the misprediction word, finds the wrong size again and
+    lays the batch out again through the gated launches -- records equal to
+    the oracle's on each replay."""
+    import random
+    import test_kernel_emu as T
+    rnd = random.Random(77)
+    lines = [T._gdg(rnd, 700) for _ in range(200)]
+    lines[150] = T._gdg(rnd, 701)
+    buf = b"".join(ln + b"\n" for ln in lines)
+    off = np.cumsum([0] + [len(ln) + 1 for ln in lines[:-1]]).astype(np.int64)
+    ln_ = np.array([len(ln) for ln in lines], dtype=np.int32)
+    dev = "cuda:0"
+    d_buf = torch.from_numpy(np.frombuffer(buf + b"\0" * 64, dtype=np.uint8).copy()).to(dev)
+    d_off = torch.from_numpy(off).to(dev)
+    d_len = torch.from_numpy(ln_).to(dev)
+    n, tot = len(lines), int(ln_.sum())
+    ws_bytes = vcfc.workspace_size(n, tot)
+    cap = vcfc.encode_bound(n, tot)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    out = torch.zeros(cap, dtype=torch.uint8, device=dev)
+    rec = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    err = torch.zeros(1, dtype=torch.int64, device=dev)
+    want = [G.oracle_encode_line(x)[1] for x in lines]
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        vcfc.encode_rows_device(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, tot, out.data_ptr(), cap,
+                                rec.data_ptr(), ws.data_ptr(), ws_bytes, err.data_ptr(),
+                                torch.cuda.current_stream().cuda_stream)
+    for _ in range(3):
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert int(err.cpu().numpy().view(np.uint64)[0]) == vcfc.NO_ERROR
+        r = rec.cpu().numpy()
+        blob = out[:int(r[n])].cpu().numpy().tobytes()
+        assert blob == b"".join(want)
 
 
 @pytest.mark.parametrize("law,kind", [(2, "1"), (1, None), (0, None), (2, None), (2, "3")])

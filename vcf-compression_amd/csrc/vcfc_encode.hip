@@ -1967,13 +1967,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
     const uint32_t cnt = vw::readfirst(*a.defer_count);
     const uint32_t G = gridDim.x * K1_WAVES;
     auto miss = [&]() {
-        if (l == 0 && atomicExch(a.mispredict, 1u) == 0u) {
-            // the size scan's ticket and tile flags, for its second launch
+        uint32_t first = 0;
+        if (l == 0) first = atomicExch(a.mispredict, 1u) == 0u ? 1u : 0u;
+        if (vw::readfirst(first)) {
+            // the first wave to miss rearms the size scan's ticket and tile
+            // flags for its second launch (the whole wave: nt + 1 words)
             const uint64_t nt = (a.n + SCAN_TILE - 1) / SCAN_TILE;
             uint32_t *tickets = reinterpret_cast<uint32_t *>(a.lb);
             uint64_t *flags_b = reinterpret_cast<uint64_t *>(a.lb + 16) + nt + 1;
-            tickets[1] = 0;
-            for (uint64_t i = 0; i <= nt; i++) flags_b[i] = 0;
+            if (l == 0) tickets[1] = 0;
+            for (uint64_t i = l; i <= nt; i += 64) flags_b[i] = 0;
         }
     };
     for (uint32_t q = blockIdx.x * K1_WAVES + wave; q < cnt; q += G) {
