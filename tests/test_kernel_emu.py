@@ -498,6 +498,62 @@ def test_predicted_deferred_records(monkeypatch):
     assert E.last_deferred() == 40 and E.last_mispredict() == 0
 
 
+@pytest.mark.parametrize("seed", range(6))
+def test_predicted_deferred_records_random_batches(seed, monkeypatch):
+    """Seeded random batches for the prediction machinery: runs of rows with
+    one sample count (predictions taken) broken by rows of another count,
+    long-first-token rows that turn plain, 1-byte escape rows, even-length
+    tokens after the first chunk, plain GT-only rows and short rows, at a
+    random buffer alignment and now and then an out_cap inside the batch.
+    Records, offsets and the error word equal those of the encode without
+    deferral, and the records equal the oracle's."""
+    rnd = random.Random(1000 + seed)
+    S0 = rnd.choice([260, 300, 700])
+    lines = []
+    for _ in range(rnd.randint(40, 90)):
+        r = rnd.random()
+        if r < 0.55:
+            lines.append(_gdg(rnd, S0))
+        elif r < 0.62:
+            lines.append(_gdg(rnd, S0 + rnd.choice([-1, 1, 7])))
+        elif r < 0.68:
+            lines.append(PFX_V + b"\t".join([b"0|1:33:99"] * rnd.randint(1, 250) +
+                                           [rnd.choice([b"0|0", b"0|1"]) for _ in range(S0)]))
+        elif r < 0.74:
+            lines.append(PFX_V + b"\t".join([rnd.choice([b"0", b"1", b"."]) for _ in range(rnd.randint(1100, 1600))] +
+                                           [rnd.choice([b"0|0", b"0|1", b"."]) for _ in range(rnd.randint(0, 300))]))
+        elif r < 0.80:
+            k = rnd.randint(250, S0 - 2)
+            lines.append(PFX_V + b"\t".join([b"0|1:33:99"] * k + [b"0|1:3:99"] * 2 + [b"0|1:33:99"] * (S0 - k - 2)))
+        elif r < 0.90:
+            lines.append(PFX_V + b"\t".join(rnd.choice([b"0|0", b"0|1", b"1|1", b"0|2"]) for _ in range(S0)))
+        else:
+            lines.append(PFX_V + b"\t".join(rnd.choice([b"0|0:1", b"1", b"0|0"]) for _ in range(rnd.randint(1, 40))))
+    lead = rnd.randint(0, 15)
+    buf = bytearray(b"#" * lead)
+    offs, lens = [], []
+    for ln in lines:
+        offs.append(len(buf))
+        lens.append(len(ln))
+        buf += ln + b"\n"
+    args = (bytes(buf), np.array(offs, np.uint64), np.array(lens, np.uint32))
+    monkeypatch.setenv("EMU_DEFER", "0")
+    st0, out0, ro0, err0 = E.emu_encode(*args)
+    assert err0 == (1 << 64) - 1
+    assert out0 == b"".join(G.oracle_encode_line(x)[1] for x in lines)
+    cap = int(ro0[rnd.randint(1, len(lines) - 1)]) + rnd.randint(0, 200) if rnd.random() < 0.4 else None
+    if cap is not None:
+        st0, out0, ro0, err0 = E.emu_encode(*args, cap=cap)
+    monkeypatch.setenv("EMU_DEFER", "1")
+    st1, out1, ro1, err1 = E.emu_encode(*args, cap=cap)
+    assert err1 == err0
+    if err0 == (1 << 64) - 1:
+        assert out1 == out0 and list(ro1) == list(ro0)
+    else:
+        bad = err0 >> 8
+        assert out1[:int(ro0[bad])] == out0[:int(ro0[bad])]
+
+
 @pytest.mark.parametrize("case", ["ntok", "mixed_later", "general_later", "long_then_plain", "cap", "newline"])
 def test_mispredicted_deferred_records(case, monkeypatch):
     """Predictions that are wrong: another token count (a row with one
