@@ -80,6 +80,8 @@ for s in $STEPS; do
     profdev2) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/profdev2" -o run -- python3 "$R/bench.py" --mode devfile --law 2 --steps 5 --warmup 1 > "$O/profdev2.log" 2>&1) || { echo "profdev2 failed rc=$?"; tail -30 "$O/profdev2.log"; exit 1; } ;;
     profdev) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/profdev" -o run -- python3 "$R/bench.py" --mode devfile --steps 5 --warmup 1 > "$O/profdev.log" 2>&1) || { echo "profdev failed rc=$?"; tail -30 "$O/profdev.log"; exit 1; } ;;
     rehearse2) VCFC_BENCH_REHEARSAL=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29623 bench.py --gpus 2 --steps 5 --warmup 1 --no-cpu-baseline > "$O/bench_n2_rehearsal.json" 2> "$O/bench_n2_rehearsal.err" || { echo "rehearse2 failed"; tail -30 "$O/bench_n2_rehearsal.err"; exit 1; } ; cat "$O/bench_n2_rehearsal.json" ;;
+    rehearse4) VCFC_BENCH_REHEARSAL=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29625 bench.py --gpus 4 --steps 5 --warmup 1 --no-cpu-baseline > "$O/bench_n4_rehearsal.json" 2> "$O/bench_n4_rehearsal.err" || { echo "rehearse4 failed"; tail -30 "$O/bench_n4_rehearsal.err"; exit 1; } ; cat "$O/bench_n4_rehearsal.json" ;;
+    rehearse4s) VCFC_BENCH_REHEARSAL=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29627 bench.py --gpus 4 --scaling strong --steps 5 --warmup 1 --no-cpu-baseline > "$O/bench_n4s_rehearsal.json" 2> "$O/bench_n4s_rehearsal.err" || { echo "rehearse4s failed"; tail -30 "$O/bench_n4s_rehearsal.err"; exit 1; } ; cat "$O/bench_n4s_rehearsal.json" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
