@@ -265,6 +265,37 @@ def test_predicted_deferred_records(ctx, odd):
     assert ctx.compress_buffer(data) == want
 
 
+def test_unphased_rows_handed_on(ctx):
+    """Unphased rows ("0/1", "./.": every token of the first 2 KiB an escape)
+    go from k_encode_fast to k_encode_var, which predicts their records;
+    with a row that turns plain after its first chunk, one with a sample
+    more, single-chunk rows and rows starting with a plain token among them:
+    byte-exact against the oracle through compress_buffer."""
+    import random
+    import test_kernel_emu as T
+    rnd = random.Random(5150)
+    unph = [b"0/0", b"0/1", b"1/1", b"./."]
+    S = 900
+    lines = [T.PFX_V + b"\t".join(rnd.choice(unph) for _ in range(S)) for _ in range(400)]
+    for i in range(13, 400, 47):
+        k = rnd.randrange(4)
+        if k == 0:
+            lines[i] = T.PFX_V + b"\t".join([rnd.choice(unph) for _ in range(600)] +
+                                            [rnd.choice([b"0|0", b"0|1"]) for _ in range(S - 600)])
+        elif k == 1:
+            lines[i] = T.PFX_V + b"\t".join(rnd.choice(unph) for _ in range(S + 1))
+        elif k == 2:
+            lines[i] = T.PFX_V + b"\t".join(rnd.choice(unph) for _ in range(200))
+        else:
+            lines[i] = T.PFX_V + b"\t".join([b"0|1"] + [rnd.choice(unph) for _ in range(S - 1)])
+    hdr = (b"##fileformat=VCFv4.2\n#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\t" +
+           b"\t".join(b"S%d" % j for j in range(S)) + b"\n")
+    data = hdr + b"\n".join(lines) + b"\n"
+    st, want, _ = G.oracle_compress(data)
+    assert st == 0
+    assert ctx.compress_buffer(data) == want
+
+
 @pytest.mark.parametrize("law", [0, 2])
 def test_encode_captured_in_hip_graph(torch, vcfc, law):
     """vcfc_encode_rows_device enqueues its whole pipeline (the reset kernel,
@@ -347,10 +378,11 @@ def test_mispredicted_batch_replayed_in_hip_graph(torch, vcfc):
 def test_deferred_records_chosen_per_row(torch, vcfc, monkeypatch, law, kind):
     """Deferred records are on by default (round 5) and the kernel chooses them
     per row from the row's bytes: every GT:DP:GQ row (law-2 kind 1: its first
-    genotype chunk all escapes, more than one chunk) is deferred, no row of
-    the chr22 / random_vcf laws nor an unphased row of 3-byte escapes (kind
-    3: the fast kernel's, staged) is, and in the law-2 mix exactly the
-    GT:DP:GQ rows are.  Every record equals the oracle's."""
+    genotype chunk all escapes, more than one chunk) is deferred, and every
+    unphased row (kind 3: a first chunk of 3-byte escapes only, which
+    k_encode_fast hands on); no row of the chr22 / random_vcf laws is, and in
+    the law-2 mix exactly the GT:DP:GQ and unphased rows are.  Every record
+    equals the oracle's."""
     import workload
     if kind is None:
         monkeypatch.delenv("VCFC_LAW2_KIND", raising=False)
@@ -371,16 +403,17 @@ def test_deferred_records_chosen_per_row(torch, vcfc, monkeypatch, law, kind):
     deferred = vcfc.encode_deferred_rows(ws.data_ptr(), n, rows.line_bytes, torch.cuda.current_stream().cuda_stream)
     assert int(err.cpu().numpy().view(np.uint64)[0]) == vcfc.NO_ERROR
     lines = rows.host_lines(range(n))
-    gdg = sum(b"GT:DP:GQ" in ln for ln in lines)
-    assert deferred == gdg, (deferred, gdg)
-    if kind == "1":
-        assert gdg == n
-    elif law != 2 or kind == "3":
-        assert gdg == 0
-    else:
-        assert 0 < gdg < n
     r = rec.cpu().numpy()
     blob = out[:int(r[n])].cpu().numpy().tobytes()
     for i, ln in enumerate(lines):
         st, want = G.oracle_encode_line(ln)
         assert st == 0 and blob[int(r[i]):int(r[i + 1])] == want, i
+    gdg = sum(b"GT:DP:GQ" in ln for ln in lines)
+    unph = sum(b"KIND=3" in ln for ln in lines)   # (law 2's INFO names the row kind)
+    assert deferred == gdg + unph, (deferred, gdg, unph)
+    if kind in ("1", "3"):
+        assert gdg + unph == n
+    elif law != 2:
+        assert gdg + unph == 0
+    else:
+        assert 0 < gdg < n and 0 < unph < n

@@ -498,6 +498,47 @@ def test_predicted_deferred_records(monkeypatch):
     assert E.last_deferred() == 40 and E.last_mispredict() == 0
 
 
+@pytest.mark.parametrize("lead", [0, 5])
+def test_unphased_rows_handed_on_and_predicted(lead, monkeypatch):
+    """Rows whose first 2 KiB genotype chunk holds 3-byte escapes only
+    (unphased "0/1", missing "./."): k_encode_fast hands them to
+    k_encode_var with VCFCD_GT0_LONG, which predicts their records without
+    reading them; among them rows that turn plain after the first chunk, a
+    row with one sample more, a single-chunk row (not handed on) and
+    chr22-like rows whose first chunk has a plain token (kept by the fast
+    kernel).  Byte-exact against the oracle and the encode without
+    deferral."""
+    rnd = random.Random(31 + lead)
+    unph = [b"0/0", b"0/1", b"1/1", b"./."]
+    S = 900
+
+    def row(toks):
+        return PFX_V + b"\t".join(toks)
+    lines = [row([rnd.choice(unph) for _ in range(S)]) for _ in range(20)]
+    lines[7] = row([rnd.choice(unph) for _ in range(600)] + [rnd.choice([b"0|0", b"0|1"]) for _ in range(S - 600)])
+    lines[11] = row([rnd.choice(unph) for _ in range(S + 1)])
+    lines[13] = row([rnd.choice(unph) for _ in range(300)])
+    lines[15] = row([b"0|1"] + [rnd.choice(unph) for _ in range(S - 1)])
+    buf = bytearray(b"#" * lead)
+    offs, lens = [], []
+    for ln in lines:
+        offs.append(len(buf))
+        lens.append(len(ln))
+        buf += ln + b"\n"
+    args = (bytes(buf), np.array(offs, np.uint64), np.array(lens, np.uint32))
+    want = b"".join(G.oracle_encode_line(x)[1] for x in lines)
+    monkeypatch.setenv("EMU_DEFER", "0")
+    st0, out0, ro0, err0 = E.emu_encode(*args)
+    monkeypatch.setenv("EMU_DEFER", "1")
+    st1, out1, ro1, err1 = E.emu_encode(*args)
+    assert err0 == err1 == (1 << 64) - 1
+    assert out0 == out1 == want and list(ro0) == list(ro1)
+    # handed on and deferred: all but the single-chunk row and the row whose
+    # first chunk has a plain token
+    assert E.last_deferred() == len(lines) - 2
+    assert E.last_mispredict() == 1
+
+
 @pytest.mark.parametrize("seed", range(6))
 def test_predicted_deferred_records_random_batches(seed, monkeypatch):
     """Seeded random batches for the prediction machinery: runs of rows with

@@ -39,8 +39,11 @@
 // the first sample's offset (< VCFCD_GT0_NONE): k_encode_var skips the parse
 #define VCFCD_RETRY_GT 0xC0000000u
 #define VCFCD_GT0_NONE 0x3FFFFFFFu
-// ... with this bit when the first sample's token is 5 bytes or longer (an
-// escape: GT:DP:GQ and the like; the offset itself is < 1 KiB)
+// ... with this bit when the row starts with escapes -- its first token is 5
+// bytes or longer (GT:DP:GQ and the like), or every token of its first 2 KiB
+// genotype chunk is a 3-byte escape (unphased "0/1", "./."): with deferred
+// records k_encode_var predicts its record without reading it (the offset
+// itself is < 1 KiB)
 #define VCFCD_GT0_LONG 0x20000000u
 // rec_size flag of a deferred row: k_encode_var only sized it (every chunk an
 // escape chunk), k_encode_defer writes its record straight to out after the

@@ -282,6 +282,8 @@ struct FastState {
     uint32_t T, phi;    // token count, gt0's byte phase mod 4
     uint32_t pcls, prs; // class / run start(+1) of the previous token
     uint32_t esc;       // the last genotype chunk held an escape: test the escape shape first
+    uint32_t hand;      // 1: a first genotype chunk of escapes only hands the row on (deferred records,
+                        // > 1 chunk, prefix in the line's first KiB); 2: it did
 };
 
 // Prefix bytes of 1 KiB chunk c -> ring[8 + x]: realign the lane's bytes to
@@ -668,8 +670,10 @@ __device__ __forceinline__ void esc_classes(uint32_t d0, uint32_t d1, uint32_t d
 // The incoming class may be an escape (p0 == 4 makes slot 0 a start whose
 // lead byte is TAB).  EDGE: slots past T-1 take token T-1's class and are
 // masked out of the starts and escapes.
+// false: chunk 0 of a row that f.hand allows to hand on holds escapes only
+// (nothing was written; f.hand = 2).
 template <bool EDGE>
-__device__ __forceinline__ void esc8(const uint32_t (&d)[TPL8], int32_t t0, int32_t tf, FastState &f, Ring &r) {
+__device__ __forceinline__ bool esc8(const uint32_t (&d)[TPL8], int32_t t0, int32_t tf, FastState &f, Ring &r) {
     // per 4 slots: gather bytes 0 (allele a), 2 (allele b) and 1 (separator)
     // of the tokens into one word each; a token is plain ("a|b", a, b in
     // {0,1}) iff a and b are '0'/'1' and the separator is '|'.  Class byte =
@@ -677,6 +681,14 @@ __device__ __forceinline__ void esc8(const uint32_t (&d)[TPL8], int32_t t0, int3
     uint32_t cbL, cbH, eL, eH;   // eL/eH: 0xFF in the byte of each escape slot
     esc_classes(d[0], d[1], d[2], d[3], cbL, eL);
     esc_classes(d[4], d[5], d[6], d[7], cbH, eH);
+    // Round 5: every token of chunk 0 an escape (unphased "0/1", "./."):
+    // records ~1.25x the line, so the row goes to k_encode_var, which sizes
+    // it without reading it (VCFCD_GT0_LONG) and has it written straight to
+    // out (deferred records) instead of staged and copied
+    if (!EDGE && f.hand == 1u && tf == 0 && vw::ballot((eL & eH) != ~0u) == 0) {
+        f.hand = 2u;
+        return false;
+    }
     f.esc = vw::ballot((eL | eH) != 0) != 0;
     if (f.pcls == CLS_NONE) {   // first chunk: see clean8 (an escape token 0 -> class 0: no lead byte)
         f.pcls = vw::readlane(cbL, 0) & 3u;
@@ -774,6 +786,7 @@ __device__ __forceinline__ void esc8(const uint32_t (&d)[TPL8], int32_t t0, int3
     f.pcls = (vw::readlane(cbH, 63) >> 24) & 7u;
     f.prs = vw::umax(vw::readlane(incl, 63), f.prs);
     ring_flush(r, false);
+    return true;
 }
 
 // every slot of the lane is "xyz\t" with x, y, z none of 0x08-0x0B (not TAB,
@@ -840,10 +853,7 @@ __device__ __forceinline__ bool gt_step8(const Chunk8 &cur, uint32_t C, FastStat
         // a chunk with escapes the next one most likely has some too (the
         // random_vcf law: ~20 per chunk): test the escape shape alone.
         if (f.esc) {
-            if (vw::ballot(shape3<false>(d, t0, T)) == 0) {
-                esc8<false>(d, t0, tf, f, r);
-                return true;
-            }
+            if (vw::ballot(shape3<false>(d, t0, T)) == 0) return esc8<false>(d, t0, tf, f, r);
             return false;
         }
         const uint32_t o = ((d[0] ^ Z) | (d[1] ^ Z)) | ((d[2] ^ Z) | (d[3] ^ Z)) |
@@ -866,14 +876,7 @@ __device__ __forceinline__ bool gt_step8(const Chunk8 &cur, uint32_t C, FastStat
             clean8<false>(d, t0, tf, f, r);
             return true;
         }
-        if (vw::ballot(shape3<false>(d, t0, T)) == 0) {
-            // (Round 5 handed rows whose chunk 0 is all escapes -- unphased
-            // "0/1", "./." -- to k_encode_var to be deferred: law 2 +4 %,
-            // law 0 +1 % in an A/B, profiles/r05/ab/ab_r5c_law{2,0}.txt;
-            // removed.)
-            esc8<false>(d, t0, tf, f, r);
-            return true;
-        }
+        if (vw::ballot(shape3<false>(d, t0, T)) == 0) return esc8<false>(d, t0, tf, f, r);
     } else {
         // last chunk: slots past T-1 are ignored; token T-1 has no TAB after it
         bool bad = false;
@@ -887,10 +890,7 @@ __device__ __forceinline__ bool gt_step8(const Chunk8 &cur, uint32_t C, FastStat
             clean8<true>(d, t0, tf, f, r);
             return true;
         }
-        if (vw::ballot(shape3<true>(d, t0, T)) == 0) {
-            esc8<true>(d, t0, tf, f, r);
-            return true;
-        }
+        if (vw::ballot(shape3<true>(d, t0, T)) == 0) return esc8<true>(d, t0, tf, f, r);
     }
     return false;   // tokens of another length or empty fields: the caller runs gt_general on this chunk
 }
@@ -899,7 +899,7 @@ __device__ __forceinline__ bool gt_step8(const Chunk8 &cur, uint32_t C, FastStat
 // prefix (in the first 1 KiB) was clean and only the tokens were of another
 // shape (k_encode_var then skips the prefix parse), else ~0
 __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring &r, uint32_t *rec_bytes,
-                            uint32_t *gt0_hint) {
+                            uint32_t *gt0_hint, bool defer) {
     const uint32_t l = vw::lane_id();
     const uint32_t lead = (uint32_t)(reinterpret_cast<uintptr_t>(line) & 15);
     const uint8_t *A = line - lead;
@@ -909,7 +909,7 @@ __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring
     const uint32_t nch = (span + CHUNK - 1) / CHUNK;
     const uint32_t lo16 = BPL * l;
     FastState f;
-    f.nf = 0; f.carryT = 1; f.gt0 = -1; f.T = 0; f.phi = 0; f.pcls = CLS_NONE; f.prs = 0; f.esc = 0;
+    f.nf = 0; f.carryT = 1; f.gt0 = -1; f.T = 0; f.phi = 0; f.pcls = CLS_NONE; f.prs = 0; f.esc = 0; f.hand = 0;
     r.wpos = 8;
     r.fpos = 0;
 
@@ -938,6 +938,7 @@ __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring
     const vw::brsrc rsG = vw::make_rsrc(line + f.gt0 - phi, (phi + len - (uint32_t)f.gt0 + 3u) & ~3u);
     const uint32_t ncG = (T + SLOTS8 - 1) / SLOTS8;
     const uint32_t lo32 = BPL8 * l;
+    f.hand = defer && c == 0 && ncG > 1 ? 1u : 0u;   // (esc8: an all-escape chunk 0 hands the row on)
     uint32_t C0 = 0;
     // three chunks in flight per wave (two: 8 waves/SIMD but +3 % on the
     // headline law, ab_depth_occupancy.txt; four: 5 waves/SIMD, slower,
@@ -963,6 +964,10 @@ __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring
             if (!ok || C >= ncG) break;
         }
         if (ok) break;
+        if (f.hand == 2u) {   // chunk 0 all escapes: k_encode_var's row, to be deferred (esc8)
+            *gt0_hint = (uint32_t)f.gt0 | VCFCD_GT0_LONG;
+            return false;
+        }
         // chunk `gen`: the general step over its two 1 KiB halves
         for (uint32_t h = 0; h < 2; h++) {
             const Chunk hc = look_ahead(load_chunk(rsG, 2 * gen + h, lo16));
@@ -1452,7 +1457,7 @@ __device__ __forceinline__ bool encode_var(const uint8_t *__restrict__ line, uin
     const uint32_t nch = (span + CHUNK - 1) / CHUNK;
     const uint32_t lo16 = BPL * l;
     VarState f;
-    f.nf = 0; f.carryT = 1; f.gt0 = -1; f.T = 0; f.phi = 0; f.pcls = CLS_NONE; f.prs = 0; f.esc = 0; f.ntok = 0;
+    f.nf = 0; f.carryT = 1; f.gt0 = -1; f.T = 0; f.phi = 0; f.pcls = CLS_NONE; f.prs = 0; f.esc = 0; f.hand = 0; f.ntok = 0;
     f.nlc = nlc ? 1u : 0u; f.nlhit = 0; f.defer = 0; f.sizeonly = 0;
     *nlhit = false;
     *deferred = false;
@@ -1464,9 +1469,10 @@ __device__ __forceinline__ bool encode_var(const uint8_t *__restrict__ line, uin
     const bool long1 = gt0_hint < VCFCD_GT0_NONE && (gt0_hint & VCFCD_GT0_LONG) != 0;
     if (gt0_hint < VCFCD_GT0_NONE) gt0_hint &= ~VCFCD_GT0_LONG;
     const bool known = gt0_hint < VCFCD_GT0_NONE && gt0_hint < len;
-    // A deferred row's size predicted before any load: the first token is an
-    // escape of 5+ bytes (k_encode_fast's VCFCD_GT0_LONG), the genotype
-    // region spans more than one chunk and has odd-length tokens' parity.
+    // A deferred row's size predicted before any load: it starts with
+    // escapes (k_encode_fast's VCFCD_GT0_LONG: a first token of 5+ bytes, or
+    // a first 2 KiB chunk of 3-byte escapes only), the genotype region spans
+    // more than one chunk and has odd-length tokens' parity.
     // (k_encode_defer<1> checks it as it writes the record.)
     if (VM == VAR_DEFER && known && long1 && ntok_ref != 0 && ntok_ref <= (len + 1) / 2) {
         const uint32_t glen = len - gt0_hint;
@@ -1832,7 +1838,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 6))) voi
     Ring r;
     if (!row_setup(a, row, lds + wave * RING_STRIDE, r)) return;
     uint32_t bytes = 0, gt0 = ~0u;
-    const bool ok = encode_fast(a.buf + a.line_off[row], a.line_len[row], r, &bytes, &gt0);
+    const bool ok = encode_fast(a.buf + a.line_off[row], a.line_len[row], r, &bytes, &gt0, a.defer_records != 0);
     VCFC_DIAG_ROW_END(a, row);
     if (vw::lane_id() == 0) {
         // not the fast shape: k_encode_var's wave for this row takes it
