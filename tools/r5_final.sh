@@ -6,7 +6,7 @@
 # device-resident file (laws 1 and 2), the 2-rank rehearsals.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
-T=${FINAL_TAG:-r5final}
+T=${FINAL_TAG:-r5final3}
 bash tools/gpu_check.sh $T smoke tests pmcenc pmcinstall bench profbench || exit 1
 bash tools/gpu_check.sh $T bench0 bench2 benchdec benchq benchdev benchdev2 rehearse2 distfile2 || exit 1
 echo done
