@@ -646,8 +646,12 @@ __device__ __forceinline__ void clean8(const uint32_t (&d)[TPL8], int32_t t0, in
 
 // classes of four 3-byte tokens (byte j = 0x90 + 2a + b, or 0x94 for an
 // escape) and their escape mask (byte j = 0xFF for an escape)
+// CHK: also OR into `bad` a 0x80 for every byte 0-2 of a token that is
+// 0x08-0x0B (TAB, '\n': not the 3-byte shape; the other two go the general
+// way as in shape3) -- exact "some byte is zero" tests on the gathered bytes
+template <bool CHK>
 __device__ __forceinline__ void esc_classes(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3, uint32_t &cb,
-                                            uint32_t &em) {
+                                            uint32_t &em, uint32_t &bad) {
     const uint32_t g0 = vw::perm(d1, d0, 0x06040200u), g1 = vw::perm(d3, d2, 0x06040200u);
     const uint32_t A = vw::perm(g1, g0, 0x06040200u), B = vw::perm(g1, g0, 0x07050301u);
     const uint32_t S = vw::perm(vw::perm(d3, d2, 0x05010C0Cu), vw::perm(d1, d0, 0x0C0C0501u), 0x07060100u);
@@ -657,6 +661,13 @@ __device__ __forceinline__ void esc_classes(uint32_t d0, uint32_t d1, uint32_t d
     em = (n << 1) - (n >> 7);
     const uint32_t c = (((A & 0x01010101u) << 1) + (B & 0x01010101u)) | 0x90909090u;
     cb = (c & ~em) | (0x94949494u & em);
+    if (CHK) {
+        auto tabish = [](uint32_t x) {   // 0x80 in some byte iff one is 0x08-0x0B
+            const uint32_t t = (x & 0xFCFCFCFCu) ^ 0x08080808u;
+            return (t - 0x01010101u) & ~t & 0x80808080u;
+        };
+        bad |= tabish(A) | tabish(B) | tabish(S);
+    }
 }
 
 // Escape chunk: every slot in [0, T) is a 3-byte token followed by one TAB
@@ -670,8 +681,12 @@ __device__ __forceinline__ void esc_classes(uint32_t d0, uint32_t d1, uint32_t d
 // The incoming class may be an escape (p0 == 4 makes slot 0 a start whose
 // lead byte is TAB).  EDGE: slots past T-1 take token T-1's class and are
 // masked out of the starts and escapes.
-// false: chunk 0 of a row that f.hand allows to hand on holds escapes only
-// (nothing was written; f.hand = 2).
+// false (nothing written, no state changed): the chunk is not the escape
+// shape (interior chunks: byte 3 of some slot is not TAB, or a token byte is
+// 0x08-0x0B -- the caller's general step takes it), or it is chunk 0 of a
+// row that f.hand allows to hand on and holds escapes only (f.hand = 2).
+// (Round 5: the interior shape test folded into the classification's
+// gathered bytes instead of shape3's pass over the slots.)
 template <bool EDGE>
 __device__ __forceinline__ bool esc8(const uint32_t (&d)[TPL8], int32_t t0, int32_t tf, FastState &f, Ring &r) {
     // per 4 slots: gather bytes 0 (allele a), 2 (allele b) and 1 (separator)
@@ -679,8 +694,15 @@ __device__ __forceinline__ bool esc8(const uint32_t (&d)[TPL8], int32_t t0, int3
     // {0,1}) iff a and b are '0'/'1' and the separator is '|'.  Class byte =
     // 0x90 + 2a + b, escapes 0x94; an escape's bytes never reach a neighbour.
     uint32_t cbL, cbH, eL, eH;   // eL/eH: 0xFF in the byte of each escape slot
-    esc_classes(d[0], d[1], d[2], d[3], cbL, eL);
-    esc_classes(d[4], d[5], d[6], d[7], cbH, eH);
+    uint32_t bad = 0;
+    esc_classes<!EDGE>(d[0], d[1], d[2], d[3], cbL, eL, bad);
+    esc_classes<!EDGE>(d[4], d[5], d[6], d[7], cbH, eH, bad);
+    if (!EDGE) {
+        uint32_t at = 0;   // byte 3 of every slot a TAB
+#pragma unroll
+        for (int j = 0; j < (int)TPL8; j++) at |= d[j] ^ 0x09090909u;
+        if (vw::ballot((bad | (at & 0xFF000000u)) != 0)) return false;
+    }
     // Round 5: every token of chunk 0 an escape (unphased "0/1", "./."):
     // records ~1.25x the line, so the row goes to k_encode_var, which sizes
     // it without reading it (VCFCD_GT0_LONG) and has it written straight to
@@ -853,8 +875,7 @@ __device__ __forceinline__ bool gt_step8(const Chunk8 &cur, uint32_t C, FastStat
         // a chunk with escapes the next one most likely has some too (the
         // random_vcf law: ~20 per chunk): test the escape shape alone.
         if (f.esc) {
-            if (vw::ballot(shape3<false>(d, t0, T)) == 0) return esc8<false>(d, t0, tf, f, r);
-            return false;
+            return esc8<false>(d, t0, tf, f, r);   // (its own shape test)
         }
         const uint32_t o = ((d[0] ^ Z) | (d[1] ^ Z)) | ((d[2] ^ Z) | (d[3] ^ Z)) |
                            ((d[4] ^ Z) | (d[5] ^ Z)) | ((d[6] ^ Z) | (d[7] ^ Z));
@@ -876,7 +897,7 @@ __device__ __forceinline__ bool gt_step8(const Chunk8 &cur, uint32_t C, FastStat
             clean8<false>(d, t0, tf, f, r);
             return true;
         }
-        if (vw::ballot(shape3<false>(d, t0, T)) == 0) return esc8<false>(d, t0, tf, f, r);
+        return esc8<false>(d, t0, tf, f, r);   // (its own shape test; false: the general step)
     } else {
         // last chunk: slots past T-1 are ignored; token T-1 has no TAB after it
         bool bad = false;
