@@ -498,6 +498,41 @@ def test_predicted_deferred_records(monkeypatch):
     assert E.last_deferred() == 40 and E.last_mispredict() == 0
 
 
+@pytest.mark.parametrize("where", ["interior", "last"])
+def test_escape_step_refuses_other_shapes(where):
+    """esc8 tests the 3-byte shape itself (round 5: on its gathered bytes, for
+    interior chunks and the row's last chunk): a 1-byte and a 5-byte token in
+    place of two 3-byte ones (the line length, and so the slot count, stays
+    that of 3-byte tokens), a token holding 0x0B or 0x08, a TAB inside a
+    token -- in a chunk that follows an escape chunk (the escape shape is
+    tested alone there) or not -- go to the general step: byte-exact."""
+    rnd = random.Random(77 if where == "interior" else 78)
+    S = 1100   # chunks of 512 tokens: 0, 1 interior, 2 the last (76 tokens)
+    pos = 700 if where == "interior" else 1060
+    lines = []
+    for defect in ("len15", "vt", "bs", "tab"):
+        for esc_before in (False, True):
+            toks = [rnd.choice([b"0|0", b"0|1", b"1|1"]) for _ in range(S)]
+            if esc_before:   # escapes in the chunk before the defect's
+                for k in range(pos - 300, pos - 280):
+                    toks[k] = b"0|2"
+            if defect == "len15":
+                toks[pos], toks[pos + 3] = b"1", b"0|1:5"
+            elif defect == "vt":
+                toks[pos] = b"0\x0b1"
+            elif defect == "bs":
+                toks[pos] = b"\x08|1"
+            else:
+                toks[pos] = b"0\t1"
+            lines.append(PFX_V + b"\t".join(toks))
+    want = [G.oracle_encode_line(x) for x in lines]
+    for lead in (0, 3):
+        st, out, ro, err = run(lines, lead)
+        assert err == (1 << 64) - 1
+        for i, (s0, w) in enumerate(want):
+            assert s0 == 0 and out[int(ro[i]):int(ro[i + 1])] == w, (lead, i)
+
+
 @pytest.mark.parametrize("lead", [0, 5])
 def test_unphased_rows_handed_on_and_predicted(lead, monkeypatch):
     """Rows whose first 2 KiB genotype chunk holds 3-byte escapes only

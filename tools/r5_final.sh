@@ -7,7 +7,7 @@
 # 2-rank rehearsals.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
-T=${FINAL_TAG:-r5final4}
+T=${FINAL_TAG:-r5final5}
 bash tools/gpu_check.sh $T smoke tests pmcenc || exit 1
 LAW=2 bash tools/gpu_check.sh $T pmcdev || exit 1
 bash tools/gpu_check.sh $T pmcinstall bench profbench || exit 1

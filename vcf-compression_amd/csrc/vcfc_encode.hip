@@ -281,7 +281,7 @@ struct FastState {
     int32_t gt0;        // line offset of the first sample token (-1: not found yet)
     uint32_t T, phi;    // token count, gt0's byte phase mod 4
     uint32_t pcls, prs; // class / run start(+1) of the previous token
-    uint32_t esc;       // the last genotype chunk held an escape: test the escape shape first
+    uint32_t esc;       // lanes of the last genotype chunk holding an escape: test the escape shape first
     uint32_t hand;      // 1: a first genotype chunk of escapes only hands the row on (deferred records,
                         // > 1 chunk, prefix in the line's first KiB); 2: it did
 };
@@ -694,14 +694,25 @@ __device__ __forceinline__ bool esc8(const uint32_t (&d)[TPL8], int32_t t0, int3
     // {0,1}) iff a and b are '0'/'1' and the separator is '|'.  Class byte =
     // 0x90 + 2a + b, escapes 0x94; an escape's bytes never reach a neighbour.
     uint32_t cbL, cbH, eL, eH;   // eL/eH: 0xFF in the byte of each escape slot
-    uint32_t bad = 0;
-    esc_classes<!EDGE>(d[0], d[1], d[2], d[3], cbL, eL, bad);
-    esc_classes<!EDGE>(d[4], d[5], d[6], d[7], cbH, eH, bad);
+    uint32_t badL = 0, badH = 0;
+    esc_classes<true>(d[0], d[1], d[2], d[3], cbL, eL, badL);
+    esc_classes<true>(d[4], d[5], d[6], d[7], cbH, eH, badH);
     if (!EDGE) {
         uint32_t at = 0;   // byte 3 of every slot a TAB
 #pragma unroll
         for (int j = 0; j < (int)TPL8; j++) at |= d[j] ^ 0x09090909u;
-        if (vw::ballot((bad | (at & 0xFF000000u)) != 0)) return false;
+        if (vw::ballot((badL | badH | (at & 0xFF000000u)) != 0)) return false;
+    } else {
+        // the row's last chunk: only slots t0 + j < T count (the bytes of the
+        // others lie above theirs in each word, so a borrow of theirs cannot
+        // reach a valid byte), and the last token has no TAB after it
+        const int32_t nv = (int32_t)f.T - t0;   // valid slots in the lane
+        const uint32_t vL = nv >= 4 ? 0x80808080u : (nv <= 0 ? 0u : (0x80808080u & ((1u << (8 * nv)) - 1u)));
+        const uint32_t vH = nv >= 8 ? 0x80808080u : (nv <= 4 ? 0u : (0x80808080u & ((1u << (8 * (nv - 4))) - 1u)));
+        uint32_t at = 0;   // byte 3 of every slot but the last valid one a TAB
+#pragma unroll
+        for (int j = 0; j < (int)TPL8; j++) at |= (d[j] ^ 0x09090909u) & (j < nv - 1 ? 0xFF000000u : 0u);
+        if (vw::ballot(((badL & vL) | (badH & vH) | at) != 0)) return false;
     }
     // Round 5: every token of chunk 0 an escape (unphased "0/1", "./."):
     // records ~1.25x the line, so the row goes to k_encode_var, which sizes
@@ -711,7 +722,7 @@ __device__ __forceinline__ bool esc8(const uint32_t (&d)[TPL8], int32_t t0, int3
         f.hand = 2u;
         return false;
     }
-    f.esc = vw::ballot((eL | eH) != 0) != 0;
+    f.esc = (uint32_t)__builtin_popcountll(vw::ballot((eL | eH) != 0));
     if (f.pcls == CLS_NONE) {   // first chunk: see clean8 (an escape token 0 -> class 0: no lead byte)
         f.pcls = vw::readlane(cbL, 0) & 3u;
         f.prs = 1;
@@ -811,42 +822,6 @@ __device__ __forceinline__ bool esc8(const uint32_t (&d)[TPL8], int32_t t0, int3
     return true;
 }
 
-// every slot of the lane is "xyz\t" with x, y, z none of 0x08-0x0B (not TAB,
-// not '\n': a row holding one is the hop index's wrong guess; the other two go
-// the general way) -- the last token: no TAB needed; slots past it ignored
-template <bool EDGE>
-__device__ __forceinline__ bool shape3(const uint32_t (&d)[TPL8], int32_t t0, uint32_t T) {
-    if (!EDGE) {
-        // t = d ^ TABs: byte 3 must be 0 (a TAB) in every slot -- OR them all;
-        // bytes 0..2 must not be (haszero on t with byte 3 forced to 0xFF,
-        // exact for "some byte is zero", OR-accumulated over the slots)
-        uint32_t at = 0, az = 0;
-#pragma unroll
-        for (int j = 0; j < (int)TPL8; j++) {
-            const uint32_t t = d[j] ^ 0x09090909u;
-            const uint32_t u = (t & 0x00FCFCFCu) | 0xFF000000u;
-            at |= t;
-            az |= (u - 0x01010101u) & ~u;
-        }
-        return (at >> 24) != 0 || (az & 0x80808080u) != 0;
-    }
-    bool bad = false;
-#pragma unroll
-    for (int j = 0; j < (int)TPL8; j++) {
-        const uint32_t x = (d[j] ^ 0x09090909u) & 0xFFFCFCFCu;
-        const uint32_t zb = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);   // 0x80 per TAB byte (0x08-0x0B in bytes 0..2)
-        if (EDGE) {
-            const int32_t t = t0 + j;
-            const uint32_t want = (uint32_t)t + 1u == T ? 0u : 0x80000000u;
-            const uint32_t m = (uint32_t)t + 1u == T ? 0x00808080u : 0x80808080u;
-            bad |= (uint32_t)t < T && (zb & m) != want;
-        } else {
-            bad |= zb != 0x80000000u;
-        }
-    }
-    return bad;
-}
-
 // Genotype chunk C (2 KiB) on the skip / clean / escape paths.  false = not
 // handled (nothing written): the chunk needs the general step.
 __device__ __forceinline__ bool gt_step8(const Chunk8 &cur, uint32_t C, FastState &f, Ring &r) {
@@ -900,18 +875,23 @@ __device__ __forceinline__ bool gt_step8(const Chunk8 &cur, uint32_t C, FastStat
         return esc8<false>(d, t0, tf, f, r);   // (its own shape test; false: the general step)
     } else {
         // last chunk: slots past T-1 are ignored; token T-1 has no TAB after it
-        bool bad = false;
+        // (after a chunk with escapes in 4+ lanes the escape shape alone, as in
+        // interior chunks: round 5, law 0 pays no clean test on its rows' last
+        // chunk; a row with a few escapes most likely ends clean)
+        if (f.esc < 4u) {
+            bool bad = false;
 #pragma unroll
-        for (int j = 0; j < (int)TPL8; j++) {
-            const int32_t t = t0 + j;
-            const uint32_t m = (uint32_t)t < T ? ((uint32_t)t + 1u == T ? 0x00FEFFFEu : 0xFFFEFFFEu) : 0u;
-            bad |= ((d[j] ^ Z) & m) != 0;
+            for (int j = 0; j < (int)TPL8; j++) {
+                const int32_t t = t0 + j;
+                const uint32_t m = (uint32_t)t < T ? ((uint32_t)t + 1u == T ? 0x00FEFFFEu : 0xFFFEFFFEu) : 0u;
+                bad |= ((d[j] ^ Z) & m) != 0;
+            }
+            if (pclean && vw::ballot(bad) == 0) {
+                clean8<true>(d, t0, tf, f, r);
+                return true;
+            }
         }
-        if (pclean && vw::ballot(bad) == 0) {
-            clean8<true>(d, t0, tf, f, r);
-            return true;
-        }
-        if (vw::ballot(shape3<true>(d, t0, T)) == 0) return esc8<true>(d, t0, tf, f, r);
+        return esc8<true>(d, t0, tf, f, r);   // (its own shape test; false: the general step)
     }
     return false;   // tokens of another length or empty fields: the caller runs gt_general on this chunk
 }
