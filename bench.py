@@ -10,7 +10,11 @@ step   : one pass of the hot path (reference compress_data_line,
          stitch offsets of the output file).
 scaling: weak (default).  Every rank encodes its own 1M-row shard (rows are
          independent; the shards are contiguous row ranges of one file).
-         --scaling strong: the 1M rows are split over the ranks (1M/N each).
+         With --gpus N > 1 the same process group then also times the
+         strong split of the N=1 line's own 1M-row dataset (1M/N rows per
+         rank, byte-identical slices) and reports it as the line's `strong`
+         object -- BASELINE's fixed-dataset 1/2/4/8-GPU curve.
+         --scaling strong: only the strong split (1M/N rows each).
 value  : GT bytes of all ranks / (max over ranks of the timed wall time).
 
 Also printed: `roofline` for the dominant kernel k_encode (algorithmic bytes
@@ -42,10 +46,15 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--rows", type=int, default=None, help="rows per GPU (default 1M; 100k in --mode biobank)")
     ap.add_argument("--samples", type=int, default=None, help="samples (default 2504; 100k in --mode biobank)")
-    ap.add_argument("--law", type=int, default=1, choices=[0, 1, 2],
-                    help="1 = chr22-shaped (headline), 0 = random_vcf law, 2 = general shapes (SURVEY D3)")
+    ap.add_argument("--law", type=int, default=1, choices=[0, 1, 2, 3],
+                    help="1 = chr22-shaped (headline), 0 = random_vcf law, 2 = general shapes (SURVEY D3), "
+                         "3 = alternating classes (SURVEY D3, the RLE worst case)")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
-                    help="weak: every rank encodes --rows rows; strong: the --rows rows are split over the ranks")
+                    help="weak: every rank encodes --rows rows (with --gpus N > 1 the line also carries the "
+                         "strong split of the N=1 dataset as its 'strong' object); strong: the --rows rows are "
+                         "split over the ranks")
+    ap.add_argument("--no-strong", action="store_true",
+                    help="--gpus N > 1, weak scaling: skip the strong-split sub-measurement")
     ap.add_argument("--cpu-rows", type=int, default=None,
                     help="rows in the CPU-baseline sample (default: about 1.2 GB of lines)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -91,7 +100,8 @@ def parse():
 
 
 def law_name(law):
-    return {0: "random_vcf-law", 1: "chr22-shaped", 2: "general-shapes (chrX haploid/GT:DP:GQ/missing)"}[law]
+    return {0: "random_vcf-law", 1: "chr22-shaped", 2: "general-shapes (chrX haploid/GT:DP:GQ/missing)",
+            3: "alternating-classes (every token a run / het 1/2)"}[law]
 
 
 def cpu_baseline(rows, torch, args):
@@ -965,6 +975,23 @@ def bench_distfile(args):
         dist.destroy_process_group()
 
 
+def strong_summary(per_rank, elapsed, steps, k_ms_rank0, rows_total, workload_name):
+    """The `strong` object of a --gpus N > 1 encode line: the N=1 line's
+    dataset (rows_total rows) split over the ranks.  per_rank: [rows, GT
+    bytes, record bytes] of every rank; elapsed: max over ranks of the K
+    timed steps (barrier + synchronize on both sides)."""
+    rows = [int(r[0]) for r in per_rank]
+    if sum(rows) != rows_total:
+        raise RuntimeError("strong split lost rows: %s != %d" % (rows, rows_total))
+    gt = sum(int(r[1]) for r in per_rank)
+    return {"value": round(gt * steps / elapsed / 1e9, 2), "unit": "GB/s", "scaling": "strong",
+            "ms_per_step": round(elapsed * 1e3 / steps, 4), "rows_total": rows_total, "rows_per_rank": rows,
+            "gt_bytes_total": gt, "record_bytes_total": sum(int(r[2]) for r in per_rank),
+            "k_encode_ms_rank0": round(k_ms_rank0, 4),
+            "dataset": "%s, the N=1 line's %d-row batch (seed 1000) cut into contiguous row ranges, "
+                       "byte-identical to it (workload.DeviceRows rows_of)" % (workload_name, rows_total)}
+
+
 SHARDED_MODES = ("encode", "biobank", "distfile")
 
 
@@ -1088,67 +1115,87 @@ def main():
         init_dist(dist, rehearsal, dev)
     rccl = rccl_report(torch, dist, dev, cdev, world, rehearsal)
     S = args.samples
+    rows_asked = args.rows
+    if rehearsal and args.mode == "encode" and args.scaling == "weak" and world > 4:
+        # all ranks share the one GPU: 1M rows each (~43 GB of HBM per rank)
+        # fit 4 ranks, so the weak phase of a wider rehearsal takes 4M rows
+        # in all; the strong phase splits the full 1M-row dataset as asked
+        args.rows = 4 * rows_asked // world
+    import dist_compress as D
+
+    def phase(n, make_rows):
+        """Encode one n-row batch per rank: W untimed steps, then K steps
+        bracketed by barrier + synchronize; returns the max-over-ranks
+        wall time with the batch, its buffers and the stage timings."""
+        def setup():
+            rows = make_rows()
+            ws_bytes = vcfc.workspace_size(n, rows.line_bytes)
+            cap = vcfc.encode_bound(n, rows.line_bytes)
+            ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+            out = torch.empty(cap, dtype=torch.uint8, device=dev)
+            rec = torch.empty(n + 1, dtype=torch.int64, device=dev)
+            err = torch.empty(1, dtype=torch.int64, device=dev)
+            return rows, ws_bytes, cap, ws, out, rec, err
+        # a rank whose setup fails (out of memory, no device) makes every rank
+        # exit non-zero here, before the first all-gather of shard sizes
+        rows, ws_bytes, cap, ws, out, rec, err = D.setup_all_or_none(
+            rank, lambda v: gather_ints(torch, dist, cdev, world, v), setup)
+        counts = torch.empty(world, dtype=torch.int64, device=cdev)
+        timer = vcfc.StageTimer()
+        stream = torch.cuda.current_stream(dev).cuda_stream
+
+        def step(timed):
+            f = timer.encode if timed else vcfc.encode_rows_device
+            f(rows.buf.data_ptr(), rows.line_off.data_ptr(), rows.line_len.data_ptr(), n, rows.line_bytes,
+              out.data_ptr(), cap, rec.data_ptr(), ws.data_ptr(), ws_bytes, err.data_ptr(), stream)
+            if world > 1:
+                # stitch: every rank learns every shard's record bytes -> its file offset
+                dist.all_gather_into_tensor(counts, rec[n:n + 1].to(cdev))
+
+        for _ in range(args.warmup):
+            step(False)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step(True)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        elapsed = time.perf_counter() - t0
+        stages, calls = timer.read()
+        try:
+            deferred = vcfc.encode_deferred_rows(ws.data_ptr(), n, rows.line_bytes, stream)
+        except RuntimeError:   # (an A/B build of the library without the export)
+            deferred = None
+        if world > 1:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        e = int(err.cpu().numpy().view(np.uint64)[0])
+        if e != vcfc.NO_ERROR:
+            raise RuntimeError("encode reported row error %x" % e)
+        return dict(elapsed=elapsed, stages=stages, calls=calls, deferred=deferred, rows=rows, out=out, rec=rec)
+
     if args.scaling == "strong":
-        # the --rows rows split over the ranks (each rank generates its own
-        # contiguous slice, same law; the total work is fixed)
+        # the --rows rows of the N=1 line's dataset split over the ranks: each
+        # rank generates its contiguous slice of that one batch, byte for byte
+        # (workload.DeviceRows rows_of; the total work is fixed)
         r0, r1 = args.rows * rank // world, args.rows * (rank + 1) // world
+        n = r1 - r0
+        P = phase(n, lambda: workload.DeviceRows(torch, vcfc, n, S, args.law, seed=1000, device=dev,
+                                                 rows_of=(args.rows, r0)))
     else:
         r0, r1 = rank * args.rows, (rank + 1) * args.rows
-    n = r1 - r0
+        n = r1 - r0
+        P = phase(n, lambda: workload.DeviceRows(torch, vcfc, n, S, args.law, seed=1000 + rank, device=dev,
+                                                 row0=r0))
+    elapsed, stages, calls, deferred = P["elapsed"], P["stages"], P["calls"], P["deferred"]
+    rows, out, rec = P["rows"], P["out"], P["rec"]
 
-    def setup():
-        rows = workload.DeviceRows(torch, vcfc, n, S, args.law, seed=1000 + rank, device=dev, row0=r0)
-        ws_bytes = vcfc.workspace_size(n, rows.line_bytes)
-        cap = vcfc.encode_bound(n, rows.line_bytes)
-        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
-        out = torch.empty(cap, dtype=torch.uint8, device=dev)
-        rec = torch.empty(n + 1, dtype=torch.int64, device=dev)
-        err = torch.empty(1, dtype=torch.int64, device=dev)
-        return rows, ws_bytes, cap, ws, out, rec, err
-    # a rank whose setup fails (out of memory, no device) makes every rank
-    # exit non-zero here, before the first all-gather of shard sizes
-    import dist_compress as D
-    rows, ws_bytes, cap, ws, out, rec, err = D.setup_all_or_none(
-        rank, lambda v: gather_ints(torch, dist, cdev, world, v), setup)
-    counts = torch.empty(world, dtype=torch.int64, device=cdev)
-    timer = vcfc.StageTimer()
-    stream = torch.cuda.current_stream(dev).cuda_stream
-
-    def step(timed):
-        f = timer.encode if timed else vcfc.encode_rows_device
-        f(rows.buf.data_ptr(), rows.line_off.data_ptr(), rows.line_len.data_ptr(), n, rows.line_bytes,
-          out.data_ptr(), cap, rec.data_ptr(), ws.data_ptr(), ws_bytes, err.data_ptr(), stream)
-        if world > 1:
-            # stitch: every rank learns every shard's record bytes -> its file offset
-            dist.all_gather_into_tensor(counts, rec[n:n + 1].to(cdev))
-
-    for _ in range(args.warmup):
-        step(False)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    stages, calls = timer.read()
-    try:
-        deferred = vcfc.encode_deferred_rows(ws.data_ptr(), n, rows.line_bytes, stream)
-    except RuntimeError:   # (an A/B build of the library without the export)
-        deferred = None
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    e = int(err.cpu().numpy().view(np.uint64)[0])
-    if e != vcfc.NO_ERROR:
-        raise RuntimeError("encode reported row error %x" % e)
     copy_gbs = measured_copy_gbs(torch, dev)
     out_bytes = int(rec[n].item())
     ms_step = elapsed * 1e3 / args.steps
@@ -1190,6 +1237,21 @@ def main():
                       "parallelism": "row shards x%d, RCCL all-gather of shard sizes" % world},
            "rccl_world": rccl,
            "roofline": roof}
+    if rehearsal and args.rows != rows_asked:
+        res["config"]["rehearsal_rows_per_rank"] = args.rows
+    if world > 1 and args.mode == "encode" and args.scaling == "weak" and not args.no_strong:
+        # BASELINE's metric is one fixed 2504 x 1M dataset on 1/2/4/8 GPUs:
+        # the same ranks, in the same process group, then time the strong
+        # split of the N=1 line's dataset (rank r: rows [1M r/N, 1M (r+1)/N))
+        del P, rows, out, rec
+        torch.cuda.empty_cache()
+        s0, s1 = rows_asked * rank // world, rows_asked * (rank + 1) // world
+        ns = s1 - s0
+        Q = phase(ns, lambda: workload.DeviceRows(torch, vcfc, ns, S, args.law, seed=1000, device=dev,
+                                                  rows_of=(rows_asked, s0)))
+        per_rank = gather_ints(torch, dist, cdev, world, [ns, Q["rows"].gt_bytes, int(Q["rec"][ns].item())])
+        res["strong"] = strong_summary(per_rank, Q["elapsed"], args.steps,
+                                       Q["stages"]["k_encode"] / max(Q["calls"], 1), rows_asked, law_name(args.law))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb, cpu_out, k = cpu_baseline(rows, torch, args)
         res["cpu_baseline"] = cb

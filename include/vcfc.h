@@ -42,6 +42,11 @@ extern "C" {
 #define VCFC_E_HIP 6       /* HIP runtime error / no GPU */
 #define VCFC_E_IO 7        /* file open/read/write failed */
 #define VCFC_E_FORMAT 8    /* malformed .vcfc input (decoder) */
+/* a data line longer than VCFC_MAX_LINE bytes: its record could pass the
+ * 30-bit LEN header (LineLengthHeader's 2^30 - 1, reference
+ * src/utils.hpp:140-160), which the reference would silently truncate */
+#define VCFC_E_TOOLONG 10
+#define VCFC_MAX_LINE ((1u << 29) - 64u)
 
 const char *vcfc_version(void);
 const char *vcfc_strerror(int status);
@@ -112,6 +117,10 @@ uint64_t vcfc_encode_workspace_size(uint64_t n_rows, uint64_t total_line_bytes);
  *                    where total >= sum of d_line_len
  *   d_err            one uint64: ~0 = success, else (row << 8 | status) of the
  *                    first failing row (rows before it are valid output)
+ * Output bytes: [0, d_rec_off[n]) hold the records; with deferred records a
+ * call may also write stale bytes into [d_rec_off[n], out_cap) (records
+ * placed on predicted offsets before a misprediction is found), never past
+ * out_cap -- several batches that share one buffer go in row order.
  * Returns VCFC_OK if the work was enqueued.  Capturable in a hipGraph: the
  * per-call state is reset by a kernel, not by hipMemsetAsync -- on this ROCm
  * a captured 24-byte memset node writes garbage into its first 16 bytes from
@@ -128,8 +137,8 @@ int vcfc_encode_rows_device(const uint8_t *d_buf, const uint64_t *d_line_off,
 /* Rows the last vcfc_encode_rows_device call on workspace d_ws (sized for
  * n, total_line_bytes) deferred and wrote straight into the output (see
  * vcfc_ctx_set_deferred_records; a row whose predicted size led there but
- * whose later bytes sent it to the general path is not counted); waits for
- * `stream`. */
+ * whose later bytes sent it to the general path, or that held a '\n' or
+ * failed, is not counted); waits for `stream`. */
 int vcfc_encode_deferred_rows(const void *d_ws, uint64_t n_rows, uint64_t total_line_bytes, void *stream,
                               uint64_t *rows);
 
@@ -327,6 +336,11 @@ int vcfc_sparse_plan_device(const uint8_t *d_recs, const uint64_t *d_rec_off, ui
  *       reference other/random_vcf.py:66-70)
  *   1 = chr22-shaped (per-row alt-allele frequency from d_row_af; ~1% of
  *       rows multi-allelic)
+ *   2 = general shapes (d_row_af = kind + allele frequency: haploid,
+ *       GT:DP:GQ, missing, unphased; vcf-compression_amd/workload.py)
+ *   3 = alternating classes, the RLE worst case (d_row_af = kind: 0 = the
+ *       classes 0|0 0|1 1|0 1|1 cycling, every token a new run; 1 = alleles
+ *       i.i.d. at frequency 1/2)
  * The prefix (9 columns + '\t') of row i is copied from
  * d_prefix[d_prefix_off[i] .. d_prefix_off[i+1]); row i is written at
  * d_buf + d_line_off[i] with S tokens and a trailing '\n'. */
@@ -334,6 +348,13 @@ int vcfc_synth_rows_device(uint8_t *d_buf, const uint64_t *d_line_off, uint64_t 
                            const uint8_t *d_prefix, const uint64_t *d_prefix_off,
                            const float *d_row_af, uint32_t samples, int law, uint64_t seed,
                            void *stream);
+/* The same rows as rows [row_base, row_base + n) of a batch generated whole
+ * with this seed (the genotypes hash the batch row index): a rank generates
+ * its slice of one fixed dataset (bench.py's strong split). */
+int vcfc_synth_rows_device_at(uint8_t *d_buf, const uint64_t *d_line_off, uint64_t n,
+                              const uint8_t *d_prefix, const uint64_t *d_prefix_off,
+                              const float *d_row_af, uint32_t samples, int law, uint64_t seed,
+                              uint64_t row_base, void *stream);
 
 /* Per-record 64-bit digests of an encoded batch, in place on the GPU:
  * d_hash[i] = digest of d_recs[d_rec_off[i] .. d_rec_off[i+1]).  Digest:

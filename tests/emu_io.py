@@ -40,7 +40,7 @@ def lib():
                                           ctypes.POINTER(ctypes.c_int64), u64, u64, ctypes.c_int,
                                           ctypes.POINTER(u64)]
         L.emu_line_index.argtypes = [ctypes.c_char_p, u64, ctypes.c_uint32, vp, vp, u64, vp, u64]
-        L.emu_synth.argtypes = [vp, vp, u64, vp, vp, vp, ctypes.c_uint32, ctypes.c_int, u64]
+        L.emu_synth.argtypes = [vp, vp, u64, vp, vp, vp, ctypes.c_uint32, ctypes.c_int, u64, u64]
         _lib = L
     return _lib
 
@@ -209,13 +209,21 @@ def emu_line_index(vcf, S_hint=0, hop_walkers=0):
     return [int(c) for c in cnt], off[:k].tolist(), ln[:k].tolist()
 
 
-def emu_synth_rows(n, samples, law, seed, row0=0):
+def emu_synth_rows(n, samples, law, seed, row0=0, rows_of=None):
     """vcf-compression_amd/workload.py's synthetic rows generated by the
-    product generator kernel on the emulator: (buf, line_off, line_len)."""
+    product generator kernel on the emulator: (buf, line_off, line_len).
+    rows_of = (n_total, lo): rows [lo, lo + n) of the n_total-row batch
+    (workload.DeviceRows' slices)."""
     import sys
     sys.path.insert(0, os.path.join(REPO, "vcf-compression_amd"))
     import workload
-    blob, poff, af, _, gt_len = workload.prefixes(n, law, seed, row0, samples)
+    if rows_of is None:
+        blob, poff, af, _, gt_len = workload.prefixes(n, law, seed, row0, samples)
+        row_base = 0
+    else:
+        blob, poff, af, _, gt_len = workload.slice_prefixes(rows_of[0], rows_of[1], rows_of[1] + n, law, seed,
+                                                             samples)
+        row_base = rows_of[1]
     line_off, line_len, total = workload.layout(poff, samples, gt_len)
     buf = np.zeros(total + 64, dtype=np.uint8)
     pre = np.frombuffer(blob, dtype=np.uint8).copy()
@@ -223,5 +231,5 @@ def emu_synth_rows(n, samples, law, seed, row0=0):
     po = np.ascontiguousarray(poff, dtype=np.uint64)
     afp = af.ctypes.data if af is not None else None
     assert lib().emu_synth(buf.ctypes.data, lo.ctypes.data, n, pre.ctypes.data, po.ctypes.data, afp, samples, law,
-                           seed) == 0
+                           seed, row_base) == 0
     return buf[:total], lo, np.ascontiguousarray(line_len, dtype=np.uint32)

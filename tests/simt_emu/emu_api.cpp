@@ -212,10 +212,11 @@ extern "C" int emu_record_hash(const uint8_t *recs, const uint64_t *rec_off, uin
 // Synthetic rows (csrc/vcfc_synth.hip) on the emulator.
 hipError_t vcfc_synth_device(uint8_t *buf, const uint64_t *line_off, uint64_t n, const uint8_t *prefix,
                              const uint64_t *prefix_off, const float *row_af, uint32_t S, int law,
-                             uint64_t seed, hipStream_t s);
+                             uint64_t seed, uint64_t row_base, hipStream_t s);
 extern "C" int emu_synth(uint8_t *buf, const uint64_t *line_off, uint64_t n, const uint8_t *prefix,
-                         const uint64_t *prefix_off, const float *row_af, uint32_t S, int law, uint64_t seed) {
-    return (int)vcfc_synth_device(buf, line_off, n, prefix, prefix_off, row_af, S, law, seed, nullptr);
+                         const uint64_t *prefix_off, const float *row_af, uint32_t S, int law, uint64_t seed,
+                         uint64_t row_base) {
+    return (int)vcfc_synth_device(buf, line_off, n, prefix, prefix_off, row_af, S, law, seed, row_base, nullptr);
 }
 
 // vcfc_ing::Held (the held output of a sharded compress rank): append `n`

@@ -77,3 +77,38 @@ def test_launcher_argv_shape():
     cmd = bench.launcher_argv(8, ["--gpus", "8"], 29511)
     assert cmd[-3:] == [os.path.join(REPO, "bench.py"), "--gpus", "8"]
     assert "--master-port=29511" in cmd
+
+
+def test_strong_summary():
+    """The `strong` object of a --gpus N > 1 encode line: GT bytes of all
+    ranks over the max-rank time, rows per rank summing to the dataset."""
+    import bench
+    per = [[125_000, 1_252_000_000, 85_000_000]] * 8
+    s = bench.strong_summary(per, 0.02, 20, 0.25, 1_000_000, "chr22-shaped")
+    assert s["rows_per_rank"] == [125_000] * 8 and s["gt_bytes_total"] == 8 * 1_252_000_000
+    assert abs(s["value"] - 8 * 1_252_000_000 * 20 / 0.02 / 1e9) < 0.01 and s["ms_per_step"] == 1.0
+    assert s["scaling"] == "strong" and s["unit"] == "GB/s"
+    try:
+        bench.strong_summary(per[:7], 0.02, 20, 0.25, 1_000_000, "x")
+    except RuntimeError:
+        pass
+    else:
+        raise AssertionError("lost rows accepted")
+
+
+def test_rehearsal_line_carries_weak_and_strong():
+    """profiles/r06/bench_n8_rehearsal.json: the driver's `python bench.py
+    --gpus 8` path rehearsed on one GPU (8 gloo ranks on cuda:0,
+    VCFC_BENCH_REHEARSAL=1): one JSON line holding the weak value and the
+    strong split of the N=1 dataset (8 x 125k rows)."""
+    p = os.path.join(REPO, "profiles", "r06", "bench_n8_rehearsal.json")
+    if not os.path.exists(p):
+        import pytest
+        pytest.skip("no rehearsal record yet")
+    line = [x for x in open(p).read().splitlines() if x.startswith("{")][-1]
+    d = json.loads(line)
+    assert d["n_gpus"] == 8 and d["scaling"] == "weak" and d["value"] > 0
+    assert d["rccl_world"]["world"] == 8
+    st = d["strong"]
+    assert st["rows_total"] == 1_000_000 and st["rows_per_rank"] == [125_000] * 8 and st["value"] > 0
+    assert st["gt_bytes_total"] == 2504 * 4 * 1_000_000

@@ -115,8 +115,8 @@ def _device_encode(torch, vcfc, rows):
 
 
 @pytest.mark.parametrize("law,samples,n", [(0, 2504, 3000), (1, 2504, 3000), (0, 100, 20000), (1, 5003, 700),
-                                           (2, 2504, 3000), (2, 100, 20000), (2, 7, 5000),
-                                           (1, 100_000, 48), (0, 100_000, 24)])   # last two: configs[3] rows
+                                           (2, 2504, 3000), (2, 100, 20000), (2, 7, 5000), (3, 2504, 3000),
+                                           (3, 5, 4000), (1, 100_000, 48), (0, 100_000, 24)])   # last two: configs[3] rows
 def test_synthetic_rows_all_vs_oracle(torch, vcfc, law, samples, n):
     import workload
     rows = workload.DeviceRows(torch, vcfc, n, samples, law, seed=7 + law, device="cuda:0")
@@ -417,3 +417,42 @@ def test_deferred_records_chosen_per_row(torch, vcfc, monkeypatch, law, kind):
         assert gdg + unph == 0
     else:
         assert 0 < gdg < n and 0 < unph < n
+
+
+def test_line_longer_than_the_length_header_is_refused(torch, vcfc):
+    """a data line over VCFC_MAX_LINE (2^29 - 64 bytes) could give
+    a record past the 30-bit LEN header (reference src/utils.hpp:140-160) and
+    past the rec_size flag bits: the encode reports VCFC_E_TOOLONG at that
+    row (the rows before it are valid output) instead of a wrong record."""
+    import workload
+    small = workload.DeviceRows(torch, vcfc, 3, 50, 1, seed=3, device="cuda:0")
+    lines = small.host_lines(range(3))
+    big = lines[0] + b"\t0|0" * ((vcfc.MAX_LINE - len(lines[0])) // 4 + 1)
+    assert len(big) > vcfc.MAX_LINE
+    rows = [lines[0], lines[1], big, lines[2]]
+    buf = bytearray()
+    offs, lens = [], []
+    for ln in rows:
+        offs.append(len(buf))
+        lens.append(len(ln))
+        buf += ln + b"\n"
+    dev = torch.device("cuda:0")
+    d_buf = torch.from_numpy(np.frombuffer(bytes(buf), dtype=np.uint8).copy()).to(dev)
+    d_off = torch.tensor(offs, dtype=torch.int64, device=dev)
+    d_len = torch.tensor(lens, dtype=torch.int32, device=dev)
+    n, total = 4, sum(lens)
+    ws_bytes = vcfc.workspace_size(n, total)
+    cap = vcfc.encode_bound(n, total)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    out = torch.empty(cap, dtype=torch.uint8, device=dev)
+    rec = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    err = torch.empty(1, dtype=torch.int64, device=dev)
+    vcfc.encode_rows_device(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, total, out.data_ptr(), cap,
+                            rec.data_ptr(), ws.data_ptr(), ws_bytes, err.data_ptr(),
+                            torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    e = int(err.cpu().numpy().view(np.uint64)[0])
+    assert e == (2 << 8) | vcfc.E_TOOLONG
+    r = rec.cpu().numpy()
+    host = out[:int(r[2])].cpu().numpy().tobytes()
+    assert host == G.oracle_encode_line(lines[0])[1] + G.oracle_encode_line(lines[1])[1]

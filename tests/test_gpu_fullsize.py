@@ -40,7 +40,7 @@ def threads():
     return int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
 
 
-@pytest.mark.parametrize("law", [1, 0, 2])
+@pytest.mark.parametrize("law", [1, 0, 2, 3])   # 3: alternating classes, the RLE worst case
 def test_full_batch_every_record_and_round_trip(torch, vcfc, law):
     import workload
     from test_gpu_encode import _device_encode

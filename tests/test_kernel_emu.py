@@ -630,7 +630,8 @@ def test_predicted_deferred_records_random_batches(seed, monkeypatch):
         assert out1[:int(ro0[bad])] == out0[:int(ro0[bad])]
 
 
-@pytest.mark.parametrize("case", ["ntok", "mixed_later", "general_later", "long_then_plain", "cap", "newline"])
+@pytest.mark.parametrize("case", ["ntok", "mixed_later", "general_later", "long_then_plain", "cap",
+                                  "cap_underpredicted", "cap_general", "newline"])
 def test_mispredicted_deferred_records(case, monkeypatch):
     """Predictions that are wrong: another token count (a row with one
     sample more), plain tokens after a first chunk of 1-byte escapes (the
@@ -665,6 +666,26 @@ def test_mispredicted_deferred_records(case, monkeypatch):
         (st0, out0, ro0, err0), (st1, out1, ro1, err1) = _encode_both(lines, monkeypatch, cap)
         assert err0 == err1 == (9 << 8) | 4
         assert out1[:int(ro0[9])] == out0[:int(ro0[9])]
+        return
+    if case in ("cap_underpredicted", "cap_general"):
+        # a predicted row at the out_cap cut whose prediction is
+        # short of its record (one sample more: predicted one byte short) or
+        # that is really a general-path row, behind an over-predicted row
+        # (1-byte escapes then plain tokens).  Pass 1 cannot write it, so it
+        # must size it: the exact layout then reports NOSPACE at that row and
+        # nothing lands past out_cap (emu_encode asserts it).
+        lines[3] = PFX_V + b"\t".join([rnd.choice([b"0", b"1", b"."]) for _ in range(1100)] +
+                                      [rnd.choice([b"0|0", b"0|1"]) for _ in range(400)])
+        lines[9] = (_gdg(rnd, 701) if case == "cap_underpredicted" else
+                    PFX_V + b"\t".join([b"0|1:33:99"] * 300 + [b"0|1:3:99"] * 2 + [b"0|1:33:99"] * 398))
+        (st0, out0, ro0, err0), _ = _encode_both(lines, monkeypatch)
+        assert err0 == (1 << 64) - 1
+        for cut in (int(ro0[10]) - 1, int(ro0[9]) + 1, int(ro0[10])):
+            (st0, out0, r0, e0), (st1, out1, r1, e1) = _encode_both(lines, monkeypatch, cut)
+            assert e1 == e0, cut
+            bad = e0 >> 8 if e0 != (1 << 64) - 1 else len(lines)
+            assert e0 == (1 << 64) - 1 or bad in (9, 10)
+            assert out1[:int(r0[bad])] == out0[:int(r0[bad])]
         return
     (st0, out0, ro0, err0), (st1, out1, ro1, err1) = _encode_both(lines, monkeypatch)
     assert E.last_mispredict() == 1

@@ -50,6 +50,15 @@ for s in $STEPS; do
          done ;;
     distfile) timeout -k 10 600 python bench.py --mode distfile --steps 3 --warmup 1 > "$O/bench_distfile.json" 2> "$O/bench_distfile.err" || { echo "distfile failed"; tail -30 "$O/bench_distfile.err"; exit 1; } ; cat "$O/bench_distfile.json" ;;
     distfile2) VCFC_BENCH_REHEARSAL=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29621 bench.py --gpus 2 --mode distfile --steps 3 --warmup 1 --dist-dir /tmp/vcfc_distfile2 > "$O/bench_distfile2.json" 2> "$O/bench_distfile2.err" || { echo "distfile2 failed"; tail -30 "$O/bench_distfile2.err"; exit 1; } ; cat "$O/bench_distfile2.json" ;;
+    bench3) timeout -k 10 600 python bench.py --law 3 > "$O/bench_law3.json" 2> "$O/bench_law3.err" || { echo "bench3 failed"; tail -30 "$O/bench_law3.err"; exit 1; } ; cat "$O/bench_law3.json" ;;
+    pmcenc3) # encoder HBM bytes per launch for law 3 -> pmc_k_encode_law3.json
+         for P in FETCH_SIZE WRITE_SIZE; do
+           (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc $P --kernel-trace --output-format csv -d "$O/pmcenc_l3_$P" -o run -- python3 "$R/bench.py" --law 3 --steps 3 --warmup 1 --no-cpu-baseline > "$O/pmcenc_l3_$P.log" 2>&1) || { echo "pmcenc3 $P failed rc=$?"; tail -30 "$O/pmcenc_l3_$P.log"; exit 1; }
+         done
+         python3 tools/pmc_encode_json.py "$O/pmcenc_l3_FETCH_SIZE" "$O/pmcenc_l3_WRITE_SIZE" "alternating-classes (every token a run / het 1/2)/2504x1000000" "$O/pmc_k_encode_law3.json" "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes (tools/gpu_check.sh pmcenc3, run $TAG)" > /dev/null || { echo "pmc3 json failed"; exit 1; } ;;
+    prof3) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof3" -o run -- python3 "$R/bench.py" --law 3 --steps 10 --warmup 2 --no-cpu-baseline > "$O/prof3.log" 2>&1) || { echo "prof3 failed rc=$?"; tail -30 "$O/prof3.log"; exit 1; } ;;
+    rehearse8) # exactly the driver's `python bench.py --gpus 8` path, 8 gloo ranks on the one GPU
+         VCFC_BENCH_REHEARSAL=1 timeout -k 10 900 python bench.py --gpus 8 --steps 5 --warmup 1 --no-cpu-baseline > "$O/bench_n8_rehearsal.json" 2> "$O/bench_n8_rehearsal.err" || { echo "rehearse8 failed"; tail -30 "$O/bench_n8_rehearsal.err"; exit 1; } ; cat "$O/bench_n8_rehearsal.json" ;;
     bench2) timeout -k 10 600 python bench.py --law 2 --no-cpu-baseline > "$O/bench_law2.json" 2> "$O/bench_law2.err" || { echo "bench2 failed"; tail -30 "$O/bench_law2.err"; exit 1; } ; cat "$O/bench_law2.json" ;;
     prof2) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof2" -o run -- python3 "$R/bench.py" --law 2 --steps 10 --warmup 2 --no-cpu-baseline > "$O/prof2.log" 2>&1) || { echo "prof2 failed rc=$?"; tail -30 "$O/prof2.log"; exit 1; } ;;
     pmc2) for P in FETCH_SIZE WRITE_SIZE; do

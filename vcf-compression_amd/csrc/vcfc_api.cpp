@@ -25,7 +25,7 @@ hipError_t vcfc_sparse_plan_launch(const uint8_t *recs, const uint64_t *rec_off,
                                    uint64_t *file_off, uint8_t *prefix, uint64_t *status, hipStream_t s);
 hipError_t vcfc_synth_device(uint8_t *buf, const uint64_t *line_off, uint64_t n, const uint8_t *prefix,
                              const uint64_t *prefix_off, const float *row_af, uint32_t S, int law,
-                             uint64_t seed, hipStream_t s);
+                             uint64_t seed, uint64_t row_base, hipStream_t s);
 
 namespace {
 
@@ -241,6 +241,7 @@ const char *vcfc_strerror(int s) {
     case VCFC_E_HIP: return "HIP runtime error (is a gfx950 GPU visible?)";
     case VCFC_E_IO: return "file I/O error";
     case VCFC_E_FORMAT: return "malformed .vcfc input";
+    case VCFC_E_TOOLONG: return "VCF data line too long (its record could pass the 30-bit length header)";
     default: return "unknown status";
     }
 }
@@ -399,14 +400,22 @@ int vcfc_timer_read(vcfc_timer *t, double ms[4], uint64_t *calls) {
     return VCFC_OK;
 }
 
-int vcfc_synth_rows_device(uint8_t *d_buf, const uint64_t *d_line_off, uint64_t n, const uint8_t *d_prefix,
-                           const uint64_t *d_prefix_off, const float *d_row_af, uint32_t samples, int law,
-                           uint64_t seed, void *stream) {
+int vcfc_synth_rows_device_at(uint8_t *d_buf, const uint64_t *d_line_off, uint64_t n, const uint8_t *d_prefix,
+                              const uint64_t *d_prefix_off, const float *d_row_af, uint32_t samples, int law,
+                              uint64_t seed, uint64_t row_base, void *stream) {
     if (n && (!d_buf || !d_line_off || !d_prefix || !d_prefix_off)) return VCFC_E_ARG;
-    return vcfc_synth_device(d_buf, d_line_off, n, d_prefix, d_prefix_off, d_row_af, samples, law, seed,
+    if (law < 0 || law > 3 || (law >= 2 && n && !d_row_af)) return VCFC_E_ARG;
+    return vcfc_synth_device(d_buf, d_line_off, n, d_prefix, d_prefix_off, d_row_af, samples, law, seed, row_base,
                              static_cast<hipStream_t>(stream)) == hipSuccess
                ? VCFC_OK
                : VCFC_E_HIP;
+}
+
+int vcfc_synth_rows_device(uint8_t *d_buf, const uint64_t *d_line_off, uint64_t n, const uint8_t *d_prefix,
+                           const uint64_t *d_prefix_off, const float *d_row_af, uint32_t samples, int law,
+                           uint64_t seed, void *stream) {
+    return vcfc_synth_rows_device_at(d_buf, d_line_off, n, d_prefix, d_prefix_off, d_row_af, samples, law, seed, 0,
+                                     stream);
 }
 
 // Host batch: copy in, encode, copy out.  Synchronous on the context stream.

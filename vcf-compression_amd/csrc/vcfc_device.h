@@ -29,6 +29,11 @@
 // a deferred record came out another size than it was sized (cannot happen;
 // reported as VCFC_E_HIP, a device failure)
 #define VCFCD_E_INTERNAL 6
+// a line longer than VCFCD_MAX_LINE (include/vcfc.h VCFC_E_TOOLONG): records
+// stay below 2^30 bytes, the LEN header's range, so that every rec_size flag
+// below (VCFCD_RETRY_GT, VCFCD_DEFER: the top two bits) is free of sizes
+#define VCFCD_E_TOOLONG 10
+#define VCFCD_MAX_LINE ((1u << 29) - 64u)
 
 // error word: min over failing rows of (row << 8 | code); ~0 = no error
 #define VCFCD_NO_ERROR (~0ull)
@@ -83,7 +88,7 @@ struct VcfcEncodeArgs {
     // k_encode_defer's first pass checks every record against its size):
     uint32_t *mispredict;      // nonzero: some record's size was wrong -- the size scan, compaction and
                                // deferred writes run again on the exact sizes (gated launches)
-    uint32_t *defer_fallback;  // deferred rows that turned out not to be variable-token rows (general path)
+    uint32_t *defer_fallback;  // deferred rows not written straight to out: the general path after all, a '\n', the cap
     uint64_t *nospace;         // the first size scan's out_cap report (row << 8 | VCFCD_E_NOSPACE),
                                // merged into err unless the scan runs again
     uint8_t *lb;               // look-back scan state (tickets, tile flags; zeroed per encode)

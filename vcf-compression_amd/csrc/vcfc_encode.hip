@@ -1815,10 +1815,12 @@ __device__ __forceinline__ bool row_setup(const VcfcEncodeArgs &a, uint64_t row,
     r.wpos = 8;
     r.fpos = 0;
     r.mode = RING_STAGE;
-    if (a.slot_off[row + 1] > a.slots_cap) {
+    const uint32_t st = a.line_len[row] > VCFCD_MAX_LINE ? VCFCD_E_TOOLONG
+                        : a.slot_off[row + 1] > a.slots_cap ? VCFCD_E_NOSPACE : VCFCD_OK;
+    if (st != VCFCD_OK) {
         if (vw::lane_id() == 0) {
             a.rec_size[row] = 0;
-            atomicMin((unsigned long long *)a.err, (unsigned long long)((row << 8) | VCFCD_E_NOSPACE));
+            atomicMin((unsigned long long *)a.err, (unsigned long long)((row << 8) | st));
         }
         return false;
     }
@@ -1898,9 +1900,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
     // rows all hold one token per sample; a wrong guess costs the batch a
     // second size scan, compaction and deferred pass, never wrong output)
     uint32_t ntok_ref = 0, ntok_last = ~0u;
+#ifdef VCFC_AB_VAR_PREFETCH
+    uint32_t pfv = 0;
+#endif
     while (todo) {
         const uint64_t row = row0 + (uint64_t)__builtin_ctzll(todo);
         todo &= todo - 1;
+#ifdef VCFC_AB_VAR_PREFETCH
+        // the next flagged row's first 8 KiB towards L2 while this row
+        // computes: one dword per 128-byte line per lane (its value is
+        // consumed a row later, when it has long arrived)
+        asm volatile("" ::"v"(pfv));
+        if (todo) {
+            const uint64_t nrow = row0 + (uint64_t)__builtin_ctzll(todo);
+            const uint8_t *nl = a.buf + a.line_off[nrow];
+            const uint8_t *nb = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(nl) & ~(uintptr_t)127);
+            const uint32_t nspan = (uint32_t)(nl - nb) + a.line_len[nrow];
+            pfv = vw::bload4(vw::make_rsrc(nb, nspan), 128u * l);
+        }
+#endif
         Ring r;
         if (!row_setup(a, row, lds + wave * RING_STRIDE, r)) continue;
         // a.nl_check (the hop line index guessed line ends): a row holding a
@@ -1993,11 +2011,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
         const uint32_t size = rsz & ~VCFCD_DEFER;
         const uint32_t len = a.line_len[row];
         const uint64_t o = a.rec_off[row];
-        if (PASS == 1 && o + (uint64_t)len + (len >> 1) + 16u > a.out_cap) {
-            miss();   // (pass 2, on exact offsets, or the exact size scan's out_cap report)
+        // pass 1, a record not certainly inside out_cap (its offset may rest
+        // on predictions): sized only, never written, so that the exact
+        // layout (pass 2) rests on its true size or its true fate (general
+        // path, '\n') -- a prediction kept here could be short of the record
+        // pass 2 then writes (a write past out_cap)
+        const bool capx = PASS == 1 && o + (uint64_t)len + (len >> 1) + 16u > a.out_cap;
+        if (PASS == 2 && o + size > a.out_cap) {   // (the size scan reported it)
+            if (l == 0) atomicAdd(a.defer_fallback, 1u);   // (not written: not counted as deferred)
             continue;
         }
-        if (o + size > a.out_cap) continue;   // (pass 2: the size scan reported it)
         Ring r;
         r.lds = lds + wave * RING_STRIDE;
         r.prim = a.out + o;
@@ -2005,7 +2028,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
         r.pb = 0xFFFFFFFFu;
         r.wpos = 8;
         r.fpos = 0;
-        r.mode = RING_DIRECT;
+        r.mode = capx ? RING_SIZE : RING_DIRECT;
         uint32_t bytes = 0;
         bool nlhit = false, deferred = false;
         const bool ok = encode_var<VAR_DIRECT>(a.buf + a.line_off[row], len, r, &bytes, PASS == 1 && a.nl_check,
@@ -2015,9 +2038,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
                 atomicMin((unsigned long long *)a.err, (unsigned long long)((row << 8) | VCFCD_E_INTERNAL));
             continue;
         }
-        if (ok && bytes == size) continue;
-        miss();
-        if (ok) {   // a predicted size was wrong
+        if (ok && bytes == size && !capx) continue;
+        miss();   // (a wrong size, another fate, or the cap: pass 2 on exact offsets)
+        if (ok) {   // the exact size (a predicted one may have been wrong)
             if (l == 0) a.rec_size[row] = bytes | VCFCD_DEFER;
             continue;
         }
@@ -2025,6 +2048,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
         if (!nl && a.nl_check) nl = row_has_nl(a.buf + a.line_off[row], len);
         if (nl) {   // (as k_encode_var: the caller indexes the lines again)
             if (l == 0) {
+                atomicAdd(a.defer_fallback, 1u);
                 a.rec_size[row] = 0;
                 atomicMin((unsigned long long *)a.err, (unsigned long long)((row << 8) | VCFCD_E_NEWLINE));
             }

@@ -37,19 +37,26 @@ __device__ __forceinline__ uint32_t law2_len(uint32_t kind, uint32_t j) {
 }
 
 // one wave per row: prefix copy + S tokens separated by TABs + '\n'.
-// laws 0/1: every token "a|b"; law 2: row_af[row] = kind + allele frequency
+// laws 0/1: every token "a|b"; law 2: row_af[row] = kind + allele frequency;
+// law 3 (the RLE worst case): row_af[row] = kind, 0 = the
+// classes 0|0 0|1 1|0 1|1 cycling (every token starts a run), 1 = alleles
+// i.i.d. at frequency 1/2 (het-heavy: runs of 4/3 tokens on average).
+// Genotypes hash (seed, row_base + row, sample): a batch generated as row
+// slices with their row_base equals the batch generated whole.
 __global__ __launch_bounds__(256) void k_synth(uint8_t *buf, const uint64_t *line_off, uint64_t n,
                                                const uint8_t *prefix, const uint64_t *prefix_off,
-                                               const float *row_af, uint32_t S, int law, uint64_t seed) {
-    const uint64_t row = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (row >= n) return;
+                                               const float *row_af, uint32_t S, int law, uint64_t seed,
+                                               uint64_t row_base) {
+    const uint64_t lrow = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (lrow >= n) return;
+    const uint64_t row = row_base + lrow;   // (the genotype hash's row)
     const uint32_t l = vw::lane_id();
-    uint8_t *dst = buf + line_off[row];
-    const uint64_t p0 = prefix_off[row], p1 = prefix_off[row + 1];
+    uint8_t *dst = buf + line_off[lrow];
+    const uint64_t p0 = prefix_off[lrow], p1 = prefix_off[lrow + 1];
     const uint32_t P = (uint32_t)(p1 - p0);
     for (uint32_t i = l; i < P; i += 64) dst[i] = prefix[p0 + i];
     uint8_t *g = dst + P;
-    float af = row_af ? row_af[row] : 0.0f;
+    float af = row_af ? row_af[lrow] : 0.0f;
     if (law == 2) {
         const uint32_t kind = (uint32_t)af;
         af -= (float)kind;
@@ -82,9 +89,16 @@ __global__ __launch_bounds__(256) void k_synth(uint8_t *buf, const uint64_t *lin
         }
         return;
     }
+    const uint32_t cyc = law == 3 && af < 0.5f ? (uint32_t)(row & 3u) : 4u;   // law 3 kind 0: the phase
+    if (law == 3) af = 0.5f;
     for (uint32_t j = l; j < S; j += 64) {
         const uint64_t h = mix64(seed ^ mix64(row * 0x100000001B3ull + j));
-        const uint32_t a1 = allele((uint32_t)h, law, af), a2 = allele((uint32_t)(h >> 32), law, af);
+        uint32_t a1 = allele((uint32_t)h, law == 3 ? 1 : law, af), a2 = allele((uint32_t)(h >> 32), law == 3 ? 1 : law, af);
+        if (cyc < 4u) {   // 0|0 0|1 1|0 1|1 0|0 ...
+            const uint32_t c = (cyc + j) & 3u;
+            a1 = c >> 1;
+            a2 = c & 1u;
+        }
         g[4 * j + 0] = (uint8_t)('0' + a1);
         g[4 * j + 1] = (uint8_t)'|';
         g[4 * j + 2] = (uint8_t)('0' + a2);
@@ -96,9 +110,9 @@ __global__ __launch_bounds__(256) void k_synth(uint8_t *buf, const uint64_t *lin
 
 hipError_t vcfc_synth_device(uint8_t *buf, const uint64_t *line_off, uint64_t n, const uint8_t *prefix,
                              const uint64_t *prefix_off, const float *row_af, uint32_t S, int law,
-                             uint64_t seed, hipStream_t s) {
+                             uint64_t seed, uint64_t row_base, hipStream_t s) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_synth, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, buf, line_off, n, prefix,
-                       prefix_off, row_af, S, law, seed);
+                       prefix_off, row_af, S, law, seed, row_base);
     return hipGetLastError();
 }

@@ -23,13 +23,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("VCFC_LIB") or os.path.join(ROOT, "build", "libvcfc.so")
 
 OK, E_LT8COLS, E_8COLS, E_HEADER, E_NOSPACE, E_ARG, E_HIP, E_IO, E_FORMAT = range(9)
+E_TOOLONG = 10   # a data line longer than MAX_LINE (include/vcfc.h VCFC_E_TOOLONG)
+MAX_LINE = (1 << 29) - 64
 NO_ERROR = (1 << 64) - 1
 
 EXPORTS = [
     "vcfc_version", "vcfc_strerror", "vcfc_ctx_create", "vcfc_ctx_destroy",
     "vcfc_compress_data_line", "vcfc_encode_bound", "vcfc_encode_workspace_size",
     "vcfc_encode_rows_device", "vcfc_encode_rows", "vcfc_compress_file",
-    "vcfc_compress_bound", "vcfc_compress_buffer", "vcfc_synth_rows_device",
+    "vcfc_compress_bound", "vcfc_compress_buffer", "vcfc_synth_rows_device", "vcfc_synth_rows_device_at",
     "vcfc_timer_create", "vcfc_timer_destroy", "vcfc_encode_rows_device_timed", "vcfc_timer_read",
     "vcfc_sparse_offset", "vcfc_sparsify_file", "vcfc_sparse_plan_device",
     "vcfc_decompress_buffer", "vcfc_decompress_file", "vcfc_decode_workspace_size",
@@ -119,6 +121,7 @@ def lib():
     L.vcfc_decode_workspace_size.argtypes = [u64]
     L.vcfc_decode_records_device.argtypes = [vp, u64, vp, u64, u64, vp, u64, vp, vp, u64, vp, ctypes.c_int, vp]
     L.vcfc_synth_rows_device.argtypes = [vp, vp, u64, vp, vp, vp, u32, ctypes.c_int, u64, vp]
+    L.vcfc_synth_rows_device_at.argtypes = [vp, vp, u64, vp, vp, vp, u32, ctypes.c_int, u64, u64, vp]
     pu64 = ctypes.POINTER(u64)
     L.vcfc_parse_query.argtypes = [ctypes.c_char_p, u64, pu64, ctypes.POINTER(ctypes.c_int), pu64, pu64]
     L.vcfc_query_buffer.argtypes = [vp, vp, u64, ctypes.c_char_p, u64, ctypes.c_int, u64, u64, vp, u64, pu64]
@@ -555,9 +558,10 @@ def query_match_device(d_in, d_rec_start, n, d_ref, ref_len, has_range, start, e
                                          d_err, stream)
 
 
-def synth_rows_device(d_buf, d_line_off, n, d_prefix, d_prefix_off, d_row_af, samples, law, seed, stream=0):
-    st = lib().vcfc_synth_rows_device(d_buf, d_line_off, n, d_prefix, d_prefix_off, d_row_af, samples,
-                                      law, seed, stream)
+def synth_rows_device(d_buf, d_line_off, n, d_prefix, d_prefix_off, d_row_af, samples, law, seed, stream=0,
+                      row_base=0):
+    st = lib().vcfc_synth_rows_device_at(d_buf, d_line_off, n, d_prefix, d_prefix_off, d_row_af, samples,
+                                         law, seed, row_base, stream)
     raise_for(st)
 
 

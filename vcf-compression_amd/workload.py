@@ -21,6 +21,12 @@ law 2 "general shapes" (SURVEY §8(d) D3): chrX-shaped rows of five kinds,
        samples.  Kinds 0, 1 and 4 have tokens of another length than 3, so the
        encoder's general path takes them; 2 and 3 its escape path.  Per-row
        allele frequencies as law 1.
+law 3 "alternating classes" (the RLE emission's worst
+       case, reference src/compress.cpp:129-170): law-1 prefixes; per row
+       (50/50 %) kind 0 = the classes 0|0 0|1 1|0 1|1 cycling from a
+       per-row phase, so every token starts a new run and the record holds
+       one byte per token, or kind 1 = alleles i.i.d. at frequency 1/2
+       (het-heavy, runs of 4/3 tokens on average).
 
 The 9 leading columns are built on the host; the genotype columns (the
 dominant bytes) are generated on the GPU by vcfc_synth_rows_device.
@@ -105,11 +111,22 @@ def prefixes(n, law, seed, row0=0, samples=2504):
                         % (pos[i], rs[i], BASES[ref[i]], BASES[alt[i]], k[i], afv[i], an, samples, dp[i],
                            p[0], p[1], p[2], p[3], p[4]))
         af = (afv + multi.astype(np.float64)).astype(np.float32)
+        if law == 3:   # the row's kind (0: cycling classes, 1: alleles at 1/2)
+            af = (rng.random(n) < 0.5).astype(np.float32)
     blob = "".join(rows).encode()
     plen = np.fromiter((len(r) for r in rows), dtype=np.int64, count=n)
     poff = np.zeros(n + 1, dtype=np.int64)
     np.cumsum(plen, out=poff[1:])
     return blob, poff, af, np.asarray(pos, dtype=np.int64), gt_len
+
+
+def slice_prefixes(n_total, lo, hi, law, seed, samples=2504):
+    """prefixes() of rows [lo, hi) of the n_total-row batch (seed, row0 0):
+    one fixed dataset cut into row ranges (bench.py's strong split)."""
+    blob, poff, af, pos, gt_len = prefixes(n_total, law, seed, 0, samples)
+    b0, b1 = int(poff[lo]), int(poff[hi])
+    return (blob[b0:b1], (poff[lo:hi + 1] - b0).astype(np.int64), None if af is None else af[lo:hi].copy(),
+            pos[lo:hi].copy(), None if gt_len is None else np.asarray(gt_len)[lo:hi].copy())
 
 
 def layout(prefix_off, samples, gt_len=None):
@@ -127,9 +144,19 @@ def layout(prefix_off, samples, gt_len=None):
 class DeviceRows:
     """A synthetic batch resident in HBM (torch tensors)."""
 
-    def __init__(self, torch, vcfc, n, samples, law, seed, device, row0=0):
-        blob, poff, af, self.pos, gt_len = prefixes(n, law, seed, row0, samples)
-        self.chrom = {0: "1", 1: "22", 2: "X"}[law]
+    def __init__(self, torch, vcfc, n, samples, law, seed, device, row0=0, rows_of=None):
+        """rows_of = (n_total, lo): rows [lo, lo + n) of the batch that
+        DeviceRows(n_total, samples, law, seed) generates whole, byte for
+        byte (the prefixes of all n_total rows are drawn on the host and cut;
+        the genotypes hash the batch row index)."""
+        if rows_of is None:
+            blob, poff, af, self.pos, gt_len = prefixes(n, law, seed, row0, samples)
+            self.row_base = 0
+        else:
+            blob, poff, af, self.pos, gt_len = slice_prefixes(rows_of[0], rows_of[1], rows_of[1] + n, law, seed,
+                                                              samples)
+            self.row_base = rows_of[1]
+        self.chrom = {0: "1", 1: "22", 2: "X", 3: "22"}[law]
         line_off, line_len, total = layout(poff, samples, gt_len)
         dev = torch.device(device)
         self.n, self.samples, self.law = n, samples, law
@@ -157,7 +184,7 @@ class DeviceRows:
         s = stream if stream is not None else self._torch.cuda.current_stream(self._dev).cuda_stream
         self._vcfc.synth_rows_device(self.buf.data_ptr(), self.line_off.data_ptr(), self.n, d_prefix.data_ptr(),
                                      d_poff.data_ptr(), d_af.data_ptr() if d_af is not None else None,
-                                     self.samples, self.law, seed, s)
+                                     self.samples, self.law, seed, s, row_base=self.row_base)
 
     def host_lines(self, rows):
         """bytes of the given rows (for oracle checks)."""
