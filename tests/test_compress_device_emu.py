@@ -234,3 +234,23 @@ def test_hop_learn_choice():
     lib.emu_data_lines_irregular.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint32]
     assert lib.emu_data_lines_irregular(chr22, len(chr22), S) == 0
     assert lib.emu_data_lines_irregular(law2, len(law2), S) == 1
+
+
+@pytest.mark.parametrize("n_hdr", [1023, 1024, 1500])
+def test_many_header_lines(n_hdr):
+    """Round 6: the host reads the index counts and the first 1 024 '#' line
+    entries in one D2H (k_index_summary), and copies a header that precedes
+    every data line ahead of the encode.  Headers of 1 023 / 1 024 / 1 500
+    lines (the last past the summary: its tables come in a second D2H), one
+    chunk and 4 KiB chunks, a bad header line past entry 1 024."""
+    rnd = random.Random(n_hdr)
+    hdr = b"".join(b"##meta%d=%s\n" % (i, b"x" * rnd.randint(0, 30)) for i in range(n_hdr))
+    S = 40
+    hdr += b"#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\t" + b"\t".join(b"s%d" % i for i in range(S)) + b"\n"
+    rows = b"".join(b"1\t%d\t.\tA\tC\t50\tPASS\t.\tGT\t" % (100 + i) +
+                    b"\t".join(rnd.choice([b"0|0", b"0|1", b"1|1"]) for _ in range(S)) + b"\n" for i in range(60))
+    check(hdr + rows, 1 << 20, "one chunk")
+    check(hdr + rows, 4096, "4 KiB chunks")
+    bad = hdr.split(b"\n")
+    bad[min(n_hdr - 2, 1200)] = b"#bad\theader"
+    check(b"\n".join(bad) + rows, 1 << 20, "bad header line")

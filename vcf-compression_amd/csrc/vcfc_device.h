@@ -275,3 +275,5 @@ hipError_t vcfc_line_index(const uint8_t *buf, uint64_t n, uint8_t *ws, const Vc
 // phase 2 (n_lines = counts[0]): '\n' positions, data / pass line arrays; counts[1], counts[2]
 hipError_t vcfc_line_index_place(const uint8_t *buf, uint64_t n, uint64_t n_lines, const uint8_t *ws1, uint8_t *ws2,
                                  const VcfcLineIndexLayout &L, const VcfcLineIndex &x, hipStream_t s);
+// counts[0..3] and the first pk '#' line entries into out (32 + 24 pk bytes)
+hipError_t vcfc_index_summary(const VcfcLineIndex &x, uint64_t pk, uint8_t *out, hipStream_t s);

@@ -910,7 +910,8 @@ __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring
     const uint32_t nch = (span + CHUNK - 1) / CHUNK;
     const uint32_t lo16 = BPL * l;
     FastState f;
-    f.nf = 0; f.carryT = 1; f.gt0 = -1; f.T = 0; f.phi = 0; f.pcls = CLS_NONE; f.prs = 0; f.esc = 0; f.hand = 0;
+    f.nf = 0; f.carryT = 1; f.gt0 = -1; f.T = 0; f.phi = 0; f.pcls = CLS_NONE; f.prs = 0; f.esc = 0;
+    f.hand = 0;
     r.wpos = 8;
     r.fpos = 0;
 
@@ -936,7 +937,8 @@ __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring
     // tracking fall back to vmcnt(0)); the general step sits outside it so
     // its registers do not add to the prefetch buffers'.
     const uint32_t phi = f.phi, T = f.T;
-    const vw::brsrc rsG = vw::make_rsrc(line + f.gt0 - phi, (phi + len - (uint32_t)f.gt0 + 3u) & ~3u);
+    vw::brsrc rsG = vw::make_rsrc(line + f.gt0 - phi, (phi + len - (uint32_t)f.gt0 + 3u) & ~3u);
+    const vw::brsrc rsZ = vw::make_rsrc(line, 0u);   // an empty range: loads read 0 and touch no memory
     const uint32_t ncG = (T + SLOTS8 - 1) / SLOTS8;
     const uint32_t lo32 = BPL8 * l;
     f.hand = defer && c == 0 && ncG > 1 ? 1u : 0u;   // (esc8: an all-escape chunk 0 hands the row on)
@@ -953,6 +955,11 @@ __device__ bool encode_fast(const uint8_t *__restrict__ line, uint32_t len, Ring
         bool ok = true;
         for (;;) {
             if (ok) { ok = vw::readfirst(gt_step8(b0, C, f, r)); gen = C; }
+            // a row handed on at chunk 0 (esc8, f.hand = 2) loads nothing
+            // more: the loop's remaining loads go to an empty range (the same
+            // instructions, so the counted vmcnt waits stay as they are;
+            // unphased rows 7.06 -> 6.63 ms, profiles/r06/ab/ab_r6hn_*.txt)
+            rsG = f.hand == 2u ? rsZ : rsG;
             b0 = load_chunk8(rsG, C + 3, lo32);
             vw::pin_loads();
             if (ok && C + 1 < ncG) { ok = vw::readfirst(gt_step8(b1, C + 1, f, r)); gen = C + 1; }
@@ -1900,25 +1907,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
     // rows all hold one token per sample; a wrong guess costs the batch a
     // second size scan, compaction and deferred pass, never wrong output)
     uint32_t ntok_ref = 0, ntok_last = ~0u;
-#ifdef VCFC_AB_VAR_PREFETCH
-    uint32_t pfv = 0;
-#endif
     while (todo) {
         const uint64_t row = row0 + (uint64_t)__builtin_ctzll(todo);
         todo &= todo - 1;
-#ifdef VCFC_AB_VAR_PREFETCH
-        // the next flagged row's first 8 KiB towards L2 while this row
-        // computes: one dword per 128-byte line per lane (its value is
-        // consumed a row later, when it has long arrived)
-        asm volatile("" ::"v"(pfv));
-        if (todo) {
-            const uint64_t nrow = row0 + (uint64_t)__builtin_ctzll(todo);
-            const uint8_t *nl = a.buf + a.line_off[nrow];
-            const uint8_t *nb = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(nl) & ~(uintptr_t)127);
-            const uint32_t nspan = (uint32_t)(nl - nb) + a.line_len[nrow];
-            pfv = vw::bload4(vw::make_rsrc(nb, nspan), 128u * l);
-        }
-#endif
         Ring r;
         if (!row_setup(a, row, lds + wave * RING_STRIDE, r)) continue;
         // a.nl_check (the hop line index guessed line ends): a row holding a

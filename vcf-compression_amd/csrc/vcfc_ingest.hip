@@ -156,7 +156,9 @@ __global__ __launch_bounds__(256) void k_nl_scan(const uint8_t *buf, uint64_t n,
 // caught by the encoder (VcfcEncodeArgs::nl_check), and the chunk is indexed
 // again by k_nl_scan.
 constexpr uint32_t HOPW = 4;                   // walkers per wave
-constexpr uint64_t HOP_WALKERS = 32768;   // (devfile step: 16384 +1.2 %, 8192 +4.6 %)
+// (devfile step: 16384 +1.2 %, 8192 +4.6 %; round 6: 65536 +1.9 %, 131072 +3.0 %,
+// profiles/r06/ab/ab_r6dev_law1.txt -- more walkers, more FIND starts)
+constexpr uint64_t HOP_WALKERS = 32768;
 constexpr uint32_t GW = 256;                   // guess window (16 B per lane)
 constexpr uint32_t HOP_LINE = 0, HOP_VERIFY = 1, HOP_FIND = 2, HOP_DONE = 3, HOP_TRY = 4, HOP_LEARN = 5;
 constexpr uint32_t HOP_K = 3;                  // learned candidates per walker
@@ -534,6 +536,33 @@ hipError_t vcfc_line_index(const uint8_t *buf, uint64_t n, uint8_t *ws, const Vc
 // Phase 2, once the host knows the line count (counts[0]): the '\n'
 // positions in order, then the data / pass tables; ws1 = phase 1's
 // workspace, ws2 = L.total2 bytes for vcfc_line_index_layout(chunk, n_lines).
+// The host's view of an index in one D2H (compress_device): counts[0..3],
+// then the first pk entries of the '#' line tables -- pass_off, pass_before
+// (u64), pass_len, pass_no (u32).  Consecutive small D2H copies each cost
+// the GPU ~12 us of idle time on this runtime (profiles/r06/devfile_trace_*).
+namespace {
+__global__ __launch_bounds__(256) void k_index_summary(const uint64_t *counts, const uint64_t *po, const uint64_t *pb,
+                                                       const uint32_t *pl, const uint32_t *pn, uint64_t pk,
+                                                       uint8_t *out) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    uint64_t *o64 = reinterpret_cast<uint64_t *>(out);
+    if (i < 4) o64[i] = counts[i];
+    if (i < pk) {
+        o64[4 + i] = po[i];
+        o64[4 + pk + i] = pb[i];
+        uint32_t *o32 = reinterpret_cast<uint32_t *>(o64 + 4 + 2 * pk);
+        o32[i] = pl[i];
+        o32[pk + i] = pn[i];
+    }
+}
+}  // namespace
+
+hipError_t vcfc_index_summary(const VcfcLineIndex &x, uint64_t pk, uint8_t *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_index_summary, dim3((unsigned)((std::max<uint64_t>(pk, 4) + 255) / 256)), dim3(256), 0, s,
+                       x.counts, x.pass_off, x.pass_before, x.pass_len, x.pass_no, pk, out);
+    return hipGetLastError();
+}
+
 hipError_t vcfc_line_index_place(const uint8_t *buf, uint64_t n, uint64_t n_lines, const uint8_t *ws1, uint8_t *ws2,
                                  const VcfcLineIndexLayout &L, const VcfcLineIndex &x, hipStream_t s) {
     const uint32_t *seg_cnt = reinterpret_cast<const uint32_t *>(ws1 + L.seg_cnt);

@@ -638,31 +638,37 @@ inline int compress_device(const uint8_t *d_in, uint64_t N, uint8_t *d_out, uint
     uint64_t *d_small = static_cast<uint64_t *>(M.dev(Memory::D_SMALL, 64));
     if (!hsmall || !d_small) return ST_E_HIP;
     auto sync = [&]() { return hipStreamSynchronize(s) == hipSuccess; };
+    // (every D2H below lands in pinned memory, so the copies of one step
+    // queue behind each other and cost one host round trip per sync: a D2H
+    // into pageable memory is synchronous, ~20 us of idle GPU each --
+    // round 6, profiles/r06/devfile_trace_*.txt)
     auto d2h = [&](void *dst, const void *src, uint64_t k) {
         return hipMemcpyAsync(dst, src, k, hipMemcpyDeviceToHost, s) == hipSuccess;
     };
-    {
-        uint8_t last = 0;
-        if (!d2h(&last, d_in + N - 1, 1) || !sync()) return ST_E_HIP;
-        if (last != '\n') {
-            if (trace) fprintf(stderr, "compress_device: last byte %u\n", last);
-            return ST_E_ARG;
-        }
-    }
     // The sample count S from the "#CHROM" line (in the first MiB) lets the
     // line index hop over a data line's genotypes (vcfc_line_index S_hint);
     // a chunk whose hop index the encoder finds wrong (VCFCD_E_NEWLINE) is
     // indexed again from every byte.  cfg.hop_index false
-    // (VCFC_LINE_INDEX_SCAN): always every byte.
+    // (VCFC_LINE_INDEX_SCAN): always every byte.  The file's last byte comes
+    // with the first header window (one round trip); the window stays on the
+    // host for the '#' lines' check below (h0: d_in[0, h0_len)).
     uint32_t S_hint = 0;
     bool learn = false;
+    const uint8_t *h0 = nullptr;
+    uint64_t h0_len = 0;
     {
+        uint8_t *lastp = reinterpret_cast<uint8_t *>(hsmall + 7);
+        if (!d2h(lastp, d_in + N - 1, 1)) return ST_E_HIP;
+        bool checked = false;
         if (cfg.hop_index) {
             // 64 KiB of the file into pinned memory, 1 MiB if the header is longer
             for (uint64_t want = std::min<uint64_t>(N, 64u << 10);;) {
                 uint8_t *h = static_cast<uint8_t *>(M.host(Memory::H_IN0, want));
                 if (!h) return ST_E_HIP;
                 if (!d2h(h, d_in, want) || !sync()) return ST_E_HIP;
+                checked = true;
+                h0 = h;
+                h0_len = want;
                 bool more = false;
                 S_hint = header_samples(h, want, &more);
                 const uint64_t cap = std::min<uint64_t>(N, 1u << 20);
@@ -673,6 +679,11 @@ inline int compress_device(const uint8_t *d_in, uint64_t N, uint8_t *d_out, uint
                 want = cap;
             }
             if (S_hint < 32) S_hint = 0;   // (the check reads 32 tokens)
+        }
+        if (!checked && !sync()) return ST_E_HIP;
+        if (*lastp != '\n') {
+            if (trace) fprintf(stderr, "compress_device: last byte %u\n", *lastp);
+            return ST_E_ARG;
         }
         if (trace) fprintf(stderr, "compress_device: S_hint=%u learn=%d\n", S_hint, (int)learn);
     }
@@ -732,9 +743,17 @@ inline int compress_device(const uint8_t *d_in, uint64_t N, uint8_t *d_out, uint
         x.pass_off = reinterpret_cast<uint64_t *>(d_rec + 8 * (n_lines + 1));
         x.pass_len = reinterpret_cast<uint32_t *>(d_rec + 16 * (n_lines + 1));
         x.pass_no = x.pass_len + (n_lines + 1);
-        if (vcfc_line_index_place(d_c, n, n_lines, d_ix1, d_ix2, L, x, s) != hipSuccess || !d2h(hsmall, d_small, 32) ||
-            !sync())
+        // the counts, and with them the first PK entries of the '#' line
+        // arrays (every real header fits): gathered on the device, one D2H
+        const uint64_t PK = std::min<uint64_t>(n_lines + 1, 1024);
+        uint8_t *hsum = static_cast<uint8_t *>(M.host(Memory::H_IN1, 32 + 24 * PK));
+        uint8_t *dsum = static_cast<uint8_t *>(M.dev(Memory::D_IN1, 32 + 24 * PK));
+        if (!hsum || !dsum) return ST_E_HIP;
+        if (vcfc_line_index_place(d_c, n, n_lines, d_ix1, d_ix2, L, x, s) != hipSuccess ||
+            vcfc_index_summary(x, PK, dsum, s) != hipSuccess || !d2h(hsum, dsum, 32 + 24 * PK) || !sync())
             return ST_E_HIP;
+        memcpy(hsmall, hsum, 32);
+        const uint8_t *hpass = hsum + 32;
         // counts[3]: 1 = a line of 4 GiB or more (k_line_place), 2 = a hop
         // index that missed a line end in a segment of more than NL_SLOT
         // lines (k_nl_place's rescan; the other missed ends reach the encoder
@@ -767,29 +786,52 @@ inline int compress_device(const uint8_t *d_in, uint64_t N, uint8_t *d_out, uint
         if (n_pass) {
             std::vector<uint32_t> pl(n_pass), pn(n_pass);
             std::vector<uint64_t> po(n_pass), pb(n_pass);
-            if (!d2h(po.data(), x.pass_off, 8 * n_pass) || !d2h(pl.data(), x.pass_len, 4 * n_pass) ||
-                !d2h(pn.data(), x.pass_no, 4 * n_pass) || !d2h(pb.data(), x.pass_before, 8 * n_pass) || !sync())
-                return ST_E_HIP;
+            if (n_pass <= PK) {
+                memcpy(po.data(), hpass, 8 * n_pass);
+                memcpy(pb.data(), hpass + 8 * PK, 8 * n_pass);
+                memcpy(pl.data(), hpass + 16 * PK, 4 * n_pass);
+                memcpy(pn.data(), hpass + 20 * PK, 4 * n_pass);
+            } else {
+                uint8_t *hp = static_cast<uint8_t *>(M.host(Memory::H_IN1, 24 * n_pass));
+                if (!hp || !d2h(hp, x.pass_off, 8 * n_pass) || !d2h(hp + 8 * n_pass, x.pass_before, 8 * n_pass) ||
+                    !d2h(hp + 16 * n_pass, x.pass_len, 4 * n_pass) || !d2h(hp + 20 * n_pass, x.pass_no, 4 * n_pass) ||
+                    !sync())
+                    return ST_E_HIP;
+                memcpy(po.data(), hp, 8 * n_pass);
+                memcpy(pb.data(), hp + 8 * n_pass, 8 * n_pass);
+                memcpy(pl.data(), hp + 16 * n_pass, 4 * n_pass);
+                memcpy(pn.data(), hp + 20 * n_pass, 4 * n_pass);
+            }
             uint64_t text_bytes = 0;
             for (uint64_t k = 0; k < n_pass; k++) text_bytes += pl[k];
             const uint64_t span = po[n_pass - 1] + pl[n_pass - 1] - po[0];
             const bool one_copy = span <= 2 * text_bytes + (1u << 20);
-            std::vector<uint8_t> text(one_copy ? span : text_bytes);
-            std::vector<uint64_t> at(n_pass);   // line k's text at text.data() + at[k]
-            if (one_copy) {
-                if (span && !d2h(text.data(), d_c + po[0], span)) return ST_E_HIP;
-                for (uint64_t k = 0; k < n_pass; k++) at[k] = po[k] - po[0];
+            // the lines' text: the header window read at the start already
+            // holds a header at the file's start (no copy), else pinned D2H
+            const uint8_t *text = nullptr;
+            std::vector<uint64_t> at(n_pass);   // line k's text at text + at[k]
+            if (h0 && pos + po[n_pass - 1] + pl[n_pass - 1] <= h0_len) {
+                text = h0 + pos;
+                for (uint64_t k = 0; k < n_pass; k++) at[k] = po[k];
             } else {
-                uint64_t t = 0;
-                for (uint64_t k = 0; k < n_pass; k++) {
-                    at[k] = t;
-                    if (pl[k] && !d2h(text.data() + t, d_c + po[k], pl[k])) return ST_E_HIP;
-                    t += pl[k];
+                uint8_t *tb = static_cast<uint8_t *>(M.host(Memory::H_IN2, std::max<uint64_t>(one_copy ? span : text_bytes, 1)));
+                if (!tb) return ST_E_HIP;
+                if (one_copy) {
+                    if (span && !d2h(tb, d_c + po[0], span)) return ST_E_HIP;
+                    for (uint64_t k = 0; k < n_pass; k++) at[k] = po[k] - po[0];
+                } else {
+                    uint64_t t = 0;
+                    for (uint64_t k = 0; k < n_pass; k++) {
+                        at[k] = t;
+                        if (pl[k] && !d2h(tb + t, d_c + po[k], pl[k])) return ST_E_HIP;
+                        t += pl[k];
+                    }
                 }
+                if (!sync()) return ST_E_HIP;
+                text = tb;
             }
-            if (!sync()) return ST_E_HIP;
             for (uint64_t k = 0; k < n_pass; k++) {
-                const uint8_t *tx = text.data() + at[k];
+                const uint8_t *tx = text + at[k];
                 const uint64_t len = pl[k];
                 if (!(len >= 2 && tx[1] == '#') && !header_ok(tx, len)) {
                     hdr_err = pn[k];
@@ -810,10 +852,35 @@ inline int compress_device(const uint8_t *d_in, uint64_t N, uint8_t *d_out, uint
         int64_t bad_line = -1;
         uint8_t *d_recs = nullptr;
         // record offsets: only the few the placement needs come to the host
+        // (the batch's total with the encode's error word, the others one
+        // round trip each -- only interleaved '#' lines need them)
         auto rec_at = [&](uint64_t k, uint64_t *v) {
             *v = 0;
-            return !n_data || k == 0 || (d2h(v, d_rec_off + k, 8) && sync());
+            if (!n_data || k == 0) return true;
+            if (k == n_data) { *v = hsmall[5]; return true; }
+            return d2h(hsmall + 6, d_rec_off + k, 8) && sync() && (*v = hsmall[6], true);
         };
+        // '#' lines that all precede the chunk's data lines (every real VCF):
+        // their D2D copies go ahead of the encode, so the encode's one
+        // round trip covers them (they land at d_out[o, o + pass_bytes)
+        // whatever the encode finds: none follows a data row)
+        bool pass_placed = false;
+        if (!interleaved && !pass.empty()) {
+            if (o + pass_bytes > out_cap) return ST_E_NOSPACE;
+            uint64_t q = o, rs = pass[0].off, rl = 0, rd = o;
+            for (const DevPass &p : pass) {
+                if (rl && rs + rl != p.off) {
+                    if (hipMemcpyAsync(d_out + rd, d_c + rs, rl, hipMemcpyDeviceToDevice, s) != hipSuccess) return ST_E_HIP;
+                    rs = p.off;
+                    rd = q;
+                    rl = 0;
+                }
+                rl += p.len;
+                q += p.len;
+            }
+            if (rl && hipMemcpyAsync(d_out + rd, d_c + rs, rl, hipMemcpyDeviceToDevice, s) != hipSuccess) return ST_E_HIP;
+            pass_placed = true;
+        }
         if (n_data) {
             const VcfcWorkspaceLayout W = vcfc_encode_workspace_layout(n_data, n);
             uint8_t *ws = static_cast<uint8_t *>(M.dev(Memory::D_ENC_WS, W.total));
@@ -835,7 +902,8 @@ inline int compress_device(const uint8_t *d_in, uint64_t N, uint8_t *d_out, uint
             a.err = d_small + 4;
             a.nl_check = hop != 0;
             a.defer_records = cfg.defer_records ? 1u : 0u;
-            if (vcfc_encode_device(a, s) != hipSuccess || !d2h(hsmall + 4, d_small + 4, 8) || !sync())
+            if (vcfc_encode_device(a, s) != hipSuccess || !d2h(hsmall + 4, d_small + 4, 8) ||
+                !d2h(hsmall + 5, d_rec_off + n_data, 8) || !sync())
                 return ST_E_HIP;
             const uint64_t errw = hsmall[4];
             if (errw != VCFCD_NO_ERROR && (errw & 0xFF) == VCFCD_E_NEWLINE) {
@@ -874,6 +942,10 @@ inline int compress_device(const uint8_t *d_in, uint64_t N, uint8_t *d_out, uint
             run_len = 0;
             return ok;
         };
+        if (pass_placed) {   // (copied ahead of the encode)
+            o += pass_bytes;
+            pass.clear();
+        }
         for (const DevPass &p : pass) {
             uint64_t upto;
             if (!rec_at(std::min<uint64_t>(p.before, good), &upto)) return ST_E_HIP;
