@@ -59,11 +59,14 @@ def law2_token_lengths(samples):
                      np.where(missing, 1, 3)])
 
 
-def prefixes(n, law, seed, row0=0, samples=2504):
+def prefixes(n, law, seed, row0=0, samples=2504, keep=None):
     """Return (prefix bytes blob, prefix_off[n+1] int64, row_af float32 or None, POS int64[n]).
 
     law 1 scales with the sample count: k ~ 1/k on [1, 2S-1], AN = 2S, NS = S
-    (at S = 2504 these are the 1000 Genomes values)."""
+    (at S = 2504 these are the 1000 Genomes values).  keep = (lo, hi): the
+    random draws are those of all n rows, but only rows [lo, hi) are
+    formatted and returned (slice_prefixes)."""
+    lo, hi = keep if keep is not None else (0, n)
     rng = np.random.default_rng(seed)
     ref = rng.integers(0, 4, n)
     gt_len = None
@@ -79,7 +82,7 @@ def prefixes(n, law, seed, row0=0, samples=2504):
         alt = (ref + rng.integers(1, 4, n)) % 4
         fmt = np.where(kind == 1, "GT:DP:GQ", "GT")
         rows = ["X\t%d\t.\t%s\t%s\t50\tPASS\tAC=%d;AN=%d;KIND=%d\t%s\t"
-                % (pos[i], BASES[ref[i]], BASES[alt[i]], k[i], an, kind[i], fmt[i]) for i in range(n)]
+                % (pos[i], BASES[ref[i]], BASES[alt[i]], k[i], an, kind[i], fmt[i]) for i in range(lo, hi)]
         # (af just below 1 so kind + af keeps its integer part in float32)
         af = (kind + np.minimum(afv, 0.999)).astype(np.float32)
         gt_len = law2_token_lengths(samples).sum(axis=1)[kind] + samples   # tokens + TABs + '\n'
@@ -89,7 +92,7 @@ def prefixes(n, law, seed, row0=0, samples=2504):
         alt2 = np.where(alt2 == ref, (alt2 + 1) % 4, alt2)
         pos = 10000 + 2 * (row0 + np.arange(n, dtype=np.int64))
         rows = ["1\t%d\tvar%d\t%s\t%s,%s\t100\tPASS\tINFO\tGT\t" % (10000 + 2 * (row0 + i), row0 + i, BASES[r], BASES[a], BASES[b])
-                for i, (r, a, b) in enumerate(zip(ref.tolist(), alt1.tolist(), alt2.tolist()))]
+                for i, (r, a, b) in enumerate(zip(ref.tolist(), alt1.tolist(), alt2.tolist())) if lo <= i < hi]
         af = None
     else:
         gaps = rng.geometric(1.0 / 32.0, n)
@@ -104,7 +107,7 @@ def prefixes(n, law, seed, row0=0, samples=2504):
         multi = rng.random(n) < 0.01
         rs = rng.integers(1, 800000000, n)
         rows = []
-        for i in range(n):
+        for i in range(lo, hi):
             p = pops[i]
             rows.append("22\t%d\trs%d\t%s\t%s\t100\tPASS\tAC=%d;AF=%.4g;AN=%d;NS=%d;DP=%d;"
                         "EAS_AF=%.4g;AMR_AF=%.4g;AFR_AF=%.4g;EUR_AF=%.4g;SAS_AF=%.4g;AA=.|||;VT=SNP\tGT\t"
@@ -114,19 +117,20 @@ def prefixes(n, law, seed, row0=0, samples=2504):
         if law == 3:   # the row's kind (0: cycling classes, 1: alleles at 1/2)
             af = (rng.random(n) < 0.5).astype(np.float32)
     blob = "".join(rows).encode()
-    plen = np.fromiter((len(r) for r in rows), dtype=np.int64, count=n)
-    poff = np.zeros(n + 1, dtype=np.int64)
+    plen = np.fromiter((len(r) for r in rows), dtype=np.int64, count=hi - lo)
+    poff = np.zeros(hi - lo + 1, dtype=np.int64)
     np.cumsum(plen, out=poff[1:])
+    if keep is not None:
+        af = None if af is None else af[lo:hi].copy()
+        gt_len = None if gt_len is None else np.asarray(gt_len)[lo:hi].copy()
+        pos = np.asarray(pos)[lo:hi]
     return blob, poff, af, np.asarray(pos, dtype=np.int64), gt_len
 
 
 def slice_prefixes(n_total, lo, hi, law, seed, samples=2504):
     """prefixes() of rows [lo, hi) of the n_total-row batch (seed, row0 0):
     one fixed dataset cut into row ranges (bench.py's strong split)."""
-    blob, poff, af, pos, gt_len = prefixes(n_total, law, seed, 0, samples)
-    b0, b1 = int(poff[lo]), int(poff[hi])
-    return (blob[b0:b1], (poff[lo:hi + 1] - b0).astype(np.int64), None if af is None else af[lo:hi].copy(),
-            pos[lo:hi].copy(), None if gt_len is None else np.asarray(gt_len)[lo:hi].copy())
+    return prefixes(n_total, law, seed, 0, samples, keep=(lo, hi))
 
 
 def layout(prefix_off, samples, gt_len=None):
