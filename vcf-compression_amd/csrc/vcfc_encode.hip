@@ -802,6 +802,7 @@ __device__ __forceinline__ bool esc8(const uint32_t (&d)[TPL8], int32_t t0, int3
     // (round 5: the addresses as hand-written v_mad_i32_i24, vw::lds_sel --
     // the compiler had made most of them 64-bit v_mad_u64_u32)
     int32_t ro = ldm + (int32_t)o;
+#ifndef VCFC_DIAG_NOESCEMIT   // (diagnostic, wrong output: esc8 without its per-slot stores)
 #pragma unroll
     for (int j = 0; j < (int)TPL8; j++) {
         const int32_t s = (int32_t)((sbr >> (4 * j)) & 1u);
@@ -814,6 +815,9 @@ __device__ __forceinline__ bool esc8(const uint32_t (&d)[TPL8], int32_t t0, int3
         ro += 4 * e;
         njp = s ? -j : njp;
     }
+#else
+    (void)ro; (void)njp; (void)mL; (void)mH; (void)sbr;
+#endif
     ring_unwrap(r, base + cnt);
     r.wpos += vw::readlane(incl2, 63);
     f.pcls = (vw::readlane(cbH, 63) >> 24) & 7u;
@@ -1884,6 +1888,10 @@ __device__ bool row_has_nl(const uint8_t *__restrict__ line, uint32_t len) {
 
 // rows per wave of the variable-token kernel (16: law 2 -1.8 %, headline
 // step +0.2 % in empty waves; 8: -1.7 % / +0.5 %; profiles/r03/ab/ab_var_rows.txt)
+// (round 6, profiles/r06/ab/ab_r6vr_*.txt: 16 / 8 rows take the grid's
+// last-round tail off the haploid-mix rows, kind 0 -1.4 / -2.8 %, but the
+// prediction learns its token count per wave: GT:DP:GQ rows +3 / +10 %, law
+// 2 +1.3 / +3.6 %)
 constexpr uint32_t VAR_ROWS = 32;
 // Variable-token kernel: the rows the fast kernel flagged, VAR_ROWS per wave
 // (a flag load per 32 rows, so a batch without such rows costs next to
