@@ -1,5 +1,5 @@
 """The committed headline measurement reproduces from its own files
-(profiles/r05/final5/): the bench line's roofline fraction from the rocprofv3
+(profiles/r06/final/; round 5: profiles/r05/final5/): the bench line's roofline fraction from the rocprofv3
 kernel trace of the same command, and its HBM traffic from the PMC summary
 bench.py reads.  CPU only (reads committed files)."""
 import json
@@ -10,7 +10,7 @@ import sys
 import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-FINAL = os.path.join(REPO, "profiles", "r05", "final5")
+FINAL = os.path.join(REPO, "profiles", "r06", "final")
 
 
 def _line(name):
