@@ -194,12 +194,10 @@ __device__ __forceinline__ uint32_t walker_scan(uint32_t v) {
 // 16.5 -> 13.7 ms (profiles/r04/ab/ab_tall_law*.txt); without it the walker
 // is round 3's (86 VGPRs, 5 waves).
 template <bool LEARN>
-#ifdef VCFC_AB_HOP_WPE
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VCFC_AB_HOP_WPE, VCFC_AB_HOP_WPE)))
-void k_nl_hop(const uint8_t *buf, uint64_t n, uint64_t n_seg, uint32_t S,
-#else
+// (round 6: pinned to 6 waves per SIMD, 80 VGPRs and a 12-byte spill, the
+// same speed; to 8, 64 VGPRs and 72 bytes spilled, +4 %:
+// profiles/r06/ab/ab_r6hop_devfile_law1.txt)
 __global__ __launch_bounds__(256) void k_nl_hop(const uint8_t *buf, uint64_t n, uint64_t n_seg, uint32_t S,
-#endif
                                                 uint32_t wseg, uint32_t *seg_cnt, uint64_t *slot) {
     const uint32_t l = vw::lane_id(), wl = l & 15u, w0 = l & ~15u, sh = l & 48u;   // w0: the walker's first lane
     const uint64_t walker = ((uint64_t)blockIdx.x * IX_WAVES + (threadIdx.x >> 6)) * HOPW + (l >> 4);
