@@ -22,6 +22,7 @@ int compress_data_line(const std::string& line, const VcfCompressionSchema& /*sc
     byte_vec.resize(at + (st == VCFC_OK ? n : 0));
     if (st == VCFC_E_LT8COLS) throw VcfValidationError("VCF data line did not contain at least 8 terms");
     if (st == VCFC_E_8COLS) throw std::length_error("vector::_M_default_append");   // reference aborts here
+    if (st == VCFC_E_TOOLONG) throw std::length_error(vcfc_strerror(st));           // record past the 30-bit LEN header
     if (st != VCFC_OK) throw std::runtime_error(vcfc_strerror(st));
     return 0;
 }
@@ -35,6 +36,7 @@ int compress(const std::string& in, const std::string& out) {
     if (st == VCFC_E_LT8COLS) throw VcfValidationError("VCF data line did not contain at least 8 terms");
     if (st == VCFC_E_HEADER) throw VcfValidationError("VCF Header did not have enough columns");
     if (st == VCFC_E_8COLS) throw std::length_error("vector::_M_default_append");
+    if (st == VCFC_E_TOOLONG) throw std::length_error(vcfc_strerror(st));
     if (st != VCFC_OK) throw std::runtime_error(vcfc_strerror(st));
     return 0;
 }
