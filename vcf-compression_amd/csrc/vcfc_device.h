@@ -7,7 +7,8 @@
 // VCFC_DIAG_BUILD; a product build with any of them is refused here (and by
 // the Makefile, tests/test_capi.py::test_diag_switches_refused).
 #if (defined(VCFC_DIAG_NOSTORE) || defined(VCFC_DIAG_NOSTEP) || defined(VCFC_DIAG_CLEAN_SKIP) || \
-     defined(VCFC_VAR_SIZE_ONLY) || defined(VCFC_DIAG_DEC_NOSCAN) || defined(VCFC_DIAG_NOESCEMIT)) && \
+     defined(VCFC_VAR_SIZE_ONLY) || defined(VCFC_DIAG_DEC_NOSCAN) || defined(VCFC_DIAG_NOESCEMIT) || \
+     defined(VCFC_DIAG_NODIRECT)) && \
     !defined(VCFC_DIAG_BUILD)
 #error "VCFC_DIAG_* / VCFC_VAR_SIZE_ONLY produce wrong output: diagnostic builds only (define VCFC_DIAG_BUILD)"
 #endif

@@ -135,6 +135,10 @@ __device__ __forceinline__ void ring_stage(Ring &r, uint32_t f, uint4 v) {
         // alignment: plain stores, so that L2 merges the 16-byte pieces
         // into whole lines (non-temporal output stores were slower in the
         // compaction too, §4)
+#ifdef VCFC_DIAG_NODIRECT   // (diagnostic, wrong output: the deferred records' bursts not stored)
+        if (f == 0x7FFFFFFFu) vw::gstore16(r.prim, f, v);
+        return;
+#endif
         vw::gstore16(r.prim, f, v);
         return;
     }
