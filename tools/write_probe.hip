@@ -17,6 +17,13 @@
 //       line's bytes from its first 128-B boundary: no partial 128-B line
 //       inside a line, only at its two ends)
 //   w9  as w3 with 64-B aligned store windows
+//   w10 output-ordered chunks (round 6): the buffer (from byte 37) cut into
+//       C-byte chunks, a resident grid taking chunks g, g + G, ... (each
+//       wave-iteration writes C contiguous bytes, 1 KiB per instruction),
+//       C = 1 / 2 / 4 KiB; "+load" first reads one dword per lane of a
+//       680 MB input at the chunk (and uses it), as a tile writer reads
+//       its record window -- on gfx9 that load's wait also waits for the
+//       wave's earlier stores
 // Build: hipcc --offload-arch=gfx950 -O3 -o build/write_probe tools/write_probe.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -97,16 +104,38 @@ __global__ __launch_bounds__(256) void w_line_al(uint8_t *buf) {
     for (uint64_t o = a0 + 16 * l; o + 16 <= e; o += 1024) *reinterpret_cast<v4u *>(buf + o) = v;
 }
 
+template <uint32_t C, bool LOAD>
+__global__ __launch_bounds__(256) void w_chunk(uint8_t *buf, const uint32_t *src, uint64_t nsrc) {
+    const uint32_t l = threadIdx.x & 63;
+    const uint64_t G = (uint64_t)gridDim.x * 4, nchunk = (TOTAL - 64) / C;
+    for (uint64_t c = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); c < nchunk; c += G) {
+        uint32_t x = 0x09307C30u;
+        if (LOAD) x |= src[(c * 64 + l) % nsrc];   // the input is zero
+        const v4u v = {x, x, x, x};
+        const uint64_t o0 = 37 + c * C;
+        for (uint64_t o = o0 + 16 * l; o < o0 + C; o += 1024) __builtin_memcpy(buf + o, &v, 16);
+    }
+}
+
 int main() {
     uint8_t *buf;
     CK(hipMalloc(&buf, TOTAL + 64));
+    const uint64_t NSRC = 680000000ull / 4;
+    uint32_t *src;
+    CK(hipMalloc(&src, NSRC * 4));
+    CK(hipMemset(src, 0, NSRC * 4));
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    const char *names[13] = {"w0 grid plain", "w1 grid nt", "w2 line nt", "w3 line plain", "w4 line plain unaligned",
+    const char *names[27] = {"w0 grid plain", "w1 grid nt", "w2 line nt", "w3 line plain", "w4 line plain unaligned",
                              "w5 line plain unaligned dwords", "w6 resident 1024 blocks", "w6 resident 2048 blocks",
-                             "w6 resident 4096 blocks", "w6 resident 8192 blocks", "w7 block per line", "w8 line 128-B aligned", "w9 line 64-B aligned"};
-    for (int p = 0; p < 13; p++) {
+                             "w6 resident 4096 blocks", "w6 resident 8192 blocks", "w7 block per line", "w8 line 128-B aligned", "w9 line 64-B aligned",
+                             "w10 chunk 1K g2048", "w10 chunk 2K g2048", "w10 chunk 4K g2048",
+                             "w10 chunk 1K g2048 +load", "w10 chunk 2K g2048 +load", "w10 chunk 4K g2048 +load",
+                             "w10 chunk 1K g4096", "w10 chunk 2K g4096", "w10 chunk 4K g4096",
+                             "w10 chunk 1K g4096 +load", "w10 chunk 2K g4096 +load", "w10 chunk 4K g4096 +load",
+                             "w10 chunk 8K g2048 +load", "w10 chunk 8K g4096 +load"};
+    for (int p = 0; p < 27; p++) {
         float best = 1e9;
         for (int it = 0; it < 12; it++) {
             CK(hipEventRecord(e0));
@@ -120,6 +149,14 @@ int main() {
             if (p == 10) hipLaunchKernelGGL(w_line_block, dim3(NLINE), dim3(256), 0, 0, buf);
             if (p == 11) hipLaunchKernelGGL(w_line_al<128>, dim3(NLINE / 4), dim3(256), 0, 0, buf);
             if (p == 12) hipLaunchKernelGGL(w_line_al<64>, dim3(NLINE / 4), dim3(256), 0, 0, buf);
+            const dim3 g(p >= 19 && p < 25 ? 4096 : p == 26 ? 4096 : 2048);
+            if (p == 13 || p == 19) hipLaunchKernelGGL((w_chunk<1024, false>), g, dim3(256), 0, 0, buf, src, NSRC);
+            if (p == 14 || p == 20) hipLaunchKernelGGL((w_chunk<2048, false>), g, dim3(256), 0, 0, buf, src, NSRC);
+            if (p == 15 || p == 21) hipLaunchKernelGGL((w_chunk<4096, false>), g, dim3(256), 0, 0, buf, src, NSRC);
+            if (p == 16 || p == 22) hipLaunchKernelGGL((w_chunk<1024, true>), g, dim3(256), 0, 0, buf, src, NSRC);
+            if (p == 17 || p == 23) hipLaunchKernelGGL((w_chunk<2048, true>), g, dim3(256), 0, 0, buf, src, NSRC);
+            if (p == 18 || p == 24) hipLaunchKernelGGL((w_chunk<4096, true>), g, dim3(256), 0, 0, buf, src, NSRC);
+            if (p == 25 || p == 26) hipLaunchKernelGGL((w_chunk<8192, true>), g, dim3(256), 0, 0, buf, src, NSRC);
             CK(hipEventRecord(e1));
             CK(hipEventSynchronize(e1));
             float ms;
