@@ -130,9 +130,37 @@ def test_hop_index_equals_scan_index(S, jitter):
     300 bytes: the VERIFY round) and lines shorter than the first KiB."""
     rnd = random.Random(S)
     vcf = chr22_like(rnd, 150, S, jitter)
-    assert E.emu_line_index(vcf, S) == E.emu_line_index(vcf, 0)
+    scan = E.emu_line_index(vcf, 0)
+    assert E.emu_line_index(vcf, S) == scan
+    # the walkers compress_device takes for such files (no learned
+    # candidates: GUESS rounds), with the product's walker count and with
+    # one wave of walkers (~40 lines each)
+    assert E.emu_line_index(vcf, S, learn=False) == scan
+    assert E.emu_line_index(vcf, S, hop_walkers=4, learn=False) == scan
     for chunk in (1 << 15, 1 << 20):
         check(vcf, chunk, "chr22-like S=%d" % S)
+
+
+@pytest.mark.parametrize("S,jitter,walkers", [(2504, 40, 2), (2504, 40, 8), (700, 40, 2), (700, 300, 2)])
+def test_hop_guess_rounds(S, jitter, walkers):
+    """Round 6: GUESS rounds (k_nl_hop without learned candidates) guess the
+    next 4 / 8 line ends from the mean line length and read one 256-byte
+    window per line.  On chr22-like rows without '#' lines among them the
+    walkers read ~0.3 KB per 10 KB line (LINE rounds alone: ~0.55 KB); the
+    index is the scan's exactly, with prefixes jumping by up to 300 bytes
+    too (windows that miss: the line by LINE)."""
+    vcf = chr22_like(random.Random(S * 3 + jitter), 400, S, jitter)
+    keep = [ln for ln in vcf.split(b"\n") if ln and not ln.startswith(b"##mid")]
+    vcf = b"\n".join(keep) + b"\n"
+    scan = E.emu_line_index(vcf, 0)
+    E.emu_hop_read()
+    assert E.emu_line_index(vcf, S, hop_walkers=walkers, learn=False) == scan
+    guess = E.emu_hop_read()
+    assert E.emu_line_index(vcf, S, hop_walkers=walkers, learn=True) == scan
+    line = E.emu_hop_read()
+    if S == 2504 and jitter == 40:
+        assert guess < 0.04 * len(vcf) and guess < 0.7 * line, (guess, line, len(vcf))
+    check(vcf, 1 << 22, "guess S=%d" % S)
 
 
 @pytest.mark.parametrize("kind", ["tab", "escape", "var", "lines"])

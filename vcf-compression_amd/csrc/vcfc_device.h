@@ -224,6 +224,9 @@ hipError_t vcfc_decode_stream(const uint8_t *in, uint64_t n, uint64_t p, uint64_
 hipError_t vcfc_record_hash(const uint8_t *recs, const uint64_t *rec_off, uint64_t n, uint64_t *out, hipStream_t s);
 // exclusive u32 -> u64 scan with out[n] = total (shared with the encoder)
 hipError_t vcfc_scan_u32(const uint32_t *in, uint64_t n, uint64_t *partials, uint64_t *out, hipStream_t s);
+// The same over line kinds (bit 0: data line, bit 1: '#' line): out[i] =
+// data lines before i | '#' lines before i << 32 (line index phase 2).
+hipError_t vcfc_scan_kinds(const uint32_t *in, uint64_t n, uint64_t *partials, uint64_t *out, hipStream_t s);
 
 // ---------------------------------------------------------------------------
 // Range query (vcfc_decode.hip; reference query_compressed_file,
@@ -259,8 +262,8 @@ struct VcfcLineIndex {
     uint64_t *counts;       // {lines, data lines, pass lines, a line of >= 4 GiB}
 };
 struct VcfcLineIndexLayout {
-    uint64_t seg_cnt, seg_base, slot, partials1, total1;             // phase 1 workspace
-    uint64_t nl, is_data, is_pass, data_rank, pass_rank, partials2, total2;   // phase 2 workspace
+    uint64_t seg_cnt, seg_base, slot, wstart, partials1, total1;     // phase 1 workspace
+    uint64_t nl, kind, rank, partials2, total2;   // phase 2 workspace
 };
 VcfcLineIndexLayout vcfc_line_index_layout(uint64_t chunk_bytes, uint64_t n_lines);
 // phase 1: '\n' count of buf[0, n) (last byte '\n'); counts[0] = lines.

@@ -2216,10 +2216,16 @@ __global__ __launch_bounds__(256) void k_compact_out(const uint8_t *__restrict__
 
 // ---------------------------------------------------------------------------
 // Exclusive scan u32 -> u64 (n + 1 outputs).  MODE 0: identity, MODE 1:
-// vcfc_slot_bytes(len), MODE 2: record sizes (VCFCD_DEFER masked).  4096 items per 256-thread block.
+// vcfc_slot_bytes(len), MODE 2: record sizes (VCFCD_DEFER masked), MODE 3:
+// line kinds, two counts in one word (bit 0 -> the low half, bit 1 -> the
+// high half: both stay below 2^32 for a chunk's < 2^32 - 1 lines).  4096
+// items per 256-thread block.
 
 template <int MODE> __device__ __forceinline__ uint64_t scan_xf(uint32_t v) {
-    return MODE == 1 ? vcfc_slot_bytes(v) : MODE == 2 ? (uint64_t)(v & ~VCFCD_DEFER) : (uint64_t)v;
+    return MODE == 1   ? vcfc_slot_bytes(v)
+           : MODE == 2 ? (uint64_t)(v & ~VCFCD_DEFER)
+           : MODE == 3 ? (uint64_t)(v & 1u) | ((uint64_t)((v >> 1) & 1u) << 32)
+                       : (uint64_t)v;
 }
 
 // Exclusive block scan of u64 values: each wave scans four 16-bit limbs with
@@ -2547,4 +2553,9 @@ hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t s, hipEvent_t
 hipError_t vcfc_scan_u32(const uint32_t *in, uint64_t n, uint64_t *partials, uint64_t *out, hipStream_t s) {
     if (n == 0) return hipMemsetAsync(out, 0, 8, s);
     return launch_scan<0>(in, n, partials, out, s);
+}
+
+hipError_t vcfc_scan_kinds(const uint32_t *in, uint64_t n, uint64_t *partials, uint64_t *out, hipStream_t s) {
+    if (n == 0) return hipMemsetAsync(out, 0, 8, s);
+    return launch_scan<3>(in, n, partials, out, s);
 }

@@ -19,13 +19,16 @@
 //                 guessed and checked, ~0.5 KiB read per line; see below)
 //   scan          segment bases (the encoder's exclusive scan)
 //   k_nl_place    one lane per segment: its positions from the slot to their
-//                 place; a segment with more than NL_SLOT lines (average
-//                 line < 64 bytes: header lines) scans its bytes again
-//   k_line_kind   one lane per line: data / pass flags
-//   scan x2       data and pass ranks
-//   k_line_place  one lane per line: scatter into the output arrays
+//                 place, and the kind of the line after each (its first
+//                 byte: data, '#' or empty); a segment with more than
+//                 NL_SLOT lines (average line < 64 bytes: header lines) scans
+//                 its bytes again
+//   scan          data and '#' line ranks, two counts in one word
+//   k_line_place  one lane per line: scatter into the output arrays (the
+//                 last lane: the counts)
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <type_traits>
 #include <vcfc_wave.h>   // angle brackets: tests/simt_emu shadows it
 #include "vcfc_device.h"
 
@@ -44,6 +47,9 @@ constexpr uint32_t SEG = 16384;          // bytes per wave
 constexpr uint32_t WIN = 1024;           // bytes per wave step (16 per lane)
 constexpr uint32_t IX_WAVES = 4;
 constexpr uint32_t NL_SLOT = 128;        // '\n' positions kept per segment by k_nl_scan
+// A slot entry's top bits (the hop index): 1 + the kind of the line after
+// that '\n' when the walker saw its first byte, else 0 (k_nl_place reads it)
+constexpr uint32_t SLOT_KIND = 62;
 __device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
 
 // bit j: byte j of x is '\n' (exact per byte)
@@ -64,16 +70,25 @@ __device__ __forceinline__ uint32_t nl_mask16(const uint8_t *buf, uint64_t n, ui
     return m;
 }
 
+// kind of the line starting at byte x (phase 2): 1 data, 2 '#', 0 empty (or none: x = n)
+__device__ __forceinline__ uint32_t line_kind_at(const uint8_t *buf, uint64_t n, uint64_t x) {
+    const uint32_t c = x < n ? buf[x] : '\n';
+    return c == '\n' ? 0u : c == '#' ? 2u : 1u;
+}
+
 // positions of the '\n' bytes of one 1 KiB window (lane l: bytes [p, p + 16))
-// at out[o0 + rank] for ranks below `lim`; returns the window's count
+// at out[o0 + rank] for ranks below `lim`; returns the window's count.
+// kind (phase 2): kind[rank + 1] = the kind of the line after each.
 __device__ __forceinline__ uint32_t nl_window(const uint8_t *buf, uint64_t n, uint64_t p, uint64_t *out, uint64_t o0,
-                                              uint64_t lim) {
+                                              uint64_t lim, uint32_t *kind = nullptr) {
     uint32_t m = nl_mask16(buf, n, p);
     const uint32_t c = __builtin_popcount(m);
     const uint32_t inc = vw::scan_add(c);
     uint64_t o = o0 + inc - c;
     while (m && o < lim) {
-        out[o++] = p + (uint64_t)__builtin_ctz(m);
+        const uint64_t x = p + (uint64_t)__builtin_ctz(m);
+        if (kind) kind[o + 1] = line_kind_at(buf, n, x + 1);
+        out[o++] = x;
         m &= m - 1;
     }
     return vw::readlane(inc, 63);
@@ -143,10 +158,26 @@ __global__ __launch_bounds__(256) void k_nl_scan(const uint8_t *buf, uint64_t n,
 //           lengths are a per-column trait (haploid males, '.' for the same
 //           samples) or fixed-width (GT:DP:GQ with two-digit DP/GQ) repeat
 //           one G per row kind, so a law-2 file is hopped too.
-//   FIND    the next 1 KiB scanned for its first '\n' (also the walker's
-//           start: the first '\n' at or after its span's first byte - 1).
+//   FIND    the next 1 KiB scanned for its first '\n'.  (The walker's
+//           start, the first '\n' at or after its span's first byte - 1,
+//           comes from k_nl_hop_start, round 6: a wave per walker scanning
+//           4 KiB a step, ahead of the walk.)
 //   LEARN   after FIND ended a data line whose region is >= 256 bytes: the
 //           256 bytes ending at its '\n' become a candidate (round robin).
+//   GUESS   (round 6; walkers without TRY / LEARN, the chr22-shaped files)
+//           after a data line of L >= 512 bytes found by LINE / VERIFY: the
+//           next HOP_G lines (HOP_GL when every walker of the wave guesses:
+//           a lean round with nothing else in it) are guessed to be L bytes
+//           long, L the mean of the lines guessed so far, and one 256-byte
+//           window around each guessed end is loaded in one round -- no
+//           prefix, no 9th TAB.  Window k's line is taken when the
+//           window holds exactly one '\n', at least 64 bytes in, with TABs
+//           at the 15 places 4, 8, ..., 60 before it, and its line is a
+//           data line (its first byte, from the round's head load or the
+//           previous window, is neither '#' nor '\n'); the first window that
+//           fails ends the round and its line goes to LINE.  Lines whose
+//           lengths vary by less than ~100 bytes from one to the next (a
+//           chr22 prefix varies by tens) take one round per HOP_G lines.
 // A walker whose TRYs keep failing (HOP_TRUST misses more than hits) stops
 // trying and learning: lines of random lengths cost what they did before.
 // Loads are 16 B per lane over contiguous 256-byte rows (coalesced).  A
@@ -158,9 +189,19 @@ __global__ __launch_bounds__(256) void k_nl_scan(const uint8_t *buf, uint64_t n,
 constexpr uint32_t HOPW = 4;                   // walkers per wave
 // (devfile step: 16384 +1.2 %, 8192 +4.6 %; round 6: 65536 +1.9 %, 131072 +3.0 %,
 // profiles/r06/ab/ab_r6dev_law1.txt -- more walkers, more FIND starts)
-constexpr uint64_t HOP_WALKERS = 32768;
+#ifndef VCFC_HOP_WALKERS
+#define VCFC_HOP_WALKERS 32768
+#endif
+constexpr uint64_t HOP_WALKERS = VCFC_HOP_WALKERS;
 constexpr uint32_t GW = 256;                   // guess window (16 B per lane)
-constexpr uint32_t HOP_LINE = 0, HOP_VERIFY = 1, HOP_FIND = 2, HOP_DONE = 3, HOP_TRY = 4, HOP_LEARN = 5;
+constexpr uint32_t HOP_LINE = 0, HOP_VERIFY = 1, HOP_FIND = 2, HOP_DONE = 3, HOP_TRY = 4, HOP_LEARN = 5, HOP_GUESS = 6;
+constexpr uint32_t HOP_G = 4;                  // lines guessed per GUESS round (one window each) ...
+#ifndef VCFC_HOP_GL
+#define VCFC_HOP_GL 4
+#endif
+constexpr uint32_t HOP_GL = VCFC_HOP_GL;       // ... in a lean round (every walker of the wave guessing)
+constexpr uint32_t GUESS_MIN = 512;            // line length below which GUESS is not used
+constexpr uint32_t GUESS_LEAD = 160;           // a guessed end's window starts this far before it
 constexpr uint32_t HOP_K = 3;                  // learned candidates per walker
 constexpr uint32_t HOP_TRUST = 8;              // TRY credit: +1 per hit (capped), -1 per all-miss
 
@@ -176,6 +217,11 @@ __device__ __forceinline__ uint32_t tab_mask_v(uint4 v) {   // ('\t' = '\n' ^ 0x
     return nl_bits(v.x ^ 0x03030303u) | nl_bits(v.y ^ 0x03030303u) << 4 | nl_bits(v.z ^ 0x03030303u) << 8 |
            nl_bits(v.w ^ 0x03030303u) << 12;
 }
+// byte j (0..15) of a lane's 16 bytes
+__device__ __forceinline__ uint32_t byte16(uint4 v, uint32_t j) {
+    const uint32_t w = j < 4 ? v.x : j < 8 ? v.y : j < 12 ? v.z : v.w;
+    return (w >> (8 * (j & 3u))) & 0xFFu;
+}
 // inclusive sum over the lane's 16-lane walker
 __device__ __forceinline__ uint32_t walker_scan(uint32_t v) {
     const uint32_t l = vw::lane_id();
@@ -185,6 +231,40 @@ __device__ __forceinline__ uint32_t walker_scan(uint32_t v) {
         if ((l & 15u) >= d) v += y;
     }
     return v;
+}
+
+// Each walker's first line end: the first '\n' at or after its span's first
+// byte - 1 (walker 0: none, it starts at byte 0), or ~0 when there is none
+// before the span's end.  One wave per walker, 4 KiB per step (64 lanes x
+// 4 x 16 B): lines of ~10 KB cost ~2 steps here instead of ~5 of the walk's
+// 1 KiB FIND rounds at the start of every span (the walk's own layout, four
+// walkers of 16 lanes a wave at 4 KiB a step, was slower: 89 against 60 us
+// on the config-2 file).
+__global__ __launch_bounds__(256) void k_nl_hop_start(const uint8_t *buf, uint64_t n, uint64_t n_seg, uint32_t wseg,
+                                                      uint64_t walkers, uint64_t *wstart) {
+    const uint32_t l = vw::lane_id();
+    const uint64_t walker = (uint64_t)blockIdx.x * IX_WAVES + vw::readfirst(threadIdx.x >> 6);
+    if (walker >= walkers) return;
+    const uint64_t sg0 = walker * wseg, lo = sg0 * SEG, hi = umin64((sg0 + wseg) * SEG, n);
+    if (sg0 >= n_seg || lo == 0) {
+        if (l == 0) wstart[walker] = ~0ull;
+        return;
+    }
+    uint64_t found = ~0ull;
+    for (uint64_t c = lo - 1; c < hi && found == ~0ull; c += 4096) {
+        uint32_t m[4];
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++) m[j] = nl_mask_v(load16(buf, n, c + 1024u * j + 16u * l));
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++) {
+            const uint64_t b = vw::ballot(m[j] != 0);
+            if (b && found == ~0ull) {
+                const uint32_t f = (uint32_t)__builtin_ctzll(b);
+                found = c + 1024u * j + 16u * f + (uint32_t)__builtin_ctz(vw::readlane(m[j], f));
+            }
+        }
+    }
+    if (l == 0) wstart[walker] = found < hi ? found : ~0ull;
 }
 
 // LEARN (TRY / LEARN compiled in) is chosen by the host when the first data
@@ -198,29 +278,45 @@ template <bool LEARN>
 // same speed; to 8, 64 VGPRs and 72 bytes spilled, +4 %:
 // profiles/r06/ab/ab_r6hop_devfile_law1.txt)
 __global__ __launch_bounds__(256) void k_nl_hop(const uint8_t *buf, uint64_t n, uint64_t n_seg, uint32_t S,
-                                                uint32_t wseg, uint32_t *seg_cnt, uint64_t *slot) {
+                                                uint32_t wseg, const uint64_t *wstart, uint32_t *seg_cnt,
+                                                uint64_t *slot) {
     const uint32_t l = vw::lane_id(), wl = l & 15u, w0 = l & ~15u, sh = l & 48u;   // w0: the walker's first lane
     const uint64_t walker = ((uint64_t)blockIdx.x * IX_WAVES + (threadIdx.x >> 6)) * HOPW + (l >> 4);
     const uint64_t sg0 = walker * wseg;                              // the walker's first segment
     const uint64_t lo = sg0 * SEG, hi = umin64((sg0 + wseg) * SEG, n);
     const uint32_t nseg = sg0 >= n_seg ? 0u : (uint32_t)umin64(wseg, n_seg - sg0);
-    uint32_t mode = nseg == 0 ? HOP_DONE : (lo == 0 ? HOP_LINE : HOP_FIND);
-    uint64_t p = 0, q = lo == 0 ? 0 : lo - 1, e = 0;
+    uint32_t mode = nseg == 0 ? HOP_DONE : HOP_LINE;
+    uint64_t p = 0, q = 0, e = 0;
     uint32_t pl = 0, rows = 4;          // previous prefix length; 256-byte rows of the next LINE window
+    uint32_t L = 0;                     // GUESS: the guessed line length ('\n' included)
+    uint64_t gs0 = 0;                   // GUESS: the streak's first line start ...
+    uint32_t gn = 0;                    // ... and its lines so far
     uint32_t cur = 0, cc = 0;           // current segment (in the span) and its count
     // learned candidates (walker-uniform lengths; this lane's 16-bit TAB mask of each)
     uint32_t cg[HOP_K] = {0, 0, 0}, csig[HOP_K] = {0, 0, 0};
     uint32_t ins = 0, trust = HOP_TRUST;
     uint64_t gt = 0;                    // the current data line's gt0 (lrn: it may be learned)
     bool lrn = false, tdef = false;     // tdef: the TRY round also checks the 3-byte end e (VERIFY's job)
-    auto record = [&](uint64_t x) {     // (the walker's lanes; lo <= x < hi, in order)
+    // (the walker's lanes; lo <= x < hi, in order).  kh: the kind of the
+    // line after x when the walker saw its first byte (SLOT_KIND), else 0
+    auto record = [&](uint64_t x, uint32_t kh = 0) {
         const uint32_t k = (uint32_t)((x - lo) / SEG);
         for (; cur < k; cur++, cc = 0)
             if (l == w0) seg_cnt[sg0 + cur] = cc;
-        if (l == w0 && cc < NL_SLOT) slot[(sg0 + cur) * NL_SLOT + cc] = x;
+        if (l == w0 && cc < NL_SLOT) slot[(sg0 + cur) * NL_SLOT + cc] = x | ((uint64_t)kh << SLOT_KIND);
         cc++;
     };
     auto wbits = [&](bool pr) { return (uint32_t)(vw::ballot(pr) >> sh) & 0xFFFFu; };
+    // the walker's first line end (k_nl_hop_start): the walk starts after it
+    if (mode != HOP_DONE && lo != 0) {
+        const uint64_t e0 = wstart[walker];
+        if (e0 == ~0ull) mode = HOP_DONE;
+        else {
+            if (e0 >= lo) record(e0);
+            p = e0 + 1;
+            mode = p >= hi ? HOP_DONE : HOP_LINE;
+        }
+    }
     // learned candidates to try (trusted walkers, data lines only)
     auto have_cand = [&]() { return LEARN && lrn && trust != 0 && (cg[0] | cg[1] | cg[2]) != 0; };
     // a failed prediction: the candidates, else FIND from fq
@@ -229,13 +325,93 @@ __global__ __launch_bounds__(256) void k_nl_hop(const uint8_t *buf, uint64_t n, 
         tdef = false;
         mode = have_cand() ? HOP_TRY : HOP_FIND;
     };
+    // GUESS steps of one round (wave-uniform call; act: the walker was
+    // guessing at the round's start, v / hd its windows and head byte):
+    // the windows in order while they hold (collectives for every window; a
+    // walker takes its lines up to the first window that fails)
+    auto guess_round = [&](auto ng, const uint4 *v, uint32_t hd, bool act) {
+        constexpr uint32_t NG = decltype(ng)::value;   // windows this round
+        bool go = act && hd != '#' && hd != '\n';   // the line at p is a data line
+        uint32_t nextm = go ? HOP_GUESS : HOP_LINE;   // the mode after this round
+        uint64_t s = p;          // the current line's start
+        const uint32_t Lw = L;   // the windows' line length
+#pragma unroll
+        for (uint32_t k = 0; k < NG; k++) {
+            const uint64_t ws = p - 1 + (uint64_t)(k + 1) * Lw - GUESS_LEAD;   // (mode0 GUESS: L >= 512, p >= 1)
+            const uint32_t m = nl_mask_v(v[k]);
+            const uint32_t b = wbits(m != 0);
+            const uint32_t f = b ? (uint32_t)__builtin_ctz(b) : 0u;
+            const uint32_t mf = vw::shfl(m, w0 + f);
+            const uint32_t jf = 16u * f + (uint32_t)__builtin_ctz(mf | 0x10000u);   // the '\n', window-relative
+            const bool one = b != 0 && (b & (b - 1)) == 0 && (mf & (mf - 1)) == 0 && jf >= 64;
+            // TABs at jf - 4 i (i = 1..15): this lane's bytes [16 wl, 16 wl + 16) inside [jf - 60, jf)
+            const int32_t r0 = (int32_t)jf - 60 - (int32_t)(16u * wl), r1 = (int32_t)jf - (int32_t)(16u * wl);
+            const uint32_t lo4 = (uint32_t)(r0 < 0 ? 0 : r0 > 16 ? 16 : r0), hi4 = (uint32_t)(r1 < 0 ? 0 : r1 > 16 ? 16 : r1);
+            const uint32_t rm = ((1u << hi4) - 1u) & ~((1u << lo4) - 1u);
+            const uint32_t want = (0x1111u << ((uint32_t)r1 & 3u)) & rm;
+            const bool tabs_ok = (tab_mask_v(v[k]) & want) == want;
+            const uint32_t tbad = wbits(!tabs_ok);   // (collectives stay wave-uniform)
+            const bool hit = one && tbad == 0;
+            // the next line's first byte (window byte jf + 1; none past the window)
+            const uint32_t jn = jf + 1;
+            const uint32_t nb = vw::shfl(byte16(v[k], jn & 15u), w0 + ((jn >> 4) & 15u));
+            const uint64_t e = ws + jf;
+            if (go) {
+                if (!hit || e <= s) {   // the guess failed: this line by LINE
+                    nextm = HOP_LINE;
+                    go = false;
+                } else if (e >= hi) {
+                    nextm = HOP_DONE;
+                    go = false;
+                } else {
+                    // (the next line's kind, when its first byte is in the window)
+                    record(e, jn < GW ? (nb == '\n' ? 1u : nb == '#' ? 3u : 2u) : 0u);
+                    s = e + 1;
+                    gn++;
+                    // the next line: past the span, its first byte not in
+                    // this window (the next round's head load checks it),
+                    // a '#' or empty line (LINE), or a data line (go on)
+                    if (s >= hi) { nextm = HOP_DONE; go = false; }
+                    else if (jn >= GW) go = false;
+                    else if (nb == '#' || nb == '\n') { nextm = HOP_LINE; go = false; }
+                }
+            }
+        }
+        if (act) {
+            mode = nextm;
+            p = s;
+            // the next windows: the mean length of the streak's lines (a
+            // chr22 prefix varies by ~9 bytes from line to line: guessed from
+            // the last line alone, 8 lines ahead drift past the window's
+            // +-96 bytes in 5 % of rounds, from the mean in 0.1 %)
+            L = (uint32_t)((float)(s - gs0) / (float)gn + 0.5f);
+        }
+    };
     while (vw::ballot(mode != HOP_DONE)) {
+        if (!LEARN) {
+            // every walker of the wave guessing or done: lean rounds -- the
+            // windows, the head byte and the GUESS steps, nothing else
+            while (vw::ballot(mode != HOP_GUESS && mode != HOP_DONE) == 0 && vw::ballot(mode == HOP_GUESS) != 0) {
+                const bool act = mode == HOP_GUESS;
+                uint4 w[HOP_GL];
+#pragma unroll
+                for (uint32_t k = 0; k < HOP_GL; k++)
+                    w[k] = act ? load16(buf, n, p - 1 + (uint64_t)(k + 1) * L - GUESS_LEAD + 16u * wl) : make_uint4(0, 0, 0, 0);
+                const uint32_t hd = act && p < n ? buf[p] : 0u;
+                if (l == w0 && act) VCFC_DIAG_HOP_READ(256u * HOP_GL + 1u);
+                guess_round(std::integral_constant<uint32_t, HOP_GL>(), w, hd, act);
+            }
+            if (vw::ballot(mode != HOP_DONE) == 0) break;
+        }
         const uint32_t mode0 = mode;   // (the round's mode: the steps below may switch it for the next round)
         // ---- loads: the main window (LINE: `rows` rows, FIND: 4), the guess window ----
         const uint64_t base = mode == HOP_FIND ? q : p;
         const uint32_t nr = mode == HOP_FIND ? 4u : mode == HOP_LINE ? rows : 0u;
         // (TRY: rows 0..2 hold the 256 bytes ending at each learned
         // candidate's end gt0 + G_k, all tried in one round)
+        // (GUESS: rows 0..3 are the windows of the next HOP_G guessed ends,
+        // window k from p - 1 + (k + 1) L - GUESS_LEAD; hd = the line's first byte)
+        const bool gm = !LEARN && mode == HOP_GUESS;
         uint4 v[4];
         uint32_t cvalid = 0;
 #pragma unroll
@@ -244,8 +420,10 @@ __global__ __launch_bounds__(256) void k_nl_hop(const uint8_t *buf, uint64_t n, 
             const bool cv = LEARN && k < 3 && mode == HOP_TRY && G != 0 && gt + G + 1 >= GW && gt + G < n;
             cvalid |= cv ? 1u << k : 0u;
             v[k] = k < nr ? load16(buf, n, base + 256u * k + 16u * wl)
-                          : cv ? *reinterpret_cast<const uint4 *>(buf + gt + G + 1 - GW + 16u * wl) : make_uint4(0, 0, 0, 0);
+                   : gm   ? load16(buf, n, p - 1 + (uint64_t)(k + 1) * L - GUESS_LEAD + 16u * wl)
+                   : cv ? *reinterpret_cast<const uint4 *>(buf + gt + G + 1 - GW + 16u * wl) : make_uint4(0, 0, 0, 0);
         }
+        const uint32_t hd = gm && p < n ? buf[p] : 0u;
         uint64_t g0 = 0;
         bool gok = true;   // (VERIFY / TRY / LEARN: the window ends at e = g0 + GW - 1)
         if (mode == HOP_LINE) {
@@ -260,7 +438,7 @@ __global__ __launch_bounds__(256) void k_nl_hop(const uint8_t *buf, uint64_t n, 
         const bool gv = mode != HOP_FIND && mode != HOP_DONE && g0 + GW <= n && gok;
         const uint4 ga = gv ? *reinterpret_cast<const uint4 *>(buf + g0 + 16u * wl) : make_uint4(0, 0, 0, 0);
         if (l == w0 && mode != HOP_DONE)
-            VCFC_DIAG_HOP_READ(256u * nr + (gv ? GW : 0u) + GW * (uint32_t)__builtin_popcount(cvalid));
+            VCFC_DIAG_HOP_READ(256u * nr + (gv ? GW : 0u) + GW * (uint32_t)__builtin_popcount(cvalid) + (gm ? 256u * HOP_G + 1u : 0u));
         // ---- the first '\n' of the main window (row-major: row k, then lane) ----
         uint64_t first = ~0ull;
 #pragma unroll
@@ -397,10 +575,18 @@ __global__ __launch_bounds__(256) void k_nl_hop(const uint8_t *buf, uint64_t n, 
             if (e >= hi) mode = HOP_DONE;
             else {
                 if (e >= lo) record(e);
+                // a data line found by LINE / VERIFY: guess the next ones from its length
+                const uint64_t Ln = e + 1 - p;
+                const bool g = !LEARN && ((mode0 == HOP_LINE && b0 != '#') || mode0 == HOP_VERIFY) && Ln >= GUESS_MIN &&
+                               Ln < (1ull << 30);
+                L = g ? (uint32_t)Ln : L;
+                gs0 = g ? p : gs0;
+                gn = g ? 1u : gn;
                 p = e + 1;
-                mode = p >= hi ? HOP_DONE : HOP_LINE;
+                mode = p >= hi ? HOP_DONE : g ? HOP_GUESS : HOP_LINE;
             }
         }
+        if (!LEARN && vw::ballot(mode0 == HOP_GUESS)) guess_round(std::integral_constant<uint32_t, HOP_G>(), v, hd, mode0 == HOP_GUESS);
     }
     for (; cur < nseg; cur++, cc = 0)
         if (l == w0) seg_cnt[sg0 + cur] = cc;
@@ -410,18 +596,28 @@ __global__ __launch_bounds__(256) void k_nl_hop(const uint8_t *buf, uint64_t n, 
 // a wave per segment spent ~0.1 ms launching 622k waves for 8 MB of
 // positions); a segment with more lines than its slot holds is scanned
 // again by the whole wave, one such segment after the other.
+// A line's kind is its first byte, the byte after the previous line's '\n':
+// each placed position gives the kind of the line after it, so no lane
+// needs another segment's positions (line 0: byte 0, by segment 0's lane).
 __global__ __launch_bounds__(256) void k_nl_place(const uint8_t *buf, uint64_t n, uint64_t n_seg, const uint32_t *seg_cnt,
                                                   const uint64_t *slot, const uint64_t *seg_base, uint64_t *nl,
-                                                  uint64_t *counts) {
+                                                  uint32_t *kind, uint64_t *counts) {
     const uint32_t l = vw::lane_id();
     const uint64_t seg0 = ((uint64_t)blockIdx.x * IX_WAVES + vw::readfirst(threadIdx.x >> 6)) * 64;
     if (seg0 >= n_seg) return;
     const uint64_t seg = seg0 + l;
     const uint32_t c = seg < n_seg ? seg_cnt[seg] : 0u;
+    if (seg == 0) kind[0] = line_kind_at(buf, n, 0);
     if (c <= NL_SLOT) {
         const uint64_t *sl = slot + seg * NL_SLOT;
-        uint64_t *dst = nl + (seg < n_seg ? seg_base[seg] : 0);
-        for (uint32_t k = 0; k < c; k++) dst[k] = sl[k];
+        const uint64_t b = seg < n_seg ? seg_base[seg] : 0;
+        uint64_t *dst = nl + b;
+        for (uint32_t k = 0; k < c; k++) {
+            const uint64_t xs = sl[k], x = xs & ((1ull << SLOT_KIND) - 1);
+            const uint32_t kh = (uint32_t)(xs >> SLOT_KIND);
+            dst[k] = x;
+            kind[b + k + 1] = kh ? kh - 1u : line_kind_at(buf, n, x + 1);
+        }
     }
     // more lines than the slot holds: scan the segment again, keeping at
     // most the c positions the count scan made room for.  The hop index may
@@ -437,40 +633,43 @@ __global__ __launch_bounds__(256) void k_nl_place(const uint8_t *buf, uint64_t n
         const uint32_t cf = vw::readlane(c, f);
         uint64_t *dst = nl + seg_base[sf];
         uint32_t o = 0;
-        for (uint32_t w = 0; w < SEG; w += WIN) o += nl_window(buf, n, sf * SEG + w + 16 * l, dst, o, cf);
+        for (uint32_t w = 0; w < SEG; w += WIN) o += nl_window(buf, n, sf * SEG + w + 16 * l, dst, o, cf, kind + seg_base[sf]);
         if (o != cf && l == 0) atomicMax((unsigned long long *)(counts + 3), 2ull);
     }
 }
 
-__global__ __launch_bounds__(256) void k_line_kind(const uint8_t *buf, const uint64_t *nl, uint64_t n_lines,
-                                                   uint32_t *is_data, uint32_t *is_pass) {
+// rank[i] = data lines before line i | '#' lines before it << 32
+__global__ __launch_bounds__(256) void k_line_place(const uint64_t *nl, uint64_t n_lines, const uint64_t *rank,
+                                                    VcfcLineIndex x) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_lines) return;
     const uint64_t s = i ? nl[i - 1] + 1 : 0u;
-    const bool nonempty = nl[i] > s;
-    const bool hash = nonempty && buf[s] == '#';
-    is_data[i] = nonempty && !hash;
-    is_pass[i] = hash;
-}
-
-__global__ __launch_bounds__(256) void k_line_place(const uint64_t *nl, uint64_t n_lines, const uint64_t *data_rank,
-                                                    const uint64_t *pass_rank, VcfcLineIndex x) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_lines) return;
-    const uint64_t s = i ? nl[i - 1] + 1 : 0u;
-    const uint64_t d = data_rank[i];
+    const uint64_t r0 = rank[i], r1 = rank[i + 1];
+    const uint64_t d = (uint32_t)r0, q = r0 >> 32;
+    if (i + 1 == n_lines) {   // the counts: data and '#' lines
+        x.counts[1] = (uint32_t)r1;
+        x.counts[2] = r1 >> 32;
+    }
     if (nl[i] - s > 0xFFFFFFFFull) atomicMax((unsigned long long *)(x.counts + 3), 1ull);   // line lengths are 32-bit
-    if (data_rank[i + 1] > d) {
+    if ((uint32_t)r1 > d) {
         x.line_off[d] = s;
         x.line_len[d] = (uint32_t)(nl[i] - s);
         x.line_no[d] = (uint32_t)i;
     }
-    const uint64_t q = pass_rank[i];
-    if (pass_rank[i + 1] > q) {
+    if ((r1 >> 32) > q) {
         x.pass_off[q] = s;
         x.pass_len[q] = (uint32_t)(nl[i] - s);
         x.pass_no[q] = (uint32_t)i;
         x.pass_before[q] = d;
+    }
+}
+
+// counts[0] = the line count (the segment scan's total), counts[3] = 0 (the
+// flags phase 2 raises), in one launch instead of a copy and a memset
+__global__ void k_index_counts(const uint64_t *total, uint64_t *counts) {
+    if (threadIdx.x == 0) {
+        counts[0] = *total;
+        counts[3] = 0;
     }
 }
 
@@ -486,14 +685,13 @@ VcfcLineIndexLayout vcfc_line_index_layout(uint64_t chunk_bytes, uint64_t n_line
     L.seg_cnt = o; o = al(o + 4 * seg);
     L.seg_base = o; o = al(o + 8 * (seg + 1));
     L.slot = o; o = al(o + 8ull * NL_SLOT * seg);
+    L.wstart = o; o = al(o + 8 * (seg / 2 + 2));   // hop walkers (each over >= 2 segments)
     L.partials1 = o; o = al(o + 8 * ((seg + 4095) / 4096 + 1));
     L.total1 = o;
     o = 0;
     L.nl = o; o = al(o + 8 * (n_lines + 1));
-    L.is_data = o; o = al(o + 4 * (n_lines + 1));
-    L.is_pass = o; o = al(o + 4 * (n_lines + 1));
-    L.data_rank = o; o = al(o + 8 * (n_lines + 1));
-    L.pass_rank = o; o = al(o + 8 * (n_lines + 1));
+    L.kind = o; o = al(o + 4 * (n_lines + 1));
+    L.rank = o; o = al(o + 8 * (n_lines + 1));
     L.partials2 = o; o = al(o + 8 * ((n_lines + 4095) / 4096 + 1));
     L.total2 = o;
     return L;
@@ -524,16 +722,20 @@ hipError_t vcfc_line_index(const uint8_t *buf, uint64_t n, uint8_t *ws, const Vc
         const uint64_t walkers = (n_seg + wseg - 1) / wseg;
         const uint64_t per_block = (uint64_t)HOPW * IX_WAVES;
         const dim3 hg((unsigned)((walkers + per_block - 1) / per_block));
+        uint64_t *wstart = reinterpret_cast<uint64_t *>(ws + L.wstart);
+        hipLaunchKernelGGL(k_nl_hop_start, dim3((unsigned)((walkers + IX_WAVES - 1) / IX_WAVES)), blk, 0, s, buf, n, n_seg,
+                           (uint32_t)wseg, walkers, wstart);
         if (hop_learn)
-            hipLaunchKernelGGL(k_nl_hop<true>, hg, blk, 0, s, buf, n, n_seg, S_hint, (uint32_t)wseg, seg_cnt, slot);
+            hipLaunchKernelGGL(k_nl_hop<true>, hg, blk, 0, s, buf, n, n_seg, S_hint, (uint32_t)wseg, wstart, seg_cnt, slot);
         else
-            hipLaunchKernelGGL(k_nl_hop<false>, hg, blk, 0, s, buf, n, n_seg, S_hint, (uint32_t)wseg, seg_cnt, slot);
+            hipLaunchKernelGGL(k_nl_hop<false>, hg, blk, 0, s, buf, n, n_seg, S_hint, (uint32_t)wseg, wstart, seg_cnt, slot);
     }
     else
         hipLaunchKernelGGL(k_nl_scan, sg, blk, 0, s, buf, n, n_seg, seg_cnt, slot);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = vcfc_scan_u32(seg_cnt, n_seg, partials, seg_base, s)) != hipSuccess) return e;
-    return hipMemcpyAsync(x.counts, seg_base + n_seg, 8, hipMemcpyDeviceToDevice, s);
+    hipLaunchKernelGGL(k_index_counts, dim3(1), dim3(64), 0, s, seg_base + n_seg, x.counts);
+    return hipGetLastError();
 }
 
 // Phase 2, once the host knows the line count (counts[0]): the '\n'
@@ -572,25 +774,17 @@ hipError_t vcfc_line_index_place(const uint8_t *buf, uint64_t n, uint64_t n_line
     const uint64_t *seg_base = reinterpret_cast<const uint64_t *>(ws1 + L.seg_base);
     const uint64_t *slot = reinterpret_cast<const uint64_t *>(ws1 + L.slot);
     uint64_t *nl = reinterpret_cast<uint64_t *>(ws2 + L.nl);
-    uint32_t *is_data = reinterpret_cast<uint32_t *>(ws2 + L.is_data);
-    uint32_t *is_pass = reinterpret_cast<uint32_t *>(ws2 + L.is_pass);
-    uint64_t *data_rank = reinterpret_cast<uint64_t *>(ws2 + L.data_rank);
-    uint64_t *pass_rank = reinterpret_cast<uint64_t *>(ws2 + L.pass_rank);
+    uint32_t *kind = reinterpret_cast<uint32_t *>(ws2 + L.kind);
+    uint64_t *rank = reinterpret_cast<uint64_t *>(ws2 + L.rank);
     uint64_t *partials = reinterpret_cast<uint64_t *>(ws2 + L.partials2);
     hipError_t e;
     if (n_lines == 0) return hipMemsetAsync(x.counts + 1, 0, 24, s);
-    if ((e = hipMemsetAsync(x.counts + 3, 0, 8, s)) != hipSuccess) return e;
+    // (counts[3] was zeroed by phase 1)
     const uint64_t n_seg = (n + SEG - 1) / SEG;
     hipLaunchKernelGGL(k_nl_place, dim3((unsigned)((n_seg + 64 * IX_WAVES - 1) / (64 * IX_WAVES))), dim3(64 * IX_WAVES), 0,
-                       s, buf, n, n_seg, seg_cnt, slot, seg_base, nl, x.counts);
+                       s, buf, n, n_seg, seg_cnt, slot, seg_base, nl, kind, x.counts);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    const dim3 g((unsigned)((n_lines + 255) / 256)), blk(256);
-    hipLaunchKernelGGL(k_line_kind, g, blk, 0, s, buf, nl, n_lines, is_data, is_pass);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    if ((e = vcfc_scan_u32(is_data, n_lines, partials, data_rank, s)) != hipSuccess) return e;
-    if ((e = vcfc_scan_u32(is_pass, n_lines, partials, pass_rank, s)) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_line_place, g, blk, 0, s, nl, n_lines, data_rank, pass_rank, x);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    if ((e = hipMemcpyAsync(x.counts + 1, data_rank + n_lines, 8, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
-    return hipMemcpyAsync(x.counts + 2, pass_rank + n_lines, 8, hipMemcpyDeviceToDevice, s);
+    if ((e = vcfc_scan_kinds(kind, n_lines, partials, rank, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_line_place, dim3((unsigned)((n_lines + 255) / 256)), dim3(256), 0, s, nl, n_lines, rank, x);
+    return hipGetLastError();
 }
