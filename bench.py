@@ -550,8 +550,8 @@ def bench_devfile(args, torch, vcfc, workload):
                       "deferred_records": args.deferred_records == "on",
                       "chunk": ("%d bytes of whole lines per line index + encode" % args.dev_chunk) if args.dev_chunk
                                else "the whole file (one line index, one encode)",
-                      "line_index": ("hop (line ends guessed from the header's sample count, ~1.2 KiB read per "
-                                     "line, checked by the encoder)") if hop else "scan of every byte (--line-index scan)"},
+                      "line_index": ("hop (line ends guessed from the header's sample count and the lines' "
+                                     "mean length, ~0.3 KiB read per chr22-shaped line, checked by the encoder)") if hop else "scan of every byte (--line-index scan)"},
            "roofline": {"kernel": "line index + encoder (whole step)", "bound": "hbm",
                         "achieved": round(alg / (ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
