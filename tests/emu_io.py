@@ -192,21 +192,22 @@ def emu_hop_read(reset=True):
     return int(L.emu_hop_read(1 if reset else 0))
 
 
-def emu_line_index(vcf, S_hint=0, hop_walkers=0, learn=True):
+def emu_line_index(vcf, S_hint=0, hop_walkers=0, learn=True, len_hint=0):
     """The GPU line index of vcf (ending in '\n') on the emulator: (counts
     [lines, data lines, pass lines, long], data line offsets, lengths).
     hop_walkers: walkers of the hop index (0: the product's count); learn:
     the walkers with learned candidates (TRY / LEARN), else the GUESS ones
-    (compress_device's choice for chr22-shaped files)."""
+    (compress_device's choice for chr22-shaped files); len_hint: the GUESS
+    walkers' first line length (compress_device: the first data line's)."""
     cap = vcf.count(b"\n") + 1
     off = np.zeros(cap, dtype=np.uint64)
     ln = np.zeros(cap, dtype=np.uint32)
     cnt = np.zeros(4, dtype=np.uint64)
     L = lib()
     L.emu_line_index.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
-                                 ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int]
+                                 ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_uint32]
     st = L.emu_line_index(vcf, len(vcf), S_hint, off.ctypes.data, ln.ctypes.data, cap, cnt.ctypes.data, hop_walkers,
-                          1 if learn else 0)
+                          1 if learn else 0, len_hint)
     assert st == 0
     k = int(cnt[1])
     return [int(c) for c in cnt], off[:k].tolist(), ln[:k].tolist()

@@ -236,16 +236,17 @@ extern "C" int emu_held(const uint8_t *data, uint64_t n, uint64_t piece, uint64_
 
 // The line index (csrc/vcfc_ingest.hip) of in[0, n) (last byte '\n'): the
 // data lines' offsets and lengths and the counts; S_hint != 0: the hop index
-// (learn: its TRY / LEARN walkers, else the GUESS ones).
+// (learn: its TRY / LEARN walkers, else the GUESS ones; len_hint: their
+// first guess, compress_device's first data line length).
 extern "C" int emu_line_index(const uint8_t *in, uint64_t n, uint32_t S_hint, uint64_t *off, uint32_t *len,
-                              uint64_t cap, uint64_t *counts, uint64_t hop_walkers, int learn) {
+                              uint64_t cap, uint64_t *counts, uint64_t hop_walkers, int learn, uint32_t len_hint) {
     const VcfcLineIndexLayout L1 = vcfc_line_index_layout(n, 0);
     std::vector<uint8_t> ws1(L1.total1 + 64);
     std::vector<uint64_t> cnt(4, 0);
     VcfcLineIndex x;
     memset(&x, 0, sizeof x);
     x.counts = cnt.data();
-    if (vcfc_line_index(in, n, ws1.data(), L1, x, nullptr, S_hint, hop_walkers, learn != 0) != hipSuccess) return 1;
+    if (vcfc_line_index(in, n, ws1.data(), L1, x, nullptr, S_hint, hop_walkers, learn != 0, len_hint) != hipSuccess) return 1;
     const uint64_t lines = cnt[0];
     const VcfcLineIndexLayout L = vcfc_line_index_layout(n, lines);
     std::vector<uint8_t> ws2(L.total2 + 64);

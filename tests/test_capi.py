@@ -99,7 +99,7 @@ def test_links_the_real_hip_runtime_with_no_undefined_symbols(lib):
 
 DIAG_SWITCHES = ["VCFC_DIAG_NOSTORE", "VCFC_DIAG_NOSTEP", "VCFC_DIAG_CLEAN_SKIP", "VCFC_VAR_SIZE_ONLY",
                  "VCFC_DIAG_DEC_NOSCAN", "VCFC_DIAG_NOESCEMIT",
-                 "VCFC_DIAG_NODIRECT"]
+                 "VCFC_DIAG_NODIRECT", "VCFC_DIAG_HOP_TWICE"]
 
 
 @pytest.mark.parametrize("sw", DIAG_SWITCHES)

@@ -160,6 +160,14 @@ def test_hop_guess_rounds(S, jitter, walkers):
     line = E.emu_hop_read()
     if S == 2504 and jitter == 40:
         assert guess < 0.04 * len(vcf) and guess < 0.7 * line, (guess, line, len(vcf))
+    # every walker's first lines guessed from the first data line's length
+    # (compress_device's len_hint) instead of found by LINE
+    first = next(ln for ln in vcf.split(b"\n") if ln and not ln.startswith(b"#"))
+    assert E.emu_line_index(vcf, S, hop_walkers=walkers, learn=False, len_hint=len(first) + 1) == scan
+    hinted = E.emu_hop_read()
+    if S == 2504 and jitter == 40:
+        assert hinted < guess, (hinted, guess)
+    assert E.emu_line_index(vcf, S, hop_walkers=walkers, learn=False, len_hint=700) == scan   # a wrong hint
     check(vcf, 1 << 22, "guess S=%d" % S)
 
 

@@ -8,7 +8,7 @@
 // the Makefile, tests/test_capi.py::test_diag_switches_refused).
 #if (defined(VCFC_DIAG_NOSTORE) || defined(VCFC_DIAG_NOSTEP) || defined(VCFC_DIAG_CLEAN_SKIP) || \
      defined(VCFC_VAR_SIZE_ONLY) || defined(VCFC_DIAG_DEC_NOSCAN) || defined(VCFC_DIAG_NOESCEMIT) || \
-     defined(VCFC_DIAG_NODIRECT)) && \
+     defined(VCFC_DIAG_NODIRECT) || defined(VCFC_DIAG_HOP_TWICE)) && \
     !defined(VCFC_DIAG_BUILD)
 #error "VCFC_DIAG_* / VCFC_VAR_SIZE_ONLY produce wrong output: diagnostic builds only (define VCFC_DIAG_BUILD)"
 #endif
@@ -273,10 +273,13 @@ VcfcLineIndexLayout vcfc_line_index_layout(uint64_t chunk_bytes, uint64_t n_line
 // hop_walkers: walkers of the hop index (0: HOP_WALKERS; the tests use a few,
 // so each walks as many lines as at config size).  hop_learn: the walkers
 // learn the genotype-region lengths of lines that are not 3-byte tokens
-// (TRY / LEARN, k_nl_hop<true>).
+// (TRY / LEARN, k_nl_hop<true>).  len_hint (!hop_learn; 0: none): a data
+// line's length with its '\n' (the file's first): every walker but the
+// first guesses its first lines from it (GUESS) instead of reading the
+// first line's prefix.
 hipError_t vcfc_line_index(const uint8_t *buf, uint64_t n, uint8_t *ws, const VcfcLineIndexLayout &L,
                            const VcfcLineIndex &x, hipStream_t s, uint32_t S_hint = 0, uint64_t hop_walkers = 0,
-                           bool hop_learn = true);
+                           bool hop_learn = true, uint32_t len_hint = 0);
 // phase 2 (n_lines = counts[0]): '\n' positions, data / pass line arrays; counts[1], counts[2]
 hipError_t vcfc_line_index_place(const uint8_t *buf, uint64_t n, uint64_t n_lines, const uint8_t *ws1, uint8_t *ws2,
                                  const VcfcLineIndexLayout &L, const VcfcLineIndex &x, hipStream_t s);

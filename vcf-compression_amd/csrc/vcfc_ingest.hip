@@ -273,13 +273,13 @@ __global__ __launch_bounds__(256) void k_nl_hop_start(const uint8_t *buf, uint64
 // dwords) and costs the configs[1] device file +3.7 %, while law-2 files go
 // 16.5 -> 13.7 ms (profiles/r04/ab/ab_tall_law*.txt); without it the walker
 // is round 3's (86 VGPRs, 5 waves).
-template <bool LEARN>
+template <bool LEARN, bool NOSTORE = false>   // (NOSTORE: VCFC_DIAG_HOP_TWICE's timing copy)
 // (round 6: pinned to 6 waves per SIMD, 80 VGPRs and a 12-byte spill, the
 // same speed; to 8, 64 VGPRs and 72 bytes spilled, +4 %:
 // profiles/r06/ab/ab_r6hop_devfile_law1.txt)
 __global__ __launch_bounds__(256) void k_nl_hop(const uint8_t *buf, uint64_t n, uint64_t n_seg, uint32_t S,
                                                 uint32_t wseg, const uint64_t *wstart, uint32_t *seg_cnt,
-                                                uint64_t *slot) {
+                                                uint64_t *slot, uint32_t L0) {
     const uint32_t l = vw::lane_id(), wl = l & 15u, w0 = l & ~15u, sh = l & 48u;   // w0: the walker's first lane
     const uint64_t walker = ((uint64_t)blockIdx.x * IX_WAVES + (threadIdx.x >> 6)) * HOPW + (l >> 4);
     const uint64_t sg0 = walker * wseg;                              // the walker's first segment
@@ -299,22 +299,30 @@ __global__ __launch_bounds__(256) void k_nl_hop(const uint8_t *buf, uint64_t n, 
     bool lrn = false, tdef = false;     // tdef: the TRY round also checks the 3-byte end e (VERIFY's job)
     // (the walker's lanes; lo <= x < hi, in order).  kh: the kind of the
     // line after x when the walker saw its first byte (SLOT_KIND), else 0
+    uint64_t nsacc = 0;                 // (NOSTORE: the positions' checksum, the walk's only output)
     auto record = [&](uint64_t x, uint32_t kh = 0) {
         const uint32_t k = (uint32_t)((x - lo) / SEG);
+        if (NOSTORE) nsacc = nsacc * 31u + x + kh + cur + cc;
         for (; cur < k; cur++, cc = 0)
-            if (l == w0) seg_cnt[sg0 + cur] = cc;
-        if (l == w0 && cc < NL_SLOT) slot[(sg0 + cur) * NL_SLOT + cc] = x | ((uint64_t)kh << SLOT_KIND);
+            if (!NOSTORE && l == w0) seg_cnt[sg0 + cur] = cc;
+        if (!NOSTORE && l == w0 && cc < NL_SLOT) slot[(sg0 + cur) * NL_SLOT + cc] = x | ((uint64_t)kh << SLOT_KIND);
         cc++;
     };
     auto wbits = [&](bool pr) { return (uint32_t)(vw::ballot(pr) >> sh) & 0xFFFFu; };
-    // the walker's first line end (k_nl_hop_start): the walk starts after it
+    // the walker's first line end (k_nl_hop_start): the walk starts after it,
+    // guessing from L0 (the host's first data line; as if a line of that
+    // length ended at p - 1) when there is one
     if (mode != HOP_DONE && lo != 0) {
         const uint64_t e0 = wstart[walker];
         if (e0 == ~0ull) mode = HOP_DONE;
         else {
             if (e0 >= lo) record(e0);
             p = e0 + 1;
-            mode = p >= hi ? HOP_DONE : HOP_LINE;
+            const bool g = !LEARN && L0 >= GUESS_MIN;
+            L = g ? L0 : L;
+            gs0 = p - L0;   // (mod 2^64: s - gs0 stays exact)
+            gn = 1;
+            mode = p >= hi ? HOP_DONE : g ? HOP_GUESS : HOP_LINE;
         }
     }
     // learned candidates to try (trusted walkers, data lines only)
@@ -589,7 +597,8 @@ __global__ __launch_bounds__(256) void k_nl_hop(const uint8_t *buf, uint64_t n, 
         if (!LEARN && vw::ballot(mode0 == HOP_GUESS)) guess_round(std::integral_constant<uint32_t, HOP_G>(), v, hd, mode0 == HOP_GUESS);
     }
     for (; cur < nseg; cur++, cc = 0)
-        if (l == w0) seg_cnt[sg0 + cur] = cc;
+        if (!NOSTORE && l == w0) seg_cnt[sg0 + cur] = cc;
+    if (NOSTORE && l == w0 && nsacc == 0x5EED5EED5EED5EEDull) seg_cnt[sg0] = 0;   // (keeps the walk alive)
 }
 
 // One wave per 64 segments, one lane per segment (most hold a few lines:
@@ -704,7 +713,7 @@ VcfcLineIndexLayout vcfc_line_index_layout(uint64_t chunk_bytes, uint64_t n_line
 // one byte and its '\n') and n pass lines.
 hipError_t vcfc_line_index(const uint8_t *buf, uint64_t n, uint8_t *ws, const VcfcLineIndexLayout &L,
                            const VcfcLineIndex &x, hipStream_t s, uint32_t S_hint, uint64_t hop_walkers,
-                           bool hop_learn) {
+                           bool hop_learn, uint32_t len_hint) {
     // ws: phase 1 workspace (L.total1 bytes)
     uint32_t *seg_cnt = reinterpret_cast<uint32_t *>(ws + L.seg_cnt);
     uint64_t *seg_base = reinterpret_cast<uint64_t *>(ws + L.seg_base);
@@ -726,9 +735,16 @@ hipError_t vcfc_line_index(const uint8_t *buf, uint64_t n, uint8_t *ws, const Vc
         hipLaunchKernelGGL(k_nl_hop_start, dim3((unsigned)((walkers + IX_WAVES - 1) / IX_WAVES)), blk, 0, s, buf, n, n_seg,
                            (uint32_t)wseg, walkers, wstart);
         if (hop_learn)
-            hipLaunchKernelGGL(k_nl_hop<true>, hg, blk, 0, s, buf, n, n_seg, S_hint, (uint32_t)wseg, wstart, seg_cnt, slot);
-        else
-            hipLaunchKernelGGL(k_nl_hop<false>, hg, blk, 0, s, buf, n, n_seg, S_hint, (uint32_t)wseg, wstart, seg_cnt, slot);
+            hipLaunchKernelGGL(k_nl_hop<true>, hg, blk, 0, s, buf, n, n_seg, S_hint, (uint32_t)wseg, wstart, seg_cnt, slot,
+                               0u);
+        else {
+#ifdef VCFC_DIAG_HOP_TWICE   // (diagnostic timing: the walk once without its stores, then the real one)
+            hipLaunchKernelGGL((k_nl_hop<false, true>), hg, blk, 0, s, buf, n, n_seg, S_hint, (uint32_t)wseg, wstart,
+                               seg_cnt, slot, len_hint);
+#endif
+            hipLaunchKernelGGL(k_nl_hop<false>, hg, blk, 0, s, buf, n, n_seg, S_hint, (uint32_t)wseg, wstart, seg_cnt, slot,
+                               len_hint);
+        }
     }
     else
         hipLaunchKernelGGL(k_nl_scan, sg, blk, 0, s, buf, n, n_seg, seg_cnt, slot);

@@ -215,6 +215,25 @@ inline bool data_lines_irregular(const uint8_t *p, uint64_t len, uint32_t S) {
     return false;
 }
 
+// The length (with its '\n') of the first data line after "#CHROM" that lies
+// whole in p[0, len), or 0: the hop index's first guess (vcfc_line_index
+// len_hint) for every walker's first line.
+inline uint32_t first_data_line_len(const uint8_t *p, uint64_t len) {
+    bool in_data = false;
+    for (uint64_t q = 0; q < len;) {
+        const uint8_t *nl = static_cast<const uint8_t *>(memchr(p + q, '\n', len - q));
+        if (!nl) break;
+        const uint64_t end = (uint64_t)(nl - p);
+        if (!in_data) {
+            in_data = end - q >= 7 && memcmp(p + q, "#CHROM\t", 7) == 0;
+        } else if (end > q && p[q] != '#') {
+            return end + 1 - q < (1ull << 30) ? (uint32_t)(end + 1 - q) : 0u;
+        }
+        q = end + 1;
+    }
+    return 0;
+}
+
 namespace detail {
 
 inline double now_s() {
@@ -652,7 +671,7 @@ inline int compress_device(const uint8_t *d_in, uint64_t N, uint8_t *d_out, uint
     // (VCFC_LINE_INDEX_SCAN): always every byte.  The file's last byte comes
     // with the first header window (one round trip); the window stays on the
     // host for the '#' lines' check below (h0: d_in[0, h0_len)).
-    uint32_t S_hint = 0;
+    uint32_t S_hint = 0, len_hint = 0;
     bool learn = false;
     const uint8_t *h0 = nullptr;
     uint64_t h0_len = 0;
@@ -674,6 +693,7 @@ inline int compress_device(const uint8_t *d_in, uint64_t N, uint8_t *d_out, uint
                 const uint64_t cap = std::min<uint64_t>(N, 1u << 20);
                 if (!more || want >= cap) {
                     learn = S_hint && (cfg.hop_learn > 0 || (cfg.hop_learn < 0 && data_lines_irregular(h, want, S_hint)));
+                    len_hint = S_hint ? first_data_line_len(h, want) : 0u;
                     break;
                 }
                 want = cap;
@@ -721,7 +741,7 @@ inline int compress_device(const uint8_t *d_in, uint64_t N, uint8_t *d_out, uint
         if (!d_ix1) return ST_E_HIP;
         VcfcLineIndex x;
         x.counts = d_small;
-        if (vcfc_line_index(d_c, n, d_ix1, L1, x, s, hop, cfg.hop_walkers, learn) != hipSuccess ||
+        if (vcfc_line_index(d_c, n, d_ix1, L1, x, s, hop, cfg.hop_walkers, learn, len_hint) != hipSuccess ||
             !d2h(hsmall, d_small, 8) || !sync())
             return ST_E_HIP;
         const uint64_t n_lines = hsmall[0];
