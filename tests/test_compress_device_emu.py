@@ -242,6 +242,21 @@ def test_hop_index_law2_rows(S, dp_width):
         assert st == st_o == OK and got == want, hop
 
 
+def test_hop_seeded_candidates_law2():
+    """Round 6: compress_device seeds the learning walkers with the region
+    lengths and TAB signatures of the irregular data lines in its header
+    window (vcfc_ingest_driver.h learn_candidates): the output is the
+    oracle's, and on a 120-row law-2 file the walkers read well under half
+    of it (they no longer FIND and LEARN each row kind first)."""
+    vcf = law2_like(random.Random(2506), 120, 2504, dp_width=2)
+    st_o, want, _ = G.oracle_compress(vcf)
+    E.emu_hop_read()
+    st, got, _ = E.emu_compress_device(vcf, chunk=1 << 24)
+    read = E.emu_hop_read()
+    assert st == st_o == OK and got == want
+    assert read < 0.4 * len(vcf), (read, len(vcf))
+
+
 def test_law2_rows_deferred_records(monkeypatch):
     """compress_device with deferred records on (vcfc_ctx_set_deferred_records):
     law-2-shaped files whose GT:DP:GQ rows are sized first and written straight

@@ -277,9 +277,17 @@ VcfcLineIndexLayout vcfc_line_index_layout(uint64_t chunk_bytes, uint64_t n_line
 // line's length with its '\n' (the file's first): every walker but the
 // first guesses its first lines from it (GUESS) instead of reading the
 // first line's prefix.
+// Learned candidates handed to every TRY / LEARN walker at its start (the
+// host's: data lines of the file's first window whose genotype region is not
+// 4 S - 1 bytes): region length g[k] (0: none) and, for each of the 16 lanes
+// of a walker, the TAB mask of its 16 bytes of the 256 ending at the '\n'.
+struct VcfcHopCands {
+    uint32_t g[3];
+    uint16_t sig[3][16];
+};
 hipError_t vcfc_line_index(const uint8_t *buf, uint64_t n, uint8_t *ws, const VcfcLineIndexLayout &L,
                            const VcfcLineIndex &x, hipStream_t s, uint32_t S_hint = 0, uint64_t hop_walkers = 0,
-                           bool hop_learn = true, uint32_t len_hint = 0);
+                           bool hop_learn = true, uint32_t len_hint = 0, const VcfcHopCands *cands = nullptr);
 // phase 2 (n_lines = counts[0]): '\n' positions, data / pass line arrays; counts[1], counts[2]
 hipError_t vcfc_line_index_place(const uint8_t *buf, uint64_t n, uint64_t n_lines, const uint8_t *ws1, uint8_t *ws2,
                                  const VcfcLineIndexLayout &L, const VcfcLineIndex &x, hipStream_t s);

@@ -28,6 +28,7 @@
 //                 last lane: the counts)
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <cstring>
 #include <type_traits>
 #include <vcfc_wave.h>   // angle brackets: tests/simt_emu shadows it
 #include "vcfc_device.h"
@@ -279,7 +280,7 @@ template <bool LEARN, bool NOSTORE = false>   // (NOSTORE: VCFC_DIAG_HOP_TWICE's
 // profiles/r06/ab/ab_r6hop_devfile_law1.txt)
 __global__ __launch_bounds__(256) void k_nl_hop(const uint8_t *buf, uint64_t n, uint64_t n_seg, uint32_t S,
                                                 uint32_t wseg, const uint64_t *wstart, uint32_t *seg_cnt,
-                                                uint64_t *slot, uint32_t L0) {
+                                                uint64_t *slot, uint32_t L0, VcfcHopCands hc) {
     const uint32_t l = vw::lane_id(), wl = l & 15u, w0 = l & ~15u, sh = l & 48u;   // w0: the walker's first lane
     const uint64_t walker = ((uint64_t)blockIdx.x * IX_WAVES + (threadIdx.x >> 6)) * HOPW + (l >> 4);
     const uint64_t sg0 = walker * wseg;                              // the walker's first segment
@@ -293,8 +294,12 @@ __global__ __launch_bounds__(256) void k_nl_hop(const uint8_t *buf, uint64_t n, 
     uint32_t gn = 0;                    // ... and its lines so far
     uint32_t cur = 0, cc = 0;           // current segment (in the span) and its count
     // learned candidates (walker-uniform lengths; this lane's 16-bit TAB mask of each)
-    uint32_t cg[HOP_K] = {0, 0, 0}, csig[HOP_K] = {0, 0, 0};
-    uint32_t ins = 0, trust = HOP_TRUST;
+    // (round 6: seeded with the host's candidates from the file's first
+    // lines, so a wave need not FIND and LEARN each row kind first)
+    uint32_t cg[HOP_K] = {hc.g[0], hc.g[1], hc.g[2]};
+    uint32_t csig[HOP_K] = {hc.sig[0][wl], hc.sig[1][wl], hc.sig[2][wl]};
+    uint32_t ins = (hc.g[0] != 0) + (hc.g[1] != 0) + (hc.g[2] != 0), trust = HOP_TRUST;
+    ins = ins == HOP_K ? 0u : ins;
     uint64_t gt = 0;                    // the current data line's gt0 (lrn: it may be learned)
     bool lrn = false, tdef = false;     // tdef: the TRY round also checks the 3-byte end e (VERIFY's job)
     // (the walker's lanes; lo <= x < hi, in order).  kh: the kind of the
@@ -713,7 +718,7 @@ VcfcLineIndexLayout vcfc_line_index_layout(uint64_t chunk_bytes, uint64_t n_line
 // one byte and its '\n') and n pass lines.
 hipError_t vcfc_line_index(const uint8_t *buf, uint64_t n, uint8_t *ws, const VcfcLineIndexLayout &L,
                            const VcfcLineIndex &x, hipStream_t s, uint32_t S_hint, uint64_t hop_walkers,
-                           bool hop_learn, uint32_t len_hint) {
+                           bool hop_learn, uint32_t len_hint, const VcfcHopCands *cands) {
     // ws: phase 1 workspace (L.total1 bytes)
     uint32_t *seg_cnt = reinterpret_cast<uint32_t *>(ws + L.seg_cnt);
     uint64_t *seg_base = reinterpret_cast<uint64_t *>(ws + L.seg_base);
@@ -734,16 +739,19 @@ hipError_t vcfc_line_index(const uint8_t *buf, uint64_t n, uint8_t *ws, const Vc
         uint64_t *wstart = reinterpret_cast<uint64_t *>(ws + L.wstart);
         hipLaunchKernelGGL(k_nl_hop_start, dim3((unsigned)((walkers + IX_WAVES - 1) / IX_WAVES)), blk, 0, s, buf, n, n_seg,
                            (uint32_t)wseg, walkers, wstart);
+        VcfcHopCands hc;
+        memset(&hc, 0, sizeof hc);
+        if (cands && hop_learn) hc = *cands;
         if (hop_learn)
             hipLaunchKernelGGL(k_nl_hop<true>, hg, blk, 0, s, buf, n, n_seg, S_hint, (uint32_t)wseg, wstart, seg_cnt, slot,
-                               0u);
+                               0u, hc);
         else {
 #ifdef VCFC_DIAG_HOP_TWICE   // (diagnostic timing: the walk once without its stores, then the real one)
             hipLaunchKernelGGL((k_nl_hop<false, true>), hg, blk, 0, s, buf, n, n_seg, S_hint, (uint32_t)wseg, wstart,
-                               seg_cnt, slot, len_hint);
+                               seg_cnt, slot, len_hint, hc);
 #endif
             hipLaunchKernelGGL(k_nl_hop<false>, hg, blk, 0, s, buf, n, n_seg, S_hint, (uint32_t)wseg, wstart, seg_cnt, slot,
-                               len_hint);
+                               len_hint, hc);
         }
     }
     else

@@ -234,6 +234,40 @@ inline uint32_t first_data_line_len(const uint8_t *p, uint64_t len) {
     return 0;
 }
 
+// The TRY / LEARN walkers' first candidates (VcfcHopCands): the data lines
+// of p[0, len) after "#CHROM" whose genotype region (after the 9th TAB, up
+// to the '\n') is not 4 S - 1 bytes and at least 255 -- up to three distinct
+// region lengths, each with the TAB masks of the 256 bytes ending at its
+// '\n', exactly what a walker's LEARN takes from such a line.
+inline void learn_candidates(const uint8_t *p, uint64_t len, uint32_t S, VcfcHopCands *c) {
+    memset(c, 0, sizeof *c);
+    uint32_t k = 0;
+    bool in_data = false;
+    for (uint64_t q = 0; q < len && k < 3;) {
+        const uint8_t *nl = static_cast<const uint8_t *>(memchr(p + q, '\n', len - q));
+        if (!nl) break;
+        const uint64_t end = (uint64_t)(nl - p);
+        if (!in_data) {
+            in_data = end - q >= 7 && memcmp(p + q, "#CHROM\t", 7) == 0;
+        } else if (end > q && p[q] != '#') {
+            uint64_t t = q;
+            uint32_t tabs = 0;
+            for (; t < end && tabs < 9; t++) tabs += p[t] == '\t';
+            const uint64_t G = end - t;   // t: the first sample byte (when 9 TABs were found)
+            if (tabs == 9 && G != 4ull * S - 1 && G >= 255 && G < (1ull << 31) && G != c->g[0] && G != c->g[1]) {
+                const uint64_t g0 = end + 1 - 256;
+                for (uint32_t wl = 0; wl < 16; wl++) {
+                    uint32_t m = 0;
+                    for (uint32_t j = 0; j < 16; j++) m |= (p[g0 + 16 * wl + j] == '\t' ? 1u : 0u) << j;
+                    c->sig[k][wl] = (uint16_t)m;
+                }
+                c->g[k++] = (uint32_t)G;
+            }
+        }
+        q = end + 1;
+    }
+}
+
 namespace detail {
 
 inline double now_s() {
@@ -673,6 +707,8 @@ inline int compress_device(const uint8_t *d_in, uint64_t N, uint8_t *d_out, uint
     // host for the '#' lines' check below (h0: d_in[0, h0_len)).
     uint32_t S_hint = 0, len_hint = 0;
     bool learn = false;
+    VcfcHopCands cands;
+    memset(&cands, 0, sizeof cands);
     const uint8_t *h0 = nullptr;
     uint64_t h0_len = 0;
     {
@@ -694,6 +730,7 @@ inline int compress_device(const uint8_t *d_in, uint64_t N, uint8_t *d_out, uint
                 if (!more || want >= cap) {
                     learn = S_hint && (cfg.hop_learn > 0 || (cfg.hop_learn < 0 && data_lines_irregular(h, want, S_hint)));
                     len_hint = S_hint ? first_data_line_len(h, want) : 0u;
+                    if (learn) learn_candidates(h, want, S_hint, &cands);
                     break;
                 }
                 want = cap;
@@ -741,7 +778,8 @@ inline int compress_device(const uint8_t *d_in, uint64_t N, uint8_t *d_out, uint
         if (!d_ix1) return ST_E_HIP;
         VcfcLineIndex x;
         x.counts = d_small;
-        if (vcfc_line_index(d_c, n, d_ix1, L1, x, s, hop, cfg.hop_walkers, learn, len_hint) != hipSuccess ||
+        if (vcfc_line_index(d_c, n, d_ix1, L1, x, s, hop, cfg.hop_walkers, learn, len_hint, &cands) !=
+                hipSuccess ||
             !d2h(hsmall, d_small, 8) || !sync())
             return ST_E_HIP;
         const uint64_t n_lines = hsmall[0];
