@@ -399,17 +399,33 @@ __global__ __launch_bounds__(256) void k_dec_seq(VcfcDecodeArgs a) {
     }
 }
 
-__device__ __forceinline__ void write_one(const VcfcDecodeArgs &a, uint64_t i, uint8_t *sb, uint32_t *W) {
+// A record's metadata (record start / end, line start / end, plan status).
+struct RecMeta {
+    uint64_t rs, re, l0, l1;
+    uint32_t st;
+};
+__device__ __forceinline__ RecMeta rec_meta(const VcfcDecodeArgs &a, uint64_t i) {
+    return RecMeta{a.rec_start[i], a.rec_start[i + 1], a.line_off[i], a.line_off[i + 1], a.st[i]};
+}
+
+// PRE: the record's metadata comes preloaded in mt (the selected decode),
+// else it is loaded here where it is used (the full decode: loading it all
+// up front was +1.6 %, profiles/r06/ab/ab_r6selpf_dec.txt)
+template <bool PRE>
+__device__ __forceinline__ void write_one(const VcfcDecodeArgs &a, uint64_t i, const RecMeta &mt, uint8_t *sb,
+                                          uint32_t *W) {
     const uint32_t l = vw::lane_id();
-    const uint64_t rs_abs = a.rec_start[i];
-    const uint64_t L0 = a.line_off[i];
-    if (a.line_off[i + 1] > a.out_cap) {
+    const uint64_t rs_abs = PRE ? mt.rs : a.rec_start[i];
+    const uint64_t L0 = PRE ? mt.l0 : a.line_off[i];
+    const uint64_t L1 = PRE ? mt.l1 : a.line_off[i + 1];
+    if (L1 > a.out_cap) {
         if (l == 0) atomicMin((unsigned long long *)a.err, (unsigned long long)((i << 8) | 0xFFu));
         return;
     }
     uint8_t *line = a.out + L0;
-    if (a.st[i] == DS_ERR || a.st[i] == DS_SKIP) return;   // no line (size 0)
-    if (a.st[i] != DS_SIMPLE) {
+    const uint32_t rst = PRE ? mt.st : a.st[i];
+    if (rst == DS_ERR || rst == DS_SKIP) return;   // no line (size 0)
+    if (rst != DS_SIMPLE) {
         if (l == 0) {
             uint64_t size, end;
             (void)dec_line_seq(a.in, a.n_bytes, rs_abs, a.S, line, &size, &end);
@@ -417,13 +433,13 @@ __device__ __forceinline__ void write_one(const VcfcDecodeArgs &a, uint64_t i, u
         return;
     }
     const uint64_t rbase = rs_abs & ~15ull;
-    const uint32_t rs = (uint32_t)(rs_abs - rbase), re = (uint32_t)(a.rec_start[i + 1] - rbase);
+    const uint32_t rs = (uint32_t)(rs_abs - rbase), re = (uint32_t)((PRE ? mt.re : a.rec_start[i + 1]) - rbase);
     const uint32_t S = (uint32_t)a.S;
     Staged sg;
     sg.init(sb, a.in + rbase, re);
     sg.load(rs);
     const uint32_t req = ((sg.at(rs + 4) & 0x3Fu) << 24) | (sg.at(rs + 5) << 16) | (sg.at(rs + 6) << 8) | sg.at(rs + 7);
-    const uint32_t slen = (uint32_t)(a.line_off[i + 1] - L0 - 4ull * S);   // REQ' = line - 4S
+    const uint32_t slen = (uint32_t)(L1 - L0 - 4ull * S);   // REQ' = line - 4S
     // copy REQ', and check what a light plan assumed: 9 TABs in REQ, REQ'
     // ends at REQ's first NUL (an exact plan made both true)
     // (4 bytes per lane, 256 per step: one step for REQs of the usual size)
@@ -575,14 +591,24 @@ __global__ __launch_bounds__(256) void k_dec_write(VcfcDecodeArgs a, uint64_t fi
     uint32_t *W = tbuf + wave * (TB + 4);
     const uint64_t g = (uint64_t)blockIdx.x * DEC_WAVES + wave;
     if (!SEL) {
-        if (first + g < last) write_one(a, first + g, sb, W);
+        if (first + g < last) write_one<false>(a, first + g, RecMeta{0, 0, 0, 0, 0}, sb, W);
         return;
     }
     const uint64_t G = (uint64_t)gridDim.x * DEC_WAVES;
     const uint32_t l = vw::lane_id();
     const uint64_t il = first + g + (uint64_t)l * G;
-    for (uint64_t m = vw::ballot(l < SEL_R && il < last && a.select[il]); m; m &= m - 1)
-        write_one(a, first + g + (uint64_t)__builtin_ctzll(m) * G, sb, W);
+    // (round 6: each candidate's metadata loaded with its flag, by its own
+    // lane, so the selected record's loads do not wait for the flags)
+    const bool cand = l < SEL_R && il < last;
+    const RecMeta ml = cand ? rec_meta(a, il) : RecMeta{0, 0, 0, 0, 0};
+    for (uint64_t m = vw::ballot(cand && a.select[il]); m; m &= m - 1) {
+        const uint32_t j = (uint32_t)__builtin_ctzll(m);
+        auto rl64 = [&](uint64_t v) {
+            return ((uint64_t)vw::readlane((uint32_t)(v >> 32), j) << 32) | vw::readlane((uint32_t)v, j);
+        };
+        const RecMeta mj{rl64(ml.rs), rl64(ml.re), rl64(ml.l0), rl64(ml.l1), vw::readlane(ml.st, j)};
+        write_one<true>(a, first + g + (uint64_t)j * G, mj, sb, W);
+    }
 }
 
 // Byte-serial decode of [p, n), at most max_lines lines: out == nullptr
