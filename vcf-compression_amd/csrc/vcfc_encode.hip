@@ -2136,8 +2136,14 @@ __global__ __launch_bounds__(256) void k_compact_out(const uint8_t *__restrict__
                                                      const uint64_t *__restrict__ rec_off, uint64_t n,
                                                      const uint32_t *__restrict__ tile_first,
                                                      uint8_t *__restrict__ out, uint64_t out_cap, uint32_t pb,
-                                                     const uint32_t *gate) {
+                                                     const uint32_t *gate, const uint32_t *__restrict__ rec_size,
+                                                     const uint32_t *defer_count) {
     if (gate && *gate == 0) return;   // (the second compaction: only after a misprediction)
+    // (round 6: with deferred records in the batch, a 16-byte block whose
+    // bytes all belong to deferred records is neither loaded nor stored --
+    // k_encode_defer writes it; blocks shared with a staged record are
+    // copied whole as before, their deferred bytes rewritten by k_encode_defer)
+    const bool anyd = defer_count && vw::readfirst(*defer_count) != 0;
     const uint32_t l = vw::lane_id();
     const uint64_t g = (uint64_t)blockIdx.x * 4 + vw::readfirst(threadIdx.x >> 6);
     const uint64_t G = (uint64_t)gridDim.x * 4;
@@ -2154,6 +2160,8 @@ __global__ __launch_bounds__(256) void k_compact_out(const uint8_t *__restrict__
         // past n start "at infinity"
         const uint64_t ro = r0 + l <= n ? rec_off[r0 + l] : ~0ull;
         const uint64_t so = r0 + l < n ? slot_off[r0 + l] : 0;
+        // deferred rows of the batch as a 64-bit lane mask (anyd only)
+        uint64_t dmask = anyd ? vw::ballot(r0 + l < n && (rec_size[r0 + l] & VCFCD_DEFER)) : 0ull;
         // rows that start before the tile ends; a tile over more than 63
         // rows (records of < 64 B on average) takes the rows in batches
         uint64_t base = r0;   // row of lane 0's values
@@ -2163,6 +2171,7 @@ __global__ __launch_bounds__(256) void k_compact_out(const uint8_t *__restrict__
         // records; empty rows -- failed lines -- start where the next begins)
         uint32_t idx[CTB], idx2[CTB];
         uint64_t st[CTB], en[CTB], sl[CTB];
+        uint32_t skm = 0;   // (anyd) bit k: every record touching block k is deferred
 #pragma unroll
         for (int k = 0; k < (int)CTB; k++) { idx[k] = 0; idx2[k] = 0; st[k] = 0; en[k] = 0; sl[k] = 0; }
         for (;;) {
@@ -2174,11 +2183,16 @@ __global__ __launch_bounds__(256) void k_compact_out(const uint8_t *__restrict__
                 const uint64_t ej = ((uint64_t)vw::readlane((uint32_t)(rov >> 32), j + 1) << 32) | vw::readlane((uint32_t)rov, j + 1);
                 const uint64_t sj = ((uint64_t)vw::readlane((uint32_t)(sov >> 32), j) << 32) | vw::readlane((uint32_t)sov, j);
                 const uint32_t ij = (uint32_t)(base - r0) + j;
+                const bool dj = (dmask >> j) & 1u;
 #pragma unroll
                 for (int k = 0; k < (int)CTB; k++) {
                     const uint64_t o = o0 + 16u * (l + 64u * k);
                     if (o >= rj) { idx[k] = ij; st[k] = rj; en[k] = ej; sl[k] = sj; }
                     if (o + 15 >= rj) idx2[k] = ij;
+                    if (anyd) {
+                        const uint32_t b = 1u << k;
+                        skm = o >= rj ? (dj ? skm | b : skm & ~b) : (o + 15 >= rj && !dj ? skm & ~b : skm);
+                    }
                 }
             }
             if (nr < 64) break;
@@ -2186,11 +2200,13 @@ __global__ __launch_bounds__(256) void k_compact_out(const uint8_t *__restrict__
             base += 63;
             rov = base + l <= n ? rec_off[base + l] : ~0ull;
             sov = base + l < n ? slot_off[base + l] : 0;
+            dmask = anyd ? vw::ballot(base + l < n && (rec_size[base + l] & VCFCD_DEFER)) : 0ull;
         }
 #pragma unroll
         for (int k = 0; k < (int)CTB; k++) {
             const uint64_t o = o0 + 16u * (l + 64u * k);
             if (o >= lim) continue;
+            if ((skm >> k) & 1u) continue;   // (k_encode_defer's bytes)
             const uint64_t r = r0 + idx[k];
             const uint64_t x = o - st[k];   // offset in the record
             const uint8_t *prim = prims + (r << pbs);
@@ -2527,7 +2543,8 @@ hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t s, hipEvent_t
     const uint64_t tiles = vcfc_record_bound(a.n, a.line_bytes_hint) / CT + 1;
     const uint64_t cblocks = tiles < 8192 ? (tiles + 3) / 4 : 2048;
     hipLaunchKernelGGL(k_compact_out, dim3((unsigned)cblocks), dim3(256), 0, s, a.prim, a.slots, a.slot_off,
-                       a.rec_off, a.n, a.tile_first, a.out, a.out_cap, a.prim_bytes, nullptr);
+                       a.rec_off, a.n, a.tile_first, a.out, a.out_cap, a.prim_bytes, nullptr, a.rec_size,
+                       a.defer_records ? a.defer_count : nullptr);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[4], s);
     // the deferred rows' records, straight into out (a resident grid; exits
@@ -2542,7 +2559,8 @@ hipError_t vcfc_encode_device(const VcfcEncodeArgs &a, hipStream_t s, hipEvent_t
         hipLaunchKernelGGL((k_scan_lb<2, true>), dim3((unsigned)nt), dim3(SCAN_THREADS), 0, s, a.rec_size, a.n,
                            tickets + 1, flags_b, a.rec_off, a.tile_first, a.out_cap, a.err, a.mispredict, a.nospace);
         hipLaunchKernelGGL(k_compact_out, dim3((unsigned)cblocks), dim3(256), 0, s, a.prim, a.slots, a.slot_off,
-                           a.rec_off, a.n, a.tile_first, a.out, a.out_cap, a.prim_bytes, a.mispredict);
+                           a.rec_off, a.n, a.tile_first, a.out, a.out_cap, a.prim_bytes, a.mispredict, a.rec_size,
+                           a.defer_count);
         hipLaunchKernelGGL(k_encode_defer<2>, dgrid, dim3(64 * K1_WAVES), 0, s, a);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
